@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Benchmark of the north-star hot path: SIF + closed-form MMB2 utterance embeddings.
+
+One *step* = one pass of the hot path over a batch of synthetic utterances
+already resident in HBM (BASELINE.json configs[3] shape: 40 tokens / frames per
+utterance, 3 modalities x 300-d, GloVe-sized V = 400k word table, Zipf(1.1)
+ids): for every utterance both its SIF text embedding (weighted average +
+first-PC removal, a1-a5) and its closed-form MMB2 embedding (a6-a8) are
+produced in device memory.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--utts-per-gpu U]
+
+N > 1 runs one process per GPU (torch.distributed.run, RCCL): each rank owns
+its own U utterances (weak scaling: fixed work per GPU) and the ranks
+all-reduce the 300x300 Gram once per step — the only collective on the path.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "multimodal-baselines_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def stream_kernel_bytes(L, D, A, Vd):
+    """Algorithmic HBM bytes per utterance of mmb_mm2_stream:
+    ids + gathered weights + gathered text rows + audio + visual frames (read),
+    weighted sum + frame sums + (count, sum w) (write)."""
+    return 4 * L + 4 * L + 4 * D * L + 4 * A * L + 4 * Vd * L + 4 * D + 4 * 2 * (D + A + Vd) + 8
+
+
+def path_bytes(L, D, A, Vd):
+    """SURVEY.md §8d B_utt for the whole step (149,120 B at the config-3 shape)."""
+    return 4 * L + 4 * L + 4 * D * L + 2 * 4 * A * L + 3 * 4 * D + 4 * D
+
+
+def cpu_baseline(inp, gen, n_sample):
+    """The oracle (CPU restatement of the reference loops + sklearn randomized SVD
+    + the MMB2 closed form in fp32 numpy) timed on a bounded sample of the same
+    workload, on this host's cores."""
+    import numpy as np
+
+    from oracle import mmb2_oracle as M
+    from oracle import sif_oracle as O
+
+    cores = len(os.sched_getaffinity(0))
+    n = n_sample
+    table = inp["table"].cpu().numpy()
+    wt = inp["wtab"].double().cpu().numpy()
+    ids = inp["ids"][:n].long().cpu().numpy()
+    audio = inp["audio"][:n].cpu().numpy()
+    visual = inp["visual"][:n].cpu().numpy()
+    params = M.params_from_module(gen)
+    t0 = time.perf_counter()
+    w = O.seq2weight_loop(ids, np.ones(ids.shape), wt)          # sif_functions.py:8-15
+    emb = O.get_weighted_average(table, ids, w)                  # :28-56
+    O.remove_pc(emb, 1)                                          # :58-81
+    text = table[ids]
+    M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual), params, w, text,
+                                      dtype=np.float32)          # sif2.py:164-208
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "utterance-embeds/s", "cores": cores, "kind": "port",
+            "sample": f"{n} utterances of the same workload (L=T={ids.shape[1]}, 3x300-d, "
+                      f"V={table.shape[0]}), one pass: oracle/ restatement (python row loops, "
+                      f"sklearn-equivalent randomized SVD, numpy BLAS on {cores} threads)",
+            "seconds": dt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--utts-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--tokens", type=int, default=40)
+    ap.add_argument("--vocab", type=int, default=400_000)
+    ap.add_argument("--cpu-sample", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import mmb_lib
+    import models
+    import pipeline as P
+    import synth
+
+    mmb_lib.require_gpu()
+    U, T, V, D = args.utts_per_gpu, args.tokens, args.vocab, 300
+    inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
+
+    def allreduce(t):
+        if world > 1:
+            dist.all_reduce(t)
+
+    step = P.FusedStep(inp, gen.networks(), allreduce=allreduce if world > 1 else None,
+                       n_total=U * world, row0=rank * U)
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step.run()
+    torch.cuda.synchronize()
+
+    # timed region: K steps, barrier + sync on both sides; HIP events on the
+    # launch stream around the dominant kernel (mm2_stream) of every step
+    E = lambda: torch.cuda.Event(enable_timing=True)
+    ev = [[E() for _ in range(7)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        e = ev[k]
+        e[0].record()
+        P.mm2_stream(step.n, step.t, step.d, step.a, step.vd, inp["audio"], inp["visual"],
+                     ids32=inp["ids"], table=inp["table"], wtab32=inp["wtab"], flag=step.flag,
+                     out=(step.num, step.s, step.aux))
+        e[1].record()
+        cnt = step.aux[0]
+        P.gram(step.num, cnt, step.G, ws=step.gws)
+        e[2].record()
+        allreduce(step.G)
+        e[3].record()
+        pc = P.pc_solve(step.G, step.z0, 1, False)
+        e[4].record()
+        P.remove_pc(step.num, cnt, pc, out=step.sif)
+        e[5].record()
+        step.proj.refresh()
+        P.mm2_project(step.s, step.num, step.aux, step.proj, out=step.mmb2)
+        e[6].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if int(step.flag.item()) != 0:
+        raise RuntimeError("id range flag set")
+
+    names = ["mm2_stream", "gram", "allreduce", "pc_solve", "pc_remove", "mm2_prepare+project"]
+    phase_ms = {n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps
+                for i, n in enumerate(names)}
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_utts = U * world * args.steps
+    value = total_utts / elapsed
+
+    if rank == 0:
+        kb = stream_kernel_bytes(T, D, 300, 300)
+        stream_s = phase_ms["mm2_stream"] / 1e3
+        achieved = kb * U / stream_s / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("utts_per_launch") == U and tj.get("tokens") == T:
+                traffic = tj.get("mm2_stream_hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "utt_stream_kernel (mmb_mm2_stream)",
+                "algorithmic_bytes_per_utt": kb, "utts_per_launch": U,
+                "avg_launch_ms": round(phase_ms["mm2_stream"], 4)}
+        pb = path_bytes(T, D, 300, 300)
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(inp, gen.cpu(), args.cpu_sample)
+            except Exception as exc:  # keep the GPU line even if the host leg fails
+                log(f"cpu baseline failed: {exc!r}")
+        out = {
+            "metric": "utterance-embeds/sec (MMB2, 3 modalities, 300d) at 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "utterance-embeds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded, generated in HBM; no dataset or checkpoint)",
+            "config": {"workload": "configs[3]: synthetic utterances x 40 tokens/frames x 3 "
+                                   "modalities x 300d, SIF(+PC removal) + closed-form MMB2",
+                       "utts_per_gpu": U, "tokens": T, "vocab": V, "dims": [D, 300, 300],
+                       "parallelism": f"dp{world} (utterance shards) + RCCL all-reduce of the "
+                                      f"300x300 fp64 Gram"},
+            "roofline": roof,
+            "path_roofline": {"bytes_per_utt": pb, "achieved": round(pb * U * world / (ms_per_step / 1e3) / world / 1e9, 1),
+                              "unit": "GB/s per GPU", "peak": HBM_PEAK_GBS},
+            "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,181 @@
+/*
+ * mmb.h — C ABI of libmmb.so, the MI355X (gfx950) SIF / MMB2 / regressor hot path.
+ *
+ * The reference (yaochie/multimodal-baselines) has no FFI: its boundary is a set
+ * of Python functions on numpy arrays / torch tensors.  Each entry point below
+ * replaces the arithmetic of one of those functions; the Python mirror in
+ * `multimodal-baselines_amd/` keeps the reference names and signatures and
+ * calls these through ctypes.
+ *
+ * Conventions:
+ *   - every pointer argument except host_* is DEVICE memory allocated by the
+ *     caller; the library never allocates or frees caller memory;
+ *   - all work is enqueued on `stream` and is asynchronous; no entry point
+ *     synchronises, so the calls can be captured into a hipGraph;
+ *   - row-major, contiguous layouts; ids are int32 (the caller narrows the
+ *     reference's int64 ids after a range check);
+ *   - return 0 on success, MMB_EINVAL (<0) on a bad argument or shape, or a
+ *     positive hipError_t from the launch;
+ *   - `flag` (nullable) is an int32 device word OR-ed with MMB_FLAG_* bits by
+ *     kernels that meet out-of-range ids (the shim raises IndexError, like
+ *     numpy would in the reference).
+ */
+#ifndef MMB_H_
+#define MMB_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMB_OK 0
+#define MMB_EINVAL (-1)
+#define MMB_FLAG_ID_RANGE 1
+
+/* Library version (major*10000 + minor*100 + patch). */
+int mmb_version(void);
+
+/* ---------------------------------------------------------------- a1
+ * seq2weight: w[i,j] = f32(wtab64[seq[i,j]]) if sel[i,j] (nullable = all) and
+ * seq[i,j] >= 0, else 0.  Bit-exact with the reference.
+ * replaces: sif_functions.seq2weight   /root/reference/sif_functions.py:8-15
+ *           sif.get_sentence_word_weights /root/reference/sif.py:78-82      */
+int mmb_seq2weight(const int32_t* seq, const uint8_t* sel, int64_t n, int64_t l,
+                   const double* wtab64, int64_t v, float* w_out, int32_t* flag,
+                   hipStream_t stream);
+
+/* ---------------------------------------------------------------- a1+a2
+ * Weighted average of gathered table rows per utterance:
+ *   num[i] = sum_j w[i,j] * table[ids[i,j]],  cnt[i] = count_nonzero(w[i,:]),
+ *   x[i]   = num[i] / cnt[i]                       (all float32)
+ * Weights come from `w` [n,l] when non-null (get_weighted_average), else from
+ * the f32 table `wtab32` gathered by id with id<0 -> 0 (a1 fused).
+ * Negative ids wrap like numpy (table[v+id]).  Outputs x/num/cnt are each
+ * nullable (at least one required).
+ * replaces: sif_functions.get_weighted_average /root/reference/sif_functions.py:28-56 */
+int mmb_sif_wavg(const float* table, int64_t v, int d, const int32_t* ids, int64_t n, int l,
+                 const float* w, const float* wtab32, float* x_out, float* num_out,
+                 float* cnt_out, int32_t* flag, hipStream_t stream);
+
+/* ---------------------------------------------------------------- a3 (Gram)
+ * g[d,d] (float64, full symmetric) = sum_i x_i x_i^T with x_i = num[i]/cnt[i]
+ * (cnt nullable -> x = num).  Products of f32 values are exact in f64 (fp64
+ * MFMA).  `ws` is scratch of mmb_gram_workspace_bytes(n, d) bytes.
+ * If accumulate != 0 the result is added to g (multi-split use).            */
+size_t mmb_gram_workspace_bytes(int64_t n, int d);
+int mmb_gram(const float* num, const float* cnt, int64_t n, int d, double* g, int accumulate,
+             void* ws, hipStream_t stream);
+
+/* z0[d,k] = X^T omega  (omega [n,k] float64) — start block of the transposed
+ * randomized-SVD branch (n < d).                                             */
+int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d, const double* omega,
+                 int k, double* z0, hipStream_t stream);
+
+/* ---------------------------------------------------------------- a3 (solve)
+ * Top-npc right singular vectors of X exactly as scikit-learn's
+ * TruncatedSVD(npc, n_iter, random_state=0) (randomized_svd, k = npc+10
+ * oversampled block, LU-normalised power iterations, svd_flip on components)
+ * computes them, evaluated from the Gram g alone: span(G^n_iter Z0) is the
+ * subspace the reference's iterations build, and the final SVD of Q^T X is
+ * solved as a k x k (generalised) symmetric eigenproblem.  One workgroup, fp64.
+ *   transposed = (n_total < d): z0 = X^T Omega_n, else z0 = Omega_d [d,k].
+ * pc_out [npc, d] float64.  d <= 512, k <= 16.
+ * replaces: sif_functions.compute_pc /root/reference/sif_functions.py:58-67 */
+int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n_iter,
+                 int transposed, double* pc_out, hipStream_t stream);
+
+/* ---------------------------------------------------------------- a4
+ * out[i] = x_i - sum_c (x_i . pc_c) pc_c   in float64, x_i = num[i]/cnt[i]
+ * (cnt nullable).  Exactly one of out32 / out64 non-null.
+ * replaces: sif_functions.remove_pc /root/reference/sif_functions.py:69-81 */
+int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int d, const double* pc,
+                  int npc, float* out32, double* out64, hipStream_t stream);
+
+/* Host helper: numpy RandomState(seed).normal(size=count) (MT19937 +
+ * legacy polar Box-Muller), written to host memory.  Used for the
+ * randomized-SVD start block Omega.                                          */
+int mmb_host_randn(uint32_t seed, int64_t count, double* host_out);
+
+/* ---------------------------------------------------------------- a7
+ * q_mean = (x-b)/exp(2 ls), q_sigma = (x-b)^2/exp(2 ls) - 1 over [n*t, f].
+ * replaces: sif2.calc_weights /root/reference/sif2.py:103-114               */
+int mmb_calc_weights(const float* x, int64_t rows, int f, const float* b_mean,
+                     const float* b_log_sigma, float* q_mean, float* q_sigma, hipStream_t stream);
+
+/* ---------------------------------------------------------------- a6+a7+a8 (stream)
+ * One pass over every utterance's text tokens and audio/visual frames.
+ * Text rows come from the table by id (ids non-null; wtab32 gives the weights)
+ * or from dense [n,t,d] tensors (ids null: text_dense for the modality sums,
+ * emb_dense for the weighted sum, w_dense [n,t] the sentence weights).
+ * Writes, per utterance i:
+ *   num[i,:d]  = sum_t w_t E_t                      (weighted text sum)
+ *   s[i,:]     = [Sx_e | Sxx_e | Sx_a | Sxx_a | Sx_v | Sxx_v | 0-pad]  (sum
+ *                over t of x and x^2 per feature; row stride mmb_mm2_k())
+ *   aux[0][i]  = count_nonzero(w), aux[1][i] = sum_t w_t   (planar [2][n]:
+ *                aux[0] is the SIF count the Gram / removal kernels take)
+ * replaces the frame loops of sif2.estimate_embedding_overall_gpu2
+ *   /root/reference/sif2.py:181-205 and the gathers at simplesif.py:862-871 */
+int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const float* wtab32,
+                   const float* text_dense, const float* emb_dense, const float* w_dense,
+                   const float* audio, const float* visual, int64_t n, int t, int d, int a,
+                   int vd, float* num_out, float* s_out, float* aux_out, int32_t* flag,
+                   hipStream_t stream);
+
+/* Padded width (row stride) of the per-utterance sums: roundup(2(d+a+vd), 32). */
+int mmb_mm2_k(int d, int a, int vd);
+
+/* Leading dimension of the merged projection: roundup(d+1, 64). */
+int mmb_mm2_ldw(int d);
+
+/* Merge the 6 combinations' (W_mu, b_mu, W_log_sigma, b_log_sigma) into
+ * wm [k, ldw] (ldw >= d+1; column d carries the total-weight row) and
+ * c0 [ldw] for frame count t.  Pointer arrays are HOST arrays of DEVICE
+ * pointers in key order audio, visual, audiovisual, textaudio, textvisual,
+ * textaudiovisual (sif2.py:167-174).                                         */
+int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_mu,
+                    const float* const* w_ls, const float* const* b_ls, int d, int a, int vd,
+                    int t, float* wm, int ldw, float* c0, hipStream_t stream);
+
+/* cs = (num + s @ wm[:, :d] + c0) / (aux[1] + s @ wm[:, d] + c0[d]);
+ * out = cs / ||cs||_2 (fp32 MFMA GEMM + fused epilogue).
+ * replaces: sif2.py:186-207                                                  */
+int mmb_mm2_project(const float* s, const float* num, const float* aux, const float* wm,
+                    int ldw, const float* c0, int64_t n, int k, int d, float* out,
+                    hipStream_t stream);
+
+/* ---------------------------------------------------------------- a10/a11
+ * SentimentModel(d -> h -> o): y = squeeze(W2 relu(W1 x + b1) + b2).
+ * Forward for rows idx[0..b) (idx nullable = 0..b) of latents [*, d].
+ * replaces: sentiment_model.SentimentModel.forward /root/reference/sentiment_model.py:36-41 */
+int mmb_mlp_forward(const float* latents, const int64_t* idx, int64_t b, int d, int h, int o,
+                    const float* w1, const float* b1, const float* w2, const float* b2,
+                    float* y_out, hipStream_t stream);
+
+/* L1 loss sum for prediction rows vs labels (per-batch means written to
+ * batch_loss): the evaluation loops of sentiment_model.py:60-74,117-125.
+ * Batches are consecutive slices of `perm` of size batch (last one ragged). */
+int mmb_mlp_eval(const float* latents, const float* labels, const int64_t* perm, int64_t n,
+                 int batch, int d, int h, int o, const float* w1, const float* b1,
+                 const float* w2, const float* b2, float* batch_loss, float* pred_out,
+                 hipStream_t stream);
+
+/* SGD training of the regressor over `n_steps` consecutive mini-batches drawn
+ * from `perm` (the DataLoader order, batches of `batch` rows, last one
+ * ragged, epochs concatenated: steps_per_epoch batches each), with
+ * loss = L1(reduction='none').mean() and p -= lr * grad, all in one launch of
+ * one workgroup.  Parameters are updated in place; per-step losses go to
+ * step_loss; ws is scratch of mmb_mlp_workspace_bytes(d, h) bytes (16-B aligned).
+ * replaces: sentiment_model.train_sentiment inner loop
+ *   /root/reference/sentiment_model.py:98-110                               */
+size_t mmb_mlp_workspace_bytes(int d, int h);
+int mmb_mlp_train(const float* latents, const float* labels, const int64_t* perm,
+                  int64_t n_per_epoch, int n_epochs, int batch, int d, int h, int o, float lr,
+                  float* w1, float* b1, float* w2, float* b2, float* step_loss, void* ws,
+                  hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMB_H_ */

@@ -1,0 +1,350 @@
+// Sentiment regressor (a10/a11): SentimentModel(d -> h -> o) forward, L1
+// backward and SGD, for MI355X.
+//
+// The reference trains with one PyTorch step per 32-row mini-batch
+// (sentiment_model.py:98-110): ~16 k tiny launches-worth of work per run.
+// Here a whole run of mini-batches is ONE launch of ONE workgroup (16 waves):
+// the parameters never leave the CU's L1/L2 and no host round trip sits
+// between steps.  W1 is kept as fp32-MFMA accumulator tiles of W1^T
+// (lane&31 = hidden unit, the 16 accumulator registers = 16 input features)
+// in an L2-resident tiled copy.  That layout is at once
+//   * the B operand of the forward  pre = X W1^T   (32x32x2, K = features, taken
+//     in the accumulator's register order — any K order is a valid sum), and
+//   * the C layout of the gradient  dW1^T = X^T dH (32x32x2, K = batch rows),
+// so the SGD update W1 -= lr dW1 is a lane-local FMA on the fragment with no
+// shuffles.  Each tile is owned by one wave for the whole run (its own
+// stores are re-read only by itself).  Bias, output layer and loss are VALU on LDS.
+#include "mmb_common.h"
+
+namespace mmb {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+constexpr int kMlpNT = 1024;
+constexpr int kMaxWaves = kMlpNT / kWave;
+constexpr int kBatchMax = 32;  // one MFMA M-tile of batch rows
+
+struct MlpArgs {
+  const float* lat;
+  const float* lab;
+  const int64_t* perm;
+  int64_t n_per_epoch;
+  int n_epochs, B, D, H, O;
+  float lr;
+  float* w1;
+  float* b1;
+  float* w2;
+  float* b2;
+  float* step_loss;
+  float* w1t;  // workspace: [nTh*nTd][64 lanes][16] tiled W1^T
+  // tiling
+  int nTh, nTd, G, DP, HP;
+};
+
+__device__ __forceinline__ int c_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+__device__ __forceinline__ f32x16 load_frag(const float* p) {
+  f32x16 v;
+  const float4* q = reinterpret_cast<const float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 x = q[i];
+    v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void store_frag(float* p, const f32x16& v) {
+  float4* q = reinterpret_cast<float4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+__global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
+  extern __shared__ float smem[];
+  const int DP = a.DP, HP = a.HP, O = a.O;
+  float* sx = smem;                                   // [32][DP+1]
+  float* spart = sx + kBatchMax * (DP + 1);           // [G][32][HP]  (aliased by sdh)
+  float* shid = spart + a.G * kBatchMax * HP;         // [32][HP]
+  float* sW2 = shid + kBatchMax * HP;                 // [O][HP]
+  float* sb1 = sW2 + O * HP;                          // [HP]
+  float* sb2 = sb1 + HP;                              // [O]
+  float* sg = sb2 + O;                                // [32][O]
+  float* sy = sg + kBatchMax * O;                     // [32][O]
+  float* s_red = sy + kBatchMax * O;                  // [kMaxWaves]
+  float* sdh = spart;                                 // [32][HP]
+  const int SX = DP + 1;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool mw = wave < a.nTh * a.G;
+  const int Th = mw ? wave % a.nTh : 0, grp = mw ? wave / a.nTh : 0;
+  const int tpg = (a.nTd + a.G - 1) / a.G;
+  const int td0 = grp * tpg;
+  const int ntiles = mw ? max(0, min(tpg, a.nTd - td0)) : 0;
+  const int hcol = 32 * Th + (lane & 31);
+  float* wt = a.w1t + (static_cast<int64_t>(Th) * a.nTd * kWave + lane) * 16;  // + td*64*16
+
+  // W1 -> tiled W1^T workspace (zero outside [H) x [D))
+  for (int64_t e = tid; e < static_cast<int64_t>(a.nTh) * a.nTd * kWave * 16; e += kMlpNT) {
+    const int r = static_cast<int>(e & 15), l = static_cast<int>((e >> 4) & 63);
+    const int64_t tile = e >> 10;
+    const int th = static_cast<int>(tile / a.nTd), td = static_cast<int>(tile % a.nTd);
+    const int h = 32 * th + (l & 31), d = 32 * td + c_row(r, l);
+    a.w1t[e] = (h < a.H && d < a.D) ? a.w1[static_cast<int64_t>(h) * a.D + d] : 0.f;
+  }
+  for (int e = tid; e < O * HP; e += kMlpNT) {
+    const int o = e / HP, h = e % HP;
+    sW2[e] = h < a.H ? a.w2[o * a.H + h] : 0.f;
+  }
+  for (int h = tid; h < HP; h += kMlpNT) sb1[h] = h < a.H ? a.b1[h] : 0.f;
+  for (int o = tid; o < O; o += kMlpNT) sb2[o] = a.b2[o];
+  __threadfence_block();
+  __syncthreads();
+
+  const int64_t spe = (a.n_per_epoch + a.B - 1) / a.B;
+  const int64_t nsteps = spe * a.n_epochs;
+  for (int64_t step = 0; step < nsteps; ++step) {
+    const int64_t ep = step / spe, bi = step % spe;
+    const int64_t base = ep * a.n_per_epoch + bi * a.B;
+    const int Bc = static_cast<int>(min<int64_t>(a.B, a.n_per_epoch - bi * a.B));
+    // 1. gather the batch rows (DataLoader order) into LDS
+    for (int e = tid; e < kBatchMax * DP; e += kMlpNT) {
+      const int b = e / DP, d = e % DP;
+      float v = 0.f;
+      if (b < Bc && d < a.D) v = a.lat[a.perm[base + b] * a.D + d];
+      sx[b * SX + d] = v;
+    }
+    for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
+      const int b = e / O, o = e % O;
+      sy[e] = (b < Bc) ? a.lab[a.perm[base + b] * O + o] : 0.f;
+    }
+    __syncthreads();
+    // 2. forward partials: pre[b][h] over this wave's feature tiles (MFMA)
+    if (mw) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const float* xb = sx + (lane & 31) * SX + 4 * (lane >> 5);
+      for (int t = 0; t < ntiles; ++t) {
+        const int td = td0 + t;
+        const f32x16 w = load_frag(wt + static_cast<int64_t>(td) * kWave * 16);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float xa = xb[32 * td + (r & 3) + 8 * (r >> 2)];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, w[r], acc, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) spart[(grp * kBatchMax + c_row(r, lane)) * HP + hcol] = acc[r];
+    }
+    __syncthreads();
+    // 3. hidden = relu(sum_g partial + b1)  (fixed group order)
+    for (int e = tid; e < kBatchMax * HP; e += kMlpNT) {
+      const int b = e / HP, h = e % HP;
+      float p = sb1[h];
+      for (int g = 0; g < a.G; ++g) p += spart[(g * kBatchMax + b) * HP + h];
+      shid[e] = (h < a.H && p > 0.f) ? p : 0.f;
+    }
+    __syncthreads();
+    // 4. output layer, L1 loss and its gradient (mean over Bc*O elements)
+    float lsum = 0.f;
+    for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
+      const int b = e / O, o = e % O;
+      float out = sb2[o];
+      for (int h = 0; h < a.H; ++h) out = fmaf(sW2[o * HP + h], shid[b * HP + h], out);
+      const float diff = out - sy[e];
+      const bool valid = b < Bc;
+      sg[e] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc * O) : 0.f;
+      if (valid) lsum += fabsf(diff);
+    }
+    lsum = wave_sum(lsum);
+    if (lane == 0) s_red[wave] = lsum;
+    __syncthreads();
+    // 5. dH = relu'(.) * g W2 ; then W2/b2 gradients (old W2 already consumed)
+    for (int e = tid; e < kBatchMax * HP; e += kMlpNT) {
+      const int b = e / HP, h = e % HP;
+      float s = 0.f;
+      if (shid[e] > 0.f)
+        for (int o = 0; o < O; ++o) s = fmaf(sg[b * O + o], sW2[o * HP + h], s);
+      sdh[e] = s;
+    }
+    __syncthreads();
+    // 6. dW1^T = X^T dH (MFMA, K = batch) and the SGD step on the owned tiles;
+    //    VALU updates of b1/W2/b2
+    if (mw) {
+      for (int t = 0; t < ntiles; ++t) {
+        const int td = td0 + t;
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < kBatchMax / 2; ++s) {
+          const int b = 2 * s + (lane >> 5);
+          const float xa = sx[b * SX + 32 * td + (lane & 31)];
+          const float db = sdh[b * HP + hcol];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, db, acc, 0, 0, 0);
+        }
+        float* p = wt + static_cast<int64_t>(td) * kWave * 16;
+        f32x16 w = load_frag(p);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w[r] = fmaf(-a.lr, acc[r], w[r]);
+        store_frag(p, w);
+      }
+    }
+    for (int e = tid; e < O * HP; e += kMlpNT) {
+      const int o = e / HP, h = e % HP;
+      if (h < a.H) {
+        float gsum = 0.f;
+        for (int b = 0; b < kBatchMax; ++b) gsum = fmaf(sg[b * O + o], shid[b * HP + h], gsum);
+        sW2[e] = fmaf(-a.lr, gsum, sW2[e]);
+      }
+    }
+    for (int h = tid; h < a.H; h += kMlpNT) {
+      float gsum = 0.f;
+      for (int b = 0; b < kBatchMax; ++b) gsum += sdh[b * HP + h];
+      sb1[h] = fmaf(-a.lr, gsum, sb1[h]);
+    }
+    for (int o = tid; o < O; o += kMlpNT) {
+      float gsum = 0.f;
+      for (int b = 0; b < kBatchMax; ++b) gsum += sg[b * O + o];
+      sb2[o] = fmaf(-a.lr, gsum, sb2[o]);
+    }
+    if (tid == 0) {
+      float l = 0.f;
+      for (int w = 0; w < kMaxWaves; ++w) l += s_red[w];
+      a.step_loss[step] = l / static_cast<float>(Bc * O);
+    }
+    __syncthreads();
+  }
+
+  // write the parameters back
+  __threadfence_block();
+  __syncthreads();
+  for (int64_t e = tid; e < static_cast<int64_t>(a.H) * a.D; e += kMlpNT) {
+    const int h = static_cast<int>(e / a.D), d = static_cast<int>(e % a.D);
+    const int th = h >> 5, td = d >> 5, dr = d & 31;
+    // invert c_row: dr = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    const int hl = (dr >> 2) & 1, r = (dr & 3) + 4 * (dr >> 3);
+    const int l = (h & 31) + 32 * hl;
+    a.w1[e] = a.w1t[((static_cast<int64_t>(th) * a.nTd + td) * kWave + l) * 16 + r];
+  }
+  for (int e = tid; e < O * a.H; e += kMlpNT) a.w2[e] = sW2[(e / a.H) * HP + e % a.H];
+  for (int h = tid; h < a.H; h += kMlpNT) a.b1[h] = sb1[h];
+  for (int o = tid; o < O; o += kMlpNT) a.b2[o] = sb2[o];
+}
+
+// Forward (+ optional L1 per batch) — one workgroup per batch of rows.
+__global__ __launch_bounds__(256) void mlp_eval_kernel(const float* __restrict__ lat,
+                                                       const float* __restrict__ lab,
+                                                       const int64_t* __restrict__ perm, int64_t n,
+                                                       int B, int D, int H, int O,
+                                                       const float* __restrict__ w1,
+                                                       const float* __restrict__ b1,
+                                                       const float* __restrict__ w2,
+                                                       const float* __restrict__ b2,
+                                                       float* __restrict__ batch_loss,
+                                                       float* __restrict__ pred) {
+  extern __shared__ float sm[];
+  float* sx = sm;          // [D]
+  float* shid = sx + D;    // [H]
+  __shared__ float s_red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * B;
+  const int Bc = static_cast<int>(min<int64_t>(B, n - b0));
+  float lsum = 0.f;
+  for (int bb = 0; bb < Bc; ++bb) {
+    const int64_t row = perm ? perm[b0 + bb] : (b0 + bb);
+    for (int d = tid; d < D; d += 256) sx[d] = lat[row * D + d];
+    __syncthreads();
+    for (int h = tid; h < H; h += 256) {
+      float p = b1[h];
+      for (int d = 0; d < D; ++d) p = fmaf(w1[static_cast<int64_t>(h) * D + d], sx[d], p);
+      shid[h] = p > 0.f ? p : 0.f;
+    }
+    __syncthreads();
+    for (int o = tid; o < O; o += 256) {
+      float out = b2[o];
+      for (int h = 0; h < H; ++h) out = fmaf(w2[o * H + h], shid[h], out);
+      if (pred) pred[(b0 + bb) * O + o] = out;
+      if (lab) lsum += fabsf(out - lab[row * O + o]);
+    }
+    __syncthreads();
+  }
+  lsum = wave_sum(lsum);
+  if (lane == 0) s_red[wave] = lsum;
+  __syncthreads();
+  if (tid == 0 && batch_loss) batch_loss[blockIdx.x] = (s_red[0] + s_red[1] + s_red[2] + s_red[3]) / static_cast<float>(Bc * O);
+}
+
+static int launch_train(const MlpArgs& a, size_t lds, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  mlp_train_kernel<<<1, kMlpNT, lds, stream>>>(a);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+}  // namespace mmb
+
+using namespace mmb;
+
+extern "C" int mmb_mlp_forward(const float* latents, const int64_t* idx, int64_t b, int d, int h,
+                               int o, const float* w1, const float* b1, const float* w2,
+                               const float* b2, float* y_out, hipStream_t stream) {
+  MMB_REQUIRE(latents && w1 && b1 && w2 && b2 && y_out && b >= 0 && d > 0 && h > 0 && o > 0);
+  if (b == 0) return MMB_OK;
+  const int B = 32;
+  mlp_eval_kernel<<<static_cast<int>(ceil_div(b, B)), 256, sizeof(float) * (d + h), stream>>>(
+      latents, nullptr, idx, b, B, d, h, o, w1, b1, w2, b2, nullptr, y_out);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_mlp_eval(const float* latents, const float* labels, const int64_t* perm,
+                            int64_t n, int batch, int d, int h, int o, const float* w1,
+                            const float* b1, const float* w2, const float* b2, float* batch_loss,
+                            float* pred_out, hipStream_t stream) {
+  MMB_REQUIRE(latents && labels && w1 && b1 && w2 && b2 && n >= 0 && batch > 0 && d > 0 && h > 0 && o > 0);
+  if (n == 0) return MMB_OK;
+  mlp_eval_kernel<<<static_cast<int>(ceil_div(n, batch)), 256, sizeof(float) * (d + h), stream>>>(
+      latents, labels, perm, n, batch, d, h, o, w1, b1, w2, b2, batch_loss, pred_out);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" size_t mmb_mlp_workspace_bytes(int d, int h) {
+  return static_cast<size_t>(ceil_div(h, 32)) * ceil_div(d, 32) * kWave * 16 * sizeof(float);
+}
+
+extern "C" int mmb_mlp_train(const float* latents, const float* labels, const int64_t* perm,
+                             int64_t n_per_epoch, int n_epochs, int batch, int d, int h, int o,
+                             float lr, float* w1, float* b1, float* w2, float* b2,
+                             float* step_loss, void* ws, hipStream_t stream) {
+  MMB_REQUIRE(latents && labels && perm && w1 && b1 && w2 && b2 && step_loss && ws);
+  MMB_REQUIRE(n_per_epoch > 0 && n_epochs >= 0 && batch >= 1 && batch <= kBatchMax);
+  MMB_REQUIRE(d > 0 && h > 0 && o >= 1 && o <= 32);
+  MMB_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0);
+  if (n_epochs == 0) return MMB_OK;
+  MlpArgs a{};
+  a.lat = latents; a.lab = labels; a.perm = perm; a.n_per_epoch = n_per_epoch;
+  a.n_epochs = n_epochs; a.B = batch; a.D = d; a.H = h; a.O = o; a.lr = lr;
+  a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.step_loss = step_loss;
+  a.w1t = static_cast<float*>(ws);
+  a.nTh = static_cast<int>(ceil_div(h, 32));
+  a.nTd = static_cast<int>(ceil_div(d, 32));
+  MMB_REQUIRE(a.nTh <= kMaxWaves);
+  a.G = kMaxWaves / a.nTh;
+  if (a.G > a.nTd) a.G = a.nTd;
+  a.DP = a.nTd * 32;
+  a.HP = a.nTh * 32;
+  const size_t lds = sizeof(float) * (static_cast<size_t>(kBatchMax) * (a.DP + 1) +
+                                      static_cast<size_t>(a.G) * kBatchMax * a.HP +
+                                      static_cast<size_t>(kBatchMax) * a.HP + o * a.HP + a.HP +
+                                      o + 2 * kBatchMax * o + kMaxWaves);
+  MMB_REQUIRE(lds <= 160 * 1024);
+  return launch_train(a, lds, stream);
+}

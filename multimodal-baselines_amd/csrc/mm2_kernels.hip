@@ -1,0 +1,288 @@
+// Closed-form MMB2 projection (a7/a8 after the frame sums) for MI355X.
+//
+// The reference (sif2.py:164-208) materialises q_mean/q_sigma [N,T,F_k] for
+// six modality combinations and runs twelve [N,T,F_k] x [F_k,300] matmuls
+// before summing over T.  Both q's are affine in the frame values, so the sum
+// over T commutes with them (exact algebra):
+//   sum_t q_mean_k  = a_k (Sx - T b_k)
+//   sum_t q_sigma_k = a_k (Sxx - 2 b_k Sx + T b_k^2) - T,   a_k = 1/exp(2 ls_k)
+// with Sx, Sxx the per-feature frame sums of each raw modality (streamed by
+// mmb_mm2_stream).  All twelve projections then fold into ONE merged matrix
+// Wm [2(d+a+vd), d+1] (column d accumulates the total weight, sif2.py:186-188)
+// and a constant c0 — a single [N,K] x [K,ldw] fp32-MFMA GEMM with the
+// division by the total weight and the row L2 normalisation (:207) fused into
+// its epilogue.
+#include "mmb_common.h"
+
+namespace mmb {
+
+struct PrepArgs {
+  const float* wmu[6];
+  const float* bmu[6];
+  const float* wls[6];
+  const float* bls[6];
+  int D, A, Vd, T, ldw, Kp;
+  float* wm;
+  float* c0;
+};
+
+// Offset of modality m (0 text, 1 audio, 2 visual) inside combination k's
+// feature vector (torch.cat order text, audio, visual), or -1.
+__host__ __device__ inline int combo_offset(int k, int m, int D, int A) {
+  // keys: 0 audio, 1 visual, 2 audiovisual, 3 textaudio, 4 textvisual, 5 textaudiovisual
+  switch (k) {
+    case 0: return m == 1 ? 0 : -1;
+    case 1: return m == 2 ? 0 : -1;
+    case 2: return m == 1 ? 0 : (m == 2 ? A : -1);
+    case 3: return m == 0 ? 0 : (m == 1 ? D : -1);
+    case 4: return m == 0 ? 0 : (m == 2 ? D : -1);
+    default: return m == 0 ? 0 : (m == 1 ? D : D + A);
+  }
+}
+
+__host__ __device__ inline int combo_width(int k, int D, int A, int Vd) {
+  switch (k) {
+    case 0: return A;
+    case 1: return Vd;
+    case 2: return A + Vd;
+    case 3: return D + A;
+    case 4: return D + Vd;
+    default: return D + A + Vd;
+  }
+}
+
+__global__ void mm2_prepare_wm_kernel(PrepArgs p) {
+  const int K = 2 * (p.D + p.A + p.Vd);
+  const int64_t total = static_cast<int64_t>(p.Kp) * p.ldw;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int r = static_cast<int>(e / p.ldw), j = static_cast<int>(e % p.ldw);
+    double acc = 0.0;
+    if (r < K && j <= p.D) {
+      // row r -> (modality m, kind sq, feature f)
+      int m, f, sq;
+      if (r < 2 * p.D) { m = 0; sq = r >= p.D; f = r - sq * p.D; }
+      else if (r < 2 * p.D + 2 * p.A) { m = 1; const int rr = r - 2 * p.D; sq = rr >= p.A; f = rr - sq * p.A; }
+      else { m = 2; const int rr = r - 2 * p.D - 2 * p.A; sq = rr >= p.Vd; f = rr - sq * p.Vd; }
+      for (int k = 0; k < 6; ++k) {
+        const int o = combo_offset(k, m, p.D, p.A);
+        if (o < 0) continue;
+        const int ff = o + f;
+        const double b = p.bmu[k][ff];
+        const double al = 1.0 / exp(2.0 * static_cast<double>(p.bls[k][ff]));
+        if (j < p.D) {
+          const double wmu = p.wmu[k][static_cast<int64_t>(ff) * p.D + j];
+          const double wls = p.wls[k][static_cast<int64_t>(ff) * p.D + j];
+          acc += sq ? al * wls : al * (wmu - 2.0 * b * wls);
+        } else {
+          acc += sq ? al : al * (1.0 - 2.0 * b);
+        }
+      }
+    }
+    p.wm[e] = static_cast<float>(acc);
+  }
+}
+
+// c0[j] = T * sum_k sum_f (-a b Wmu + a b^2 Wls - Wls)[f][j];  c0[d] = T * sum (-a b + a b^2 - 1)
+// Block: 64 columns x 16 feature groups; fixed-order combine (deterministic).
+__global__ __launch_bounds__(1024) void mm2_prepare_c0_kernel(PrepArgs p) {
+  __shared__ double s_part[16][64];
+  const int jl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + jl;
+  double acc = 0.0;
+  if (j <= p.D) {
+    for (int k = 0; k < 6; ++k) {
+      const int F = combo_width(k, p.D, p.A, p.Vd);
+      for (int f = g; f < F; f += 16) {
+        const double b = p.bmu[k][f];
+        const double al = 1.0 / exp(2.0 * static_cast<double>(p.bls[k][f]));
+        if (j < p.D) {
+          const double wmu = p.wmu[k][static_cast<int64_t>(f) * p.D + j];
+          const double wls = p.wls[k][static_cast<int64_t>(f) * p.D + j];
+          acc += -al * b * wmu + al * b * b * wls - wls;
+        } else {
+          acc += -al * b + al * b * b - 1.0;
+        }
+      }
+    }
+  }
+  s_part[g][jl] = acc;
+  __syncthreads();
+  if (g == 0 && j < p.ldw) {
+    double s = 0.0;
+    for (int q = 0; q < 16; ++q) s += s_part[q][jl];
+    p.c0[j] = (j <= p.D) ? static_cast<float>(s * p.T) : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ projection
+// fp32 MFMA 32x32x2: lane l holds A[l&31][l>>5] and B[l>>5][l&31];
+// C/D: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+constexpr int kPM = 64;   // rows per workgroup
+constexpr int kPK = 32;   // K chunk staged in LDS
+
+template <int CT>  // 32-wide column tiles per wave; ldw = 64*CT
+__global__ __launch_bounds__(256) void mm2_project_kernel(const float* __restrict__ S,
+                                                          const float* __restrict__ num,
+                                                          const float* __restrict__ aux,
+                                                          const float* __restrict__ Wm,
+                                                          const float* __restrict__ c0, int64_t N,
+                                                          int Kp, int D, float* __restrict__ out) {
+  constexpr int LDW = 64 * CT;
+  __shared__ float sA[kPM][kPK + 1];
+  __shared__ float sB[kPK][LDW];
+  __shared__ float s_tot[kPM];
+  __shared__ float s_ss[2][kPM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kPM;
+
+  f32x16 acc[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  for (int k0 = 0; k0 < Kp; k0 += kPK) {
+    // A tile 64 x 32 (float4 loads, 2 per thread)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + 256 * q;
+      const int row = idx >> 3, c4 = idx & 7;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n0 + row < N) v = *reinterpret_cast<const float4*>(S + (n0 + row) * Kp + k0 + c4 * 4);
+      sA[row][c4 * 4 + 0] = v.x;
+      sA[row][c4 * 4 + 1] = v.y;
+      sA[row][c4 * 4 + 2] = v.z;
+      sA[row][c4 * 4 + 3] = v.w;
+    }
+    // B tile 32 x LDW
+    for (int idx = tid; idx < kPK * LDW / 4; idx += 256) {
+      const int row = idx / (LDW / 4), c4 = idx % (LDW / 4);
+      *reinterpret_cast<float4*>(&sB[row][c4 * 4]) =
+          *reinterpret_cast<const float4*>(Wm + static_cast<int64_t>(k0 + row) * LDW + c4 * 4);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < kPK; kk += 2) {
+      const float a = sA[wr * 32 + (lane & 31)][kk + (lane >> 5)];
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const float b = sB[kk + (lane >> 5)][(wc * CT + t) * 32 + (lane & 31)];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: y = acc + (num | sum w) + c0; cs = y / total; out = cs / ||cs||
+  const int hl = lane >> 5, cl = lane & 31;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int col = (wc * CT + t) * 32 + cl;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const int64_t row = n0 + rl;
+      float add = 0.f;
+      if (row < N) {
+        if (col < D) add = num[row * D + col] + c0[col];
+        else if (col == D) add = aux[N + row] + c0[D];
+      }
+      acc[t][r] += add;
+      if (col == D) s_tot[rl] = acc[t][r];
+    }
+  }
+  __syncthreads();
+  float ss[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ss[r] = 0.f;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int col = (wc * CT + t) * 32 + cl;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float cs = acc[t][r] / s_tot[rl];
+      acc[t][r] = cs;
+      if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float s = half_sum(ss[r]);
+    if (cl == 0) s_ss[wc][wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    const int64_t row = n0 + rl;
+    const float nrm = sqrtf(s_ss[0][rl] + s_ss[1][rl]);
+    if (row < N) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 32 + cl;
+        if (col < D) out[row * D + col] = acc[t][r] / nrm;
+      }
+    }
+  }
+}
+
+template <int CT>
+static int launch_project(const float* s, const float* num, const float* aux, const float* wm,
+                          const float* c0, int64_t n, int kp, int d, float* out,
+                          hipStream_t stream) {
+  const int grid = static_cast<int>(ceil_div(n, kPM));
+  mm2_project_kernel<CT><<<grid, 256, 0, stream>>>(s, num, aux, wm, c0, n, kp, d, out);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+}  // namespace mmb
+
+using namespace mmb;
+
+extern "C" int mmb_mm2_ldw(int d) { return (d + 1 + 63) / 64 * 64; }
+
+extern "C" int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_mu,
+                               const float* const* w_ls, const float* const* b_ls, int d, int a,
+                               int vd, int t, float* wm, int ldw, float* c0, hipStream_t stream) {
+  MMB_REQUIRE(w_mu && b_mu && w_ls && b_ls && wm && c0 && d > 0 && a > 0 && vd > 0 && t > 0);
+  MMB_REQUIRE(ldw == mmb_mm2_ldw(d));
+  PrepArgs p{};
+  for (int k = 0; k < 6; ++k) {
+    MMB_REQUIRE(w_mu[k] && b_mu[k] && w_ls[k] && b_ls[k]);
+    p.wmu[k] = w_mu[k];
+    p.bmu[k] = b_mu[k];
+    p.wls[k] = w_ls[k];
+    p.bls[k] = b_ls[k];
+  }
+  p.D = d; p.A = a; p.Vd = vd; p.T = t; p.ldw = ldw; p.Kp = mmb_mm2_k(d, a, vd);
+  p.wm = wm; p.c0 = c0;
+  const int64_t total = static_cast<int64_t>(p.Kp) * ldw;
+  mm2_prepare_wm_kernel<<<static_cast<int>(std::min<int64_t>(ceil_div(total, 256), 4096)), 256, 0, stream>>>(p);
+  MMB_LAUNCH_CHECK();
+  mm2_prepare_c0_kernel<<<ldw / 64, 1024, 0, stream>>>(p);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_mm2_project(const float* s, const float* num, const float* aux,
+                               const float* wm, int ldw, const float* c0, int64_t n, int k,
+                               int d, float* out, hipStream_t stream) {
+  MMB_REQUIRE(s && num && aux && wm && c0 && out && n >= 0 && d > 0);
+  MMB_REQUIRE(ldw == mmb_mm2_ldw(d) && k % 32 == 0);
+  if (n == 0) return MMB_OK;
+  switch (ldw / 64) {
+    case 1: return launch_project<1>(s, num, aux, wm, c0, n, k, d, out, stream);
+    case 2: return launch_project<2>(s, num, aux, wm, c0, n, k, d, out, stream);
+    case 3: return launch_project<3>(s, num, aux, wm, c0, n, k, d, out, stream);
+    case 4: return launch_project<4>(s, num, aux, wm, c0, n, k, d, out, stream);
+    case 5: return launch_project<5>(s, num, aux, wm, c0, n, k, d, out, stream);
+    case 6: return launch_project<6>(s, num, aux, wm, c0, n, k, d, out, stream);
+    default: return MMB_EINVAL;
+  }
+}

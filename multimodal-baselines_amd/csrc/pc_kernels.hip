@@ -1,0 +1,593 @@
+// First-principal-component removal (a3/a4) for MI355X.
+//
+// The reference computes the PC with scikit-learn's randomized SVD
+// (TruncatedSVD(npc, n_iter=7, random_state=0), sif_functions.py:58-67), which
+// makes ~15 passes over X.  Here X is read ONCE for its 300x300 Gram
+// G = X^T X (fp64 MFMA: products of f32 values are exact in f64), the Gram is
+// the only thing that crosses GPUs (RCCL all-reduce, 720 KB), and the
+// randomized SVD is replayed on G in one workgroup:
+//   * direct branch (n >= d): Z0 = Omega [d,k] (RandomState(0).normal);
+//     span(G^n_iter Z0) is the span the reference's LU-normalised iterations
+//     build (LU/QR only right-multiply the block); the final SVD of Q^T X with
+//     Q = orth(X Z) reduces to the k x k generalised symmetric eigenproblem
+//     (Z^T G^2 Z) y = s^2 (Z^T G Z) y, v = G Z y;
+//   * transposed branch (n < d, extmath.py:562-566): Z0 = X^T Omega_n, the same
+//     iterations, then v = Z u with u the top eigenvector of Z^T G Z;
+//   * svd_flip(u_based_decision=False): largest-|.| entry of each component > 0.
+// The removal pass x - (x.pc) pc runs in f64 like the reference (:77-80).
+#include "mmb_common.h"
+
+namespace mmb {
+
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+
+constexpr int kGB = 64;  // Gram block edge per workgroup (4 waves x 32x32)
+
+__host__ __device__ inline int gram_pair_index(int bp, int bq, int nb) {
+  return bp * nb - bp * (bp - 1) / 2 + (bq - bp);
+}
+
+__device__ __forceinline__ float load_x(const float* __restrict__ num, const float* __restrict__ cnt,
+                                        int64_t row, int col, int D) {
+  if (col >= D) return 0.f;
+  const float v = num[row * D + col];
+  return cnt ? v / cnt[row] : v;  // x = num / count_nonzero(w), f32 (sif_functions.py:55)
+}
+
+// One workgroup: a 64x64 block (bp,bq), bp<=bq, of G over one chunk of rows.
+// fp64 MFMA 16x16x4: lane l holds A[l&15][l>>4] and B[l>>4][l&15]; with
+// A = X^T and B = X both fragments are 16 consecutive columns of 4 rows of X.
+__global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restrict__ num,
+                                                           const float* __restrict__ cnt,
+                                                           int64_t N, int D, int nb, int npairs,
+                                                           int S, int64_t chunk, int xcd_map,
+                                                           double* __restrict__ part) {
+  int pair, s;
+  if (xcd_map) {
+    // blocks b and b+8 share an XCD (round-robin dispatch; speed only): give
+    // every pair of one row chunk to one XCD so the chunk is fetched once per L2.
+    const int b = blockIdx.x, x = b & 7, local = b >> 3;
+    s = x + 8 * (local / npairs);
+    pair = local % npairs;
+  } else {
+    pair = blockIdx.x % npairs;
+    s = blockIdx.x / npairs;
+  }
+  int bp = 0, rem = pair;
+  while (rem >= nb - bp) {
+    rem -= nb - bp;
+    ++bp;
+  }
+  const int bq = bp + rem;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wp = wave >> 1, wq = wave & 1;
+  const int ca0 = bp * kGB + wp * 32 + (lane & 15), ca1 = ca0 + 16;
+  const int cb0 = bq * kGB + wq * 32 + (lane & 15), cb1 = cb0 + 16;
+  const int kr = lane >> 4;
+  const int64_t n0 = s * chunk;
+  const int64_t n1 = min(N, n0 + chunk);
+  f64x4 acc00 = {0, 0, 0, 0}, acc01 = acc00, acc10 = acc00, acc11 = acc00;
+#pragma unroll 4
+  for (int64_t n = n0; n < n1; n += 4) {
+    const int64_t row = n + kr;
+    double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    if (row < n1) {
+      a0 = load_x(num, cnt, row, ca0, D);
+      a1 = load_x(num, cnt, row, ca1, D);
+      b0 = load_x(num, cnt, row, cb0, D);
+      b1 = load_x(num, cnt, row, cb1, D);
+    }
+    acc00 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc00, 0, 0, 0);
+    acc01 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc01, 0, 0, 0);
+    acc10 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc10, 0, 0, 0);
+    acc11 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc11, 0, 0, 0);
+  }
+  // f64 C/D layout: col = lane&15, row = (lane>>4) + 4*reg
+  double* out = part + (static_cast<int64_t>(s) * npairs + pair) * (kGB * kGB);
+  const int c = lane & 15, r0 = lane >> 4;
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int i0 = wp * 32 + r0 + 4 * reg, j0 = wq * 32 + c;
+    out[i0 * kGB + j0] = acc00[reg];
+    out[i0 * kGB + j0 + 16] = acc01[reg];
+    out[(i0 + 16) * kGB + j0] = acc10[reg];
+    out[(i0 + 16) * kGB + j0 + 16] = acc11[reg];
+  }
+}
+
+// Fixed-order sum over the S row chunks (deterministic), mirrored to both halves.
+__global__ void gram_reduce_kernel(const double* __restrict__ part, int D, int nb, int npairs,
+                                   int S, int accumulate, double* __restrict__ g) {
+  const int64_t total = static_cast<int64_t>(D) * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int p = static_cast<int>(e / D), q = static_cast<int>(e % D);
+    int bp = p / kGB, bq = q / kGB, i = p % kGB, j = q % kGB;
+    if (bp > bq) {
+      int t = bp; bp = bq; bq = t;
+      t = i; i = j; j = t;
+    }
+    const int pair = gram_pair_index(bp, bq, nb);
+    double sum = 0.0;
+    for (int s = 0; s < S; ++s) sum += part[(static_cast<int64_t>(s) * npairs + pair) * (kGB * kGB) + i * kGB + j];
+    g[e] = accumulate ? g[e] + sum : sum;
+  }
+}
+
+__global__ void xt_omega_kernel(const float* __restrict__ num, const float* __restrict__ cnt,
+                                int64_t N, int D, const double* __restrict__ om, int k,
+                                double* __restrict__ z0) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= D * k) return;
+  const int p = e / k, j = e % k;
+  double acc = 0.0;
+  for (int64_t n = 0; n < N; ++n) acc += static_cast<double>(load_x(num, cnt, n, p, D)) * om[n * k + j];
+  z0[e] = acc;
+}
+
+// ------------------------------------------------------------------ pc_solve
+constexpr int kMaxD = 512;
+constexpr int kMaxK = 16;
+constexpr int kSolveNT = 1024;
+
+// Modified Gram-Schmidt, twice ("twice is enough"), on the columns of Z [D][k]
+// by one wave.  Lane l owns rows p = l (mod 64), so LDS needs no cross-lane
+// ordering; dot products travel through shuffles.
+__device__ void orth_wave(double* Z, int D, int k, int lane) {
+  for (int j = 0; j < k; ++j) {
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int i = 0; i < j; ++i) {
+        double d = 0.0;
+        for (int p = lane; p < D; p += kWave) d += Z[p * k + i] * Z[p * k + j];
+        d = wave_sum(d);
+        for (int p = lane; p < D; p += kWave) Z[p * k + j] -= d * Z[p * k + i];
+      }
+    }
+    double nn = 0.0;
+    for (int p = lane; p < D; p += kWave) nn += Z[p * k + j] * Z[p * k + j];
+    nn = wave_sum(nn);
+    const double inv = 1.0 / sqrt(nn);
+    for (int p = lane; p < D; p += kWave) Z[p * k + j] *= inv;
+  }
+}
+
+// GZ = G Z, thread p owns row p.  G symmetric: read column p (coalesced across p).
+__device__ void gz_product(const double* __restrict__ G, const double* Z, double* GZ, int D, int k) {
+  const int p = threadIdx.x;
+  if (p < D) {
+    double acc[kMaxK];
+#pragma unroll
+    for (int j = 0; j < kMaxK; ++j) acc[j] = 0.0;
+    for (int q = 0; q < D; ++q) {
+      const double gq = G[static_cast<int64_t>(q) * D + p];
+#pragma unroll
+      for (int j = 0; j < kMaxK; ++j)
+        if (j < k) acc[j] = fma(gq, Z[q * k + j], acc[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxK; ++j)
+      if (j < k) GZ[p * k + j] = acc[j];
+  }
+}
+
+// M[i][j] = sum_p X[p][i] Y[p][j] for the k x k block, all waves.
+__device__ void small_gram(const double* X, const double* Y, double* M, int D, int k) {
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+  for (int e = wave; e < k * k; e += kSolveNT / kWave) {
+    const int i = e / k, j = e % k;
+    double d = 0.0;
+    for (int p = lane; p < D; p += kWave) d += X[p * k + i] * Y[p * k + j];
+    d = wave_sum(d);
+    if (lane == 0) M[e] = d;
+  }
+}
+
+// Cyclic Jacobi on symmetric A [k][k] (LDS) by one wave; V <- eigenvectors (columns).
+__device__ void jacobi_wave(double* A, double* V, int k, int lane) {
+  for (int r = lane; r < k * k; r += kWave) V[r] = (r / k == r % k) ? 1.0 : 0.0;
+  wave_lds_sync();
+  for (int sweep = 0; sweep < 64; ++sweep) {
+    double off = 0.0, dia = 0.0;
+    for (int r = lane; r < k * k; r += kWave) {
+      const int i = r / k, j = r % k;
+      const double a = A[r];
+      if (i < j) off += a * a;
+      else if (i == j) dia += a * a;
+    }
+    off = wave_sum(off);
+    dia = wave_sum(dia);
+    if (off <= 1e-34 * dia) break;
+    for (int p = 0; p < k - 1; ++p) {
+      for (int q = p + 1; q < k; ++q) {
+        const double apq = A[p * k + q];
+        if (apq == 0.0) continue;
+        const double app = A[p * k + p], aqq = A[q * k + q];
+        const double theta = (aqq - app) / (2.0 * apq);
+        double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+        if (theta < 0.0) t = -t;
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        double arp = 0.0, arq = 0.0, vrp = 0.0, vrq = 0.0;
+        if (lane < k) {
+          arp = A[lane * k + p];
+          arq = A[lane * k + q];
+          vrp = V[lane * k + p];
+          vrq = V[lane * k + q];
+        }
+        wave_lds_sync();
+        if (lane < k) {
+          if (lane != p && lane != q) {
+            const double np_ = c * arp - s * arq, nq = s * arp + c * arq;
+            A[lane * k + p] = np_;
+            A[p * k + lane] = np_;
+            A[lane * k + q] = nq;
+            A[q * k + lane] = nq;
+          }
+          V[lane * k + p] = c * vrp - s * vrq;
+          V[lane * k + q] = s * vrp + c * vrq;
+        }
+        if (lane == 0) {
+          A[p * k + p] = app - t * apq;
+          A[q * k + q] = aqq + t * apq;
+          A[p * k + q] = 0.0;
+          A[q * k + p] = 0.0;
+        }
+        wave_lds_sync();
+      }
+    }
+  }
+}
+
+__device__ void symmetrize(double* M, int k) {
+  for (int e = threadIdx.x; e < k * k; e += blockDim.x) {
+    const int i = e / k, j = e % k;
+    if (i < j) {
+      const double m = 0.5 * (M[i * k + j] + M[j * k + i]);
+      M[i * k + j] = m;
+      M[j * k + i] = m;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __restrict__ G, int D,
+                                                            const double* __restrict__ z0, int k,
+                                                            int npc, int n_iter, int transposed,
+                                                            double* __restrict__ pc_out) {
+  __shared__ double sZ[kMaxD * kMaxK];
+  __shared__ double sGZ[kMaxD * kMaxK];
+  __shared__ double sA[kMaxK * kMaxK], sV[kMaxK * kMaxK], sW[kMaxK * kMaxK];
+  __shared__ double sL[kMaxK * kMaxK], sLi[kMaxK * kMaxK], sT[kMaxK * kMaxK];
+  __shared__ double sy[kMaxK], sv[kMaxD];
+  __shared__ double s_rd[kSolveNT / kWave];
+  __shared__ double s_rv[kSolveNT / kWave];
+  __shared__ int s_ri[kSolveNT / kWave];
+  __shared__ int s_order[kMaxK];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+
+  for (int e = tid; e < D * k; e += kSolveNT) sZ[e] = z0[e];
+  __syncthreads();
+  if (wave == 0) orth_wave(sZ, D, k, lane);
+  __syncthreads();
+  for (int it = 0; it < n_iter; ++it) {
+    gz_product(G, sZ, sGZ, D, k);
+    __syncthreads();
+    for (int e = tid; e < D * k; e += kSolveNT) sZ[e] = sGZ[e];
+    __syncthreads();
+    if (wave == 0) orth_wave(sZ, D, k, lane);
+    __syncthreads();
+  }
+  gz_product(G, sZ, sGZ, D, k);
+  __syncthreads();
+
+  if (transposed) {
+    small_gram(sZ, sGZ, sA, D, k);  // Q^T G Q
+    __syncthreads();
+    symmetrize(sA, k);
+    __syncthreads();
+  } else {
+    small_gram(sZ, sGZ, sW, D, k);   // W = Z^T G Z
+    small_gram(sGZ, sGZ, sT, D, k);  // H = (GZ)^T (GZ)
+    __syncthreads();
+    symmetrize(sW, k);
+    symmetrize(sT, k);
+    __syncthreads();
+    if (wave == 0) {
+      // Cholesky W = L L^T
+      for (int e = lane; e < k * k; e += kWave) sL[e] = 0.0;
+      wave_lds_sync();
+      for (int j = 0; j < k; ++j) {
+        if (lane == 0) {
+          double s = sW[j * k + j];
+          for (int m = 0; m < j; ++m) s -= sL[j * k + m] * sL[j * k + m];
+          sL[j * k + j] = sqrt(s);
+        }
+        wave_lds_sync();
+        if (lane > j && lane < k) {
+          double s = sW[lane * k + j];
+          for (int m = 0; m < j; ++m) s -= sL[lane * k + m] * sL[j * k + m];
+          sL[lane * k + j] = s / sL[j * k + j];
+        }
+        wave_lds_sync();
+      }
+      // Linv: lane c solves L x = e_c (column c)
+      if (lane < k) {
+        const int c = lane;
+        for (int i = 0; i < k; ++i) {
+          double s = (i == c) ? 1.0 : 0.0;
+          for (int m = c; m < i; ++m) s -= sL[i * k + m] * sLi[m * k + c];
+          sLi[i * k + c] = (i < c) ? 0.0 : s / sL[i * k + i];
+        }
+      }
+      wave_lds_sync();
+      // A = Linv H Linv^T
+      for (int e = lane; e < k * k; e += kWave) {
+        const int i = e / k, j = e % k;
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sLi[i * k + m] * sT[m * k + j];
+        sV[e] = s;  // scratch: Linv H
+      }
+      wave_lds_sync();
+      for (int e = lane; e < k * k; e += kWave) {
+        const int i = e / k, j = e % k;
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sV[i * k + m] * sLi[j * k + m];
+        sA[e] = s;
+      }
+      wave_lds_sync();
+      for (int e = lane; e < k * k; e += kWave) {
+        const int i = e / k, j = e % k;
+        if (i < j) {
+          const double m = 0.5 * (sA[i * k + j] + sA[j * k + i]);
+          sA[i * k + j] = m;
+          sA[j * k + i] = m;
+        }
+      }
+      wave_lds_sync();
+    }
+    __syncthreads();
+  }
+
+  if (wave == 0) {
+    jacobi_wave(sA, sV, k, lane);
+    if (lane == 0) {  // eigenvalues descending (selection; first max wins ties)
+      bool used[kMaxK];
+      for (int j = 0; j < k; ++j) used[j] = false;
+      for (int c = 0; c < k; ++c) {
+        int best = -1;
+        for (int j = 0; j < k; ++j)
+          if (!used[j] && (best < 0 || sA[j * k + j] > sA[best * k + best])) best = j;
+        used[best] = true;
+        s_order[c] = best;
+      }
+    }
+  }
+  __syncthreads();
+
+  for (int c = 0; c < npc; ++c) {
+    const int col = s_order[c];
+    if (!transposed) {
+      if (tid < k) {  // y = Linv^T u
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sLi[m * k + tid] * sV[m * k + col];
+        sy[tid] = s;
+      }
+      __syncthreads();
+    }
+    double v = 0.0;
+    if (tid < D) {
+      if (transposed) {
+        for (int j = 0; j < k; ++j) v += sZ[tid * k + j] * sV[j * k + col];
+      } else {
+        for (int j = 0; j < k; ++j) v += sGZ[tid * k + j] * sy[j];
+      }
+      sv[tid] = v;
+    }
+    // norm and first argmax |v|
+    double nn = wave_sum(v * v);
+    double best = (tid < D) ? fabs(v) : -1.0;
+    int bidx = (tid < D) ? tid : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best, o, kWave);
+      const int oi = __shfl_xor(bidx, o, kWave);
+      if (ob > best || (ob == best && oi < bidx)) {
+        best = ob;
+        bidx = oi;
+      }
+    }
+    if (lane == 0) {
+      s_rd[wave] = nn;
+      s_rv[wave] = best;
+      s_ri[wave] = bidx;
+    }
+    __syncthreads();
+    double tot = 0.0, bb = -1.0;
+    int bi = 0x7fffffff;
+    for (int w = 0; w < kSolveNT / kWave; ++w) {
+      tot += s_rd[w];
+      if (s_rv[w] > bb || (s_rv[w] == bb && s_ri[w] < bi)) {
+        bb = s_rv[w];
+        bi = s_ri[w];
+      }
+    }
+    const double scale = (sv[bi] < 0.0 ? -1.0 : 1.0) / sqrt(tot);
+    if (tid < D) pc_out[c * D + tid] = v * scale;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ pc_remove
+template <int VEC, int PER>
+__global__ __launch_bounds__(256) void pc_remove_kernel(const float* __restrict__ num,
+                                                        const float* __restrict__ cnt, int64_t N,
+                                                        int D, const double* __restrict__ pc,
+                                                        int npc, float* __restrict__ out32,
+                                                        double* __restrict__ out64) {
+  extern __shared__ double s_pc[];
+  for (int e = threadIdx.x; e < npc * D; e += blockDim.x) s_pc[e] = pc[e];
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int U = D / VEC;
+  const int64_t wstride = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + wave; row < N;
+       row += wstride) {
+    const float sc = cnt ? cnt[row] : 1.f;
+    double x[PER][VEC];
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+      const int u = lane + kWave * m;
+      float v[VEC];
+      if (u < U) {
+        if constexpr (VEC == 4) {
+          const float4 q = *reinterpret_cast<const float4*>(num + row * D + u * 4);
+          v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+          v[0] = num[row * D + u];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) v[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) x[m][e] = static_cast<double>(cnt ? v[e] / sc : v[e]);
+    }
+    double y[PER][VEC];
+#pragma unroll
+    for (int m = 0; m < PER; ++m)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) y[m][e] = 0.0;
+    for (int c = 0; c < npc; ++c) {
+      const double* pcc = s_pc + c * D;
+      double d = 0.0;
+#pragma unroll
+      for (int m = 0; m < PER; ++m) {
+        const int u = lane + kWave * m;
+        if (u < U) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) d = fma(x[m][e], pcc[u * VEC + e], d);
+        }
+      }
+      d = wave_sum(d);
+#pragma unroll
+      for (int m = 0; m < PER; ++m) {
+        const int u = lane + kWave * m;
+        if (u < U) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) y[m][e] = fma(d, pcc[u * VEC + e], y[m][e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+      const int u = lane + kWave * m;
+      if (u < U) {
+        if (out32) {
+          if constexpr (VEC == 4) {
+            float4 q;
+            q.x = static_cast<float>(x[m][0] - y[m][0]);
+            q.y = static_cast<float>(x[m][1] - y[m][1]);
+            q.z = static_cast<float>(x[m][2] - y[m][2]);
+            q.w = static_cast<float>(x[m][3] - y[m][3]);
+            *reinterpret_cast<float4*>(out32 + row * D + u * 4) = q;
+          } else {
+            out32[row * D + u] = static_cast<float>(x[m][0] - y[m][0]);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) out64[row * D + u * VEC + e] = x[m][e] - y[m][e];
+        }
+      }
+    }
+  }
+}
+
+template <int VEC, int PER>
+static int launch_remove(const float* num, const float* cnt, int64_t n, int d, const double* pc,
+                         int npc, float* out32, double* out64, hipStream_t stream) {
+  const int64_t waves = ceil_div(n, 1);
+  const int grid = static_cast<int>(std::min<int64_t>(ceil_div(waves, 4), 256 * 8));
+  pc_remove_kernel<VEC, PER><<<grid, 256, sizeof(double) * npc * d, stream>>>(num, cnt, n, d, pc, npc, out32, out64);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+struct GramPlan {
+  int nb, npairs, S, xcd;
+  int64_t chunk;
+};
+
+static GramPlan gram_plan(int64_t n, int d) {
+  GramPlan p;
+  p.nb = static_cast<int>(ceil_div(d, kGB));
+  p.npairs = p.nb * (p.nb + 1) / 2;
+  int64_t S = n / 4096;
+  if (S < 1) S = 1;
+  if (S > 128) S = 128;
+  if (S >= 8) S = S / 8 * 8;
+  p.S = static_cast<int>(S);
+  p.xcd = (p.S % 8 == 0) ? 1 : 0;
+  p.chunk = ceil_div(ceil_div(n, p.S), 4) * 4;
+  return p;
+}
+
+}  // namespace mmb
+
+using namespace mmb;
+
+extern "C" size_t mmb_gram_workspace_bytes(int64_t n, int d) {
+  const GramPlan p = gram_plan(n, d);
+  return static_cast<size_t>(p.S) * p.npairs * kGB * kGB * sizeof(double);
+}
+
+extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, double* g,
+                        int accumulate, void* ws, hipStream_t stream) {
+  MMB_REQUIRE(num && g && ws && n >= 0 && d > 0);
+  const GramPlan p = gram_plan(n, d);
+  double* part = static_cast<double*>(ws);
+  gram_partial_kernel<<<p.npairs * p.S, 256, 0, stream>>>(num, cnt, n, d, p.nb, p.npairs, p.S,
+                                                         p.chunk, p.xcd, part);
+  MMB_LAUNCH_CHECK();
+  const int64_t total = static_cast<int64_t>(d) * d;
+  gram_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, p.nb, p.npairs, p.S, accumulate, g);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d,
+                            const double* omega, int k, double* z0, hipStream_t stream) {
+  MMB_REQUIRE(num && omega && z0 && n >= 0 && d > 0 && k > 0);
+  xt_omega_kernel<<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n_iter,
+                            int transposed, double* pc_out, hipStream_t stream) {
+  MMB_REQUIRE(g && z0 && pc_out && d > 1 && d <= kMaxD && k >= 1 && k <= kMaxK);
+  MMB_REQUIRE(npc >= 1 && npc <= k && n_iter >= 0);
+  pc_solve_kernel<<<1, kSolveNT, 0, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int d,
+                             const double* pc, int npc, float* out32, double* out64,
+                             hipStream_t stream) {
+  MMB_REQUIRE(num && pc && n >= 0 && d > 0 && npc >= 1 && ((out32 != nullptr) != (out64 != nullptr)));
+  MMB_REQUIRE(static_cast<size_t>(npc) * d * sizeof(double) <= 64 * 1024);
+  if (n == 0) return MMB_OK;
+  const bool v4 = (d % 4 == 0) && ((reinterpret_cast<uintptr_t>(num) & 15) == 0) &&
+                  (out32 == nullptr || (reinterpret_cast<uintptr_t>(out32) & 15) == 0);
+  const int U = v4 ? d / 4 : d;
+  const int per = static_cast<int>(ceil_div(U, kWave));
+  if (v4) {
+    if (per <= 1) return launch_remove<4, 1>(num, cnt, n, d, pc, npc, out32, out64, stream);
+    if (per <= 2) return launch_remove<4, 2>(num, cnt, n, d, pc, npc, out32, out64, stream);
+    if (per <= 4) return launch_remove<4, 4>(num, cnt, n, d, pc, npc, out32, out64, stream);
+    if (per <= 8) return launch_remove<4, 8>(num, cnt, n, d, pc, npc, out32, out64, stream);
+  } else {
+    if (per <= 2) return launch_remove<1, 2>(num, cnt, n, d, pc, npc, out32, out64, stream);
+    if (per <= 4) return launch_remove<1, 4>(num, cnt, n, d, pc, npc, out32, out64, stream);
+    if (per <= 8) return launch_remove<1, 8>(num, cnt, n, d, pc, npc, out32, out64, stream);
+  }
+  return MMB_EINVAL;
+}

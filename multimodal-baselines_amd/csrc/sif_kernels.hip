@@ -1,0 +1,406 @@
+// SIF word-weight gather (a1), weighted gather-reduce (a2) and the fused
+// text+audio+visual per-utterance sums of the closed-form MMB2 (a6/a7/a8 stream).
+//
+// Design (MI355X): one workgroup of 320 threads (5 waves) owns one utterance at
+// a time (grid-stride over utterances).  A 300-wide f32 row is 75 float4 column
+// units; 4 row slots x 75 units = 300 active lanes, so every wave-instruction
+// issues 16 B/lane loads that cover contiguous 1 KiB runs of a frame row or a
+// gathered table row.  The utterance's token ids and weights are staged in LDS
+// (broadcast reads), the per-slot partial sums are combined through one LDS
+// image per accumulator in a fixed order (deterministic), and only the
+// reductions leave the chip: the [N,L,300] gathered text tensor the reference
+// materialises (simplesif.py:319-340, :871) never exists.
+#include "mmb_common.h"
+
+namespace mmb {
+
+constexpr int kNT = 320;              // threads per utterance workgroup
+constexpr int kTokChunk = 512;        // tokens staged per LDS chunk
+constexpr int kRedFloats = kNT * 4;   // one accumulator image: R*F <= NT*VEC
+
+struct StreamArgs {
+  const int32_t* ids;
+  const float* table;
+  int64_t V;
+  const float* wtab;        // f32 weight table (gather mode without w_dense)
+  const float* w_dense;     // [N,L] given weights
+  const float* text_dense;  // [N,L,D] dense text frames (MMB2 drop-in mode)
+  const float* emb_dense;   // [N,L,D] rows for the weighted sum (may alias text_dense)
+  const float* audio;       // [N,L,A]
+  const float* visual;      // [N,L,Vd]
+  int64_t N;
+  int L, D, A, Vd, Kp;
+  float* x_out;
+  float* num_out;
+  float* cnt_out;
+  float* s_out;
+  float* aux_out;
+  int32_t* flag;
+};
+
+template <int VEC>
+__device__ __forceinline__ void ldv(const float* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    v[0] = *p;
+  }
+}
+
+// Resolve token t of utterance i: element offset of its text row (or -1) and
+// its SIF weight.  Semantics of sif_functions.py:8-15 (weight gather, id<0 ->
+// 0) and numpy/torch fancy indexing for the row (negative ids wrap).
+__device__ __forceinline__ void stage_token(const StreamArgs& a, int64_t i, int t, int64_t& off,
+                                            float& w) {
+  const int64_t ft = i * a.L + t;
+  if (a.ids) {
+    int64_t id = a.ids[ft];
+    if (a.w_dense) {
+      w = a.w_dense[ft];
+    } else {
+      w = (id >= 0 && id < a.V) ? a.wtab[id] : 0.f;
+    }
+    if (id < 0) id += a.V;
+    if (id < 0 || id >= a.V) {
+      if (a.flag) atomicOr(a.flag, MMB_FLAG_ID_RANGE);
+      off = -1;
+      w = 0.f;
+    } else {
+      off = id * a.D;
+    }
+  } else {
+    w = a.w_dense ? a.w_dense[ft] : 0.f;
+    off = ft * a.D;
+  }
+}
+
+template <bool MM2, int VT, int VA, int VV>
+__global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
+  __shared__ int64_t s_off[kTokChunk];
+  __shared__ float s_w[kTokChunk];
+  __shared__ float s_red[(MM2 ? 4 : 1) * kRedFloats];
+  __shared__ float s_cnt[kNT / kWave], s_sw[kNT / kWave];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wave = tid / kWave;
+  // text lane map: CT column units of VT floats, RT row slots
+  const int CT = a.D / VT;
+  const int RT = kNT / CT;
+  const int rT = tid / CT, cT = tid - (tid / CT) * CT;
+  const bool actT = rT < RT;
+  // audio / visual lane maps
+  const int CA = MM2 ? a.A / VA : 1, RA = kNT / CA;
+  const int rA = tid / CA, cA = tid - rA * CA;
+  const int CV = MM2 ? a.Vd / VV : 1, RV = kNT / CV;
+  const int rV = tid / CV, cV = tid - rV * CV;
+  const float* tsrc = a.ids ? a.table : a.text_dense;
+  const float* esrc = a.ids ? a.table : a.emb_dense;
+  const bool split_emb = MM2 && (esrc != tsrc);
+
+  for (int64_t i = blockIdx.x; i < a.N; i += gridDim.x) {
+    float num[VT], sx[VT], sxx[VT];
+#pragma unroll
+    for (int e = 0; e < VT; ++e) num[e] = sx[e] = sxx[e] = 0.f;
+    float cntp = 0.f, swp = 0.f;
+
+    for (int t0 = 0; t0 < a.L; t0 += kTokChunk) {
+      const int tl = min(kTokChunk, a.L - t0);
+      for (int t = tid; t < tl; t += kNT) {
+        int64_t off;
+        float w;
+        stage_token(a, i, t0 + t, off, w);
+        s_off[t] = off;
+        s_w[t] = w;
+        cntp += (w != 0.f) ? 1.f : 0.f;
+        swp += w;
+      }
+      __syncthreads();
+      if (actT) {
+#pragma unroll 4
+        for (int t = rT; t < tl; t += RT) {
+          const float w = s_w[t];
+          const int64_t off = s_off[t];
+          if (off < 0 || (!MM2 && w == 0.f)) continue;
+          float v[VT];
+          ldv<VT>(tsrc + off + cT * VT, v);
+          if (split_emb) {
+            float u[VT];
+            ldv<VT>(esrc + off + cT * VT, u);
+#pragma unroll
+            for (int e = 0; e < VT; ++e) num[e] = fmaf(w, u[e], num[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < VT; ++e) num[e] = fmaf(w, v[e], num[e]);
+          }
+          if constexpr (MM2) {
+#pragma unroll
+            for (int e = 0; e < VT; ++e) {
+              sx[e] += v[e];
+              sxx[e] = fmaf(v[e], v[e], sxx[e]);
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+
+    // audio / visual frame sums (MMB2 only): sum_t x and sum_t x^2 per feature
+    float sa[VA], saa[VA], sv[VV], svv[VV];
+#pragma unroll
+    for (int e = 0; e < VA; ++e) sa[e] = saa[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < VV; ++e) sv[e] = svv[e] = 0.f;
+    if constexpr (MM2) {
+      if (rA < RA) {
+        const float* base = a.audio + (i * a.L) * a.A + cA * VA;
+#pragma unroll 4
+        for (int t = rA; t < a.L; t += RA) {
+          float v[VA];
+          ldv<VA>(base + static_cast<int64_t>(t) * a.A, v);
+#pragma unroll
+          for (int e = 0; e < VA; ++e) {
+            sa[e] += v[e];
+            saa[e] = fmaf(v[e], v[e], saa[e]);
+          }
+        }
+      }
+      if (rV < RV) {
+        const float* base = a.visual + (i * a.L) * a.Vd + cV * VV;
+#pragma unroll 4
+        for (int t = rV; t < a.L; t += RV) {
+          float v[VV];
+          ldv<VV>(base + static_cast<int64_t>(t) * a.Vd, v);
+#pragma unroll
+          for (int e = 0; e < VV; ++e) {
+            sv[e] += v[e];
+            svv[e] = fmaf(v[e], v[e], svv[e]);
+          }
+        }
+      }
+    }
+
+    // count_nonzero(w) and sum(w): wave shuffle then fixed-order wave sum
+    cntp = wave_sum(cntp);
+    swp = wave_sum(swp);
+    if (lane == 0) {
+      s_cnt[wave] = cntp;
+      s_sw[wave] = swp;
+    }
+    // round 1: text accumulators
+    if (actT) {
+#pragma unroll
+      for (int e = 0; e < VT; ++e) {
+        const int f = rT * a.D + cT * VT + e;
+        s_red[f] = num[e];
+        if constexpr (MM2) {
+          s_red[kRedFloats + f] = sx[e];
+          s_red[2 * kRedFloats + f] = sxx[e];
+        }
+      }
+    }
+    __syncthreads();
+    float cnt = 0.f, sw = 0.f;
+#pragma unroll
+    for (int w = 0; w < kNT / kWave; ++w) {
+      cnt += s_cnt[w];
+      sw += s_sw[w];
+    }
+    for (int f = tid; f < a.D; f += kNT) {
+      float n_ = 0.f;
+      for (int r = 0; r < RT; ++r) n_ += s_red[r * a.D + f];
+      if constexpr (MM2) {
+        float x1 = 0.f, x2 = 0.f;
+        for (int r = 0; r < RT; ++r) {
+          x1 += s_red[kRedFloats + r * a.D + f];
+          x2 += s_red[2 * kRedFloats + r * a.D + f];
+        }
+        a.num_out[i * a.D + f] = n_;
+        a.s_out[i * a.Kp + f] = x1;
+        a.s_out[i * a.Kp + a.D + f] = x2;
+      } else {
+        if (a.num_out) a.num_out[i * a.D + f] = n_;
+        if (a.x_out) a.x_out[i * a.D + f] = n_ / cnt;
+      }
+    }
+    if (tid == 0) {
+      if constexpr (MM2) {
+        a.aux_out[i] = cnt;         // planar [2][N]: row 0 doubles as the SIF count
+        a.aux_out[a.N + i] = sw;
+      } else {
+        if (a.cnt_out) a.cnt_out[i] = cnt;
+      }
+    }
+    if constexpr (MM2) {
+      __syncthreads();
+      // round 2: audio and visual accumulators
+      if (rA < RA) {
+#pragma unroll
+        for (int e = 0; e < VA; ++e) {
+          const int f = rA * a.A + cA * VA + e;
+          s_red[f] = sa[e];
+          s_red[kRedFloats + f] = saa[e];
+        }
+      }
+      if (rV < RV) {
+#pragma unroll
+        for (int e = 0; e < VV; ++e) {
+          const int f = rV * a.Vd + cV * VV + e;
+          s_red[2 * kRedFloats + f] = sv[e];
+          s_red[3 * kRedFloats + f] = svv[e];
+        }
+      }
+      __syncthreads();
+      float* srow = a.s_out + i * a.Kp + 2 * a.D;
+      for (int f = tid; f < a.A; f += kNT) {
+        float x1 = 0.f, x2 = 0.f;
+        for (int r = 0; r < RA; ++r) {
+          x1 += s_red[r * a.A + f];
+          x2 += s_red[kRedFloats + r * a.A + f];
+        }
+        srow[f] = x1;
+        srow[a.A + f] = x2;
+      }
+      for (int f = tid; f < a.Vd; f += kNT) {
+        float x1 = 0.f, x2 = 0.f;
+        for (int r = 0; r < RV; ++r) {
+          x1 += s_red[2 * kRedFloats + r * a.Vd + f];
+          x2 += s_red[3 * kRedFloats + r * a.Vd + f];
+        }
+        srow[2 * a.A + f] = x1;
+        srow[2 * a.A + a.Vd + f] = x2;
+      }
+      const int k = 2 * (a.D + a.A + a.Vd);
+      for (int f = k + tid; f < a.Kp; f += kNT) a.s_out[i * a.Kp + f] = 0.f;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void seq2weight_kernel(const int32_t* __restrict__ seq, const uint8_t* __restrict__ sel,
+                                  int64_t total, const double* __restrict__ wtab, int64_t V,
+                                  float* __restrict__ w, int32_t* flag) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t id = seq[k];
+    float out = 0.f;
+    if ((sel == nullptr || sel[k]) && id >= 0) {
+      if (id < V) {
+        out = static_cast<float>(wtab[id]);  // f64 -> f32, round to nearest (sif_functions.py:13)
+      } else if (flag) {
+        atomicOr(flag, MMB_FLAG_ID_RANGE);
+      }
+    }
+    w[k] = out;
+  }
+}
+
+__global__ void calc_weights_kernel(const float* __restrict__ x, int64_t total, int F,
+                                    const float* __restrict__ bm, const float* __restrict__ bl,
+                                    float* __restrict__ qm, float* __restrict__ qs) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int f = static_cast<int>(k % F);
+    const float d = x[k] - bm[f];
+    const float e = expf(2.f * bl[f]);
+    qm[k] = d / e;
+    qs[k] = d * d / e - 1.f;
+  }
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <bool MM2, int VT, int VA, int VV>
+static int launch_stream(const StreamArgs& a, hipStream_t stream) {
+  const int grid = stream_grid(a.N, 6);
+  utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+}  // namespace mmb
+
+using namespace mmb;
+
+extern "C" int mmb_version(void) { return 100; }
+
+extern "C" int mmb_seq2weight(const int32_t* seq, const uint8_t* sel, int64_t n, int64_t l,
+                              const double* wtab64, int64_t v, float* w_out, int32_t* flag,
+                              hipStream_t stream) {
+  MMB_REQUIRE(n >= 0 && l >= 0 && v > 0 && seq && wtab64 && w_out);
+  const int64_t total = n * l;
+  if (total == 0) return MMB_OK;
+  const int grid = static_cast<int>(std::min<int64_t>(ceil_div(total, 256), 256 * 16));
+  seq2weight_kernel<<<grid, 256, 0, stream>>>(seq, sel, total, wtab64, v, w_out, flag);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_sif_wavg(const float* table, int64_t v, int d, const int32_t* ids, int64_t n,
+                            int l, const float* w, const float* wtab32, float* x_out,
+                            float* num_out, float* cnt_out, int32_t* flag, hipStream_t stream) {
+  MMB_REQUIRE(table && ids && v > 0 && d > 0 && n >= 0 && l >= 0);
+  MMB_REQUIRE(w || wtab32);
+  MMB_REQUIRE(x_out || num_out || cnt_out);
+  if (n == 0) return MMB_OK;
+  StreamArgs a{};
+  a.ids = ids; a.table = table; a.V = v; a.wtab = wtab32; a.w_dense = w;
+  a.N = n; a.L = l; a.D = d;
+  a.x_out = x_out; a.num_out = num_out; a.cnt_out = cnt_out; a.flag = flag;
+  const bool v4 = (d % 4 == 0) && aligned16(table);
+  MMB_REQUIRE(d / (v4 ? 4 : 1) <= kNT && d <= kRedFloats);
+  return v4 ? launch_stream<false, 4, 1, 1>(a, stream) : launch_stream<false, 1, 1, 1>(a, stream);
+}
+
+extern "C" int mmb_calc_weights(const float* x, int64_t rows, int f, const float* b_mean,
+                                const float* b_log_sigma, float* q_mean, float* q_sigma,
+                                hipStream_t stream) {
+  MMB_REQUIRE(x && b_mean && b_log_sigma && q_mean && q_sigma && rows >= 0 && f > 0);
+  const int64_t total = rows * f;
+  if (total == 0) return MMB_OK;
+  const int grid = static_cast<int>(std::min<int64_t>(ceil_div(total, 256), 256 * 16));
+  calc_weights_kernel<<<grid, 256, 0, stream>>>(x, total, f, b_mean, b_log_sigma, q_mean, q_sigma);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_mm2_k(int d, int a, int vd) {
+  const int k = 2 * (d + a + vd);
+  return (k + 31) / 32 * 32;
+}
+
+extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
+                              const float* wtab32, const float* text_dense,
+                              const float* emb_dense, const float* w_dense, const float* audio,
+                              const float* visual, int64_t n, int t, int d, int a_, int vd,
+                              float* num_out, float* s_out, float* aux_out, int32_t* flag,
+                              hipStream_t stream) {
+  MMB_REQUIRE(n >= 0 && t > 0 && d > 0 && a_ > 0 && vd > 0);
+  MMB_REQUIRE(audio && visual && num_out && s_out && aux_out);
+  if (ids) {
+    MMB_REQUIRE(table && v > 0 && (wtab32 || w_dense));
+  } else {
+    MMB_REQUIRE(text_dense && emb_dense && w_dense);
+  }
+  if (n == 0) return MMB_OK;
+  StreamArgs s{};
+  s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.w_dense = w_dense;
+  s.text_dense = text_dense; s.emb_dense = emb_dense; s.audio = audio; s.visual = visual;
+  s.N = n; s.L = t; s.D = d; s.A = a_; s.Vd = vd; s.Kp = mmb_mm2_k(d, a_, vd);
+  s.num_out = num_out; s.s_out = s_out; s.aux_out = aux_out; s.flag = flag;
+  const bool vt = (d % 4 == 0) && (ids ? aligned16(table) : (aligned16(text_dense) && aligned16(emb_dense)));
+  const bool va = (a_ % 4 == 0) && aligned16(audio);
+  const bool vv = (vd % 4 == 0) && aligned16(visual);
+  MMB_REQUIRE(d / (vt ? 4 : 1) <= kNT && a_ / (va ? 4 : 1) <= kNT && vd / (vv ? 4 : 1) <= kNT);
+  const int sel = (vt ? 4 : 0) | (va ? 2 : 0) | (vv ? 1 : 0);
+  switch (sel) {
+    case 7: return launch_stream<true, 4, 4, 4>(s, stream);
+    case 6: return launch_stream<true, 4, 4, 1>(s, stream);
+    case 5: return launch_stream<true, 4, 1, 4>(s, stream);
+    case 4: return launch_stream<true, 4, 1, 1>(s, stream);
+    case 3: return launch_stream<true, 1, 4, 4>(s, stream);
+    case 2: return launch_stream<true, 1, 4, 1>(s, stream);
+    case 1: return launch_stream<true, 1, 1, 4>(s, stream);
+    default: return launch_stream<true, 1, 1, 1>(s, stream);
+  }
+}

@@ -1,0 +1,119 @@
+"""ctypes binding of libmmb.so (the C ABI declared in include/mmb.h).
+
+torch is imported first on purpose: torch ships its own HIP runtime with the
+same soname (libamdhip64.so.7) as /opt/rocm's, so loading libmmb.so after
+torch makes it bind to the runtime torch already initialised — one HIP
+runtime per process, and torch-allocated device pointers / torch streams are
+valid inside libmmb.
+
+There is no fallback: if libmmb.so is missing or no GPU is visible, every
+entry point raises.  (Build it with `python -c "import __graft_entry__ as g;
+g.build()"` or `make -C multimodal-baselines_amd/csrc`.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmmb.so")
+
+MMB_FLAG_ID_RANGE = 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_F = ctypes.c_float
+_S = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "mmb_version": (_I, []),
+    "mmb_seq2weight": (_I, [_P, _P, _L, _L, _P, _L, _P, _P, _P]),
+    "mmb_sif_wavg": (_I, [_P, _L, _I, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_gram_workspace_bytes": (_S, [_L, _I]),
+    "mmb_gram": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
+    "mmb_xt_omega": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
+    "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
+    "mmb_pc_remove": (_I, [_P, _P, _L, _I, _P, _I, _P, _P, _P]),
+    "mmb_host_randn": (_I, [ctypes.c_uint32, _L, _P]),
+    "mmb_calc_weights": (_I, [_P, _L, _I, _P, _P, _P, _P, _P]),
+    "mmb_mm2_k": (_I, [_I, _I, _I]),
+    "mmb_mm2_ldw": (_I, [_I]),
+    "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P,
+                            _P, _P]),
+    "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
+    "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
+    "mmb_mlp_forward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "mmb_mlp_eval": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_mlp_workspace_bytes": (_S, [_I, _I]),
+    "mmb_mlp_train": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+class MMBError(RuntimeError):
+    pass
+
+
+def load():
+    """dlopen libmmb.so once (no GPU needed to load or query symbols)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libmmb.so not built at {LIB_PATH}; run `make -C "
+                              f"{os.path.join(HERE, 'csrc')}` or __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise MMBError(f"{name} failed with code {rc}" + (" (invalid argument)" if rc < 0 else
+                                                            " (hipError)"))
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def require_gpu() -> torch.device:
+    if not torch.cuda.is_available():
+        raise MMBError("libmmb computes on an MI355X (gfx950) GPU and has no CPU fallback; "
+                       "no GPU is visible")
+    load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise MMBError("libmmb entry points take device tensors")
+    if not t.is_contiguous():
+        raise MMBError("libmmb entry points take contiguous tensors")
+    return t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def host_randn(seed: int, count: int):
+    """numpy RandomState(seed).normal(size=count), from the C++ MT19937 in libmmb."""
+    import numpy as np
+
+    out = np.empty(count, dtype=np.float64)
+    call("mmb_host_randn", seed, count, out.ctypes.data if count else None)
+    return out

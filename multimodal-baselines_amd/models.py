@@ -1,0 +1,83 @@
+"""Parameter layout of the MMB generators (consumed by the closed-form MMB2 path).
+
+Mirrors the *parameter layout* of `models.AudioVisualGeneratorMultimodal`
+(`/root/reference/models.py:107-202`): a ModuleDict keyed by modality
+combination, each holding ``{'mu', 'log_sigma'}: nn.Linear(D, F_k)``.  The
+closed-form estimate (`sif2.py:164-208`) reads only ``.weight [F_k, D]`` and
+``.bias [F_k]`` of those layers.  Construction order matches the reference so
+``torch.manual_seed(s)`` reproduces the reference's initial weights bit for bit.
+
+The generator *forward* (latent-optimisation objective) is a next row
+(SURVEY.md §8f row 1); it is provided here only as plain torch for the CLI's
+bookkeeping and is not on the accelerated path.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+# fixed key order of sif2.py:167-174 (also the ModuleDict order, models.py:134-159)
+MMB2_KEYS = ("audio", "visual", "audiovisual", "textaudio", "textvisual", "textaudiovisual")
+MMB1_KEYS = ("audio", "visual")
+
+
+def combo_dims(key: str, D: int, A: int, Vd: int) -> list[tuple[str, int]]:
+    """Segments (modality, width) that make up combination ``key``'s features.
+
+    Order is the torch.cat order used by the callers (simplesif.py:825-830):
+    text first, then audio, then visual.
+    """
+    segs = []
+    if key.startswith("text"):
+        segs.append(("text", D))
+    if "audio" in key:
+        segs.append(("audio", A))
+    if "visual" in key:
+        segs.append(("visual", Vd))
+    return segs
+
+
+class AudioVisualGeneratorMultimodal(nn.Module):
+    def __init__(self, embedding_dim, audio_dim, visual_dim, norm=None, frozen_weights=True,
+                 unimodal=False):
+        super().__init__()
+        self.embedding = None
+        self.embedding_dim = embedding_dim
+        keys = MMB1_KEYS if unimodal else MMB2_KEYS
+        layers = {}
+        for k in keys:
+            width = sum(w for _, w in combo_dims(k, embedding_dim, audio_dim, visual_dim))
+            layers[k] = nn.ModuleDict({
+                "mu": nn.Linear(embedding_dim, width),
+                "log_sigma": nn.Linear(embedding_dim, width),
+            })
+        self.embed2out = nn.ModuleDict(layers)
+        if norm is None:
+            self.norm = None
+        elif norm == "layer_norm":
+            self.norm = nn.LayerNorm(embedding_dim)
+        elif norm == "batch_norm":
+            self.norm = nn.BatchNorm1d(embedding_dim)
+        else:
+            raise NotImplementedError
+        if frozen_weights:
+            self.freeze_weights()
+
+    def freeze_weights(self):
+        for p in self.embed2out.parameters():
+            p.requires_grad = False
+
+    def init_embedding(self, embedding):
+        assert embedding.size()[-1] == self.embedding_dim
+        self.embedding = embedding
+        self.embedding.requires_grad = True
+        self.embedding_dim = self.embedding.size()[-1]
+
+    def forward(self, embeddings):
+        x = self.norm(embeddings) if self.norm is not None else embeddings
+        return {k: {"mu": m["mu"](x), "sigma": m["log_sigma"](x).exp()}
+                for k, m in self.embed2out.items()}
+
+    def networks(self):
+        """``{key: (mu_linear, log_sigma_linear)}`` as built at simplesif.py:853-856."""
+        return {k: (m["mu"], m["log_sigma"]) for k, m in self.embed2out.items()}

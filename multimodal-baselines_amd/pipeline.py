@@ -1,0 +1,307 @@
+"""Device-resident hot path: SIF (a1-a5) and closed-form MMB2 (a6-a8) on HBM tensors.
+
+Every function here takes and returns torch device tensors and calls libmmb
+through its C ABI on the current stream; nothing is synchronised.  The
+reference-signature mirrors (`sif_functions.py`, `sif.py`, `sif2.py`) and
+`bench.py` are thin layers over these.
+
+Data layout in HBM (one utterance per row, row-major, fp32 unless noted):
+  table [V, D], wtab [V] (f32 rounding of the f64 SIF weights), ids [N, L] int32,
+  audio [N, T, A], visual [N, T, Vd]                                  (inputs)
+  num [N, D]   weighted text sum           s [N, Kp] frame sums       aux [2, N]
+  G [D, D] f64 Gram   pc [npc, D] f64                                  (intermediates)
+  sif [N, D] (f32 or f64)   mmb2 [N, D]                               (outputs)
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import mmb_lib as L
+from models import MMB2_KEYS
+
+N_OVERSAMPLES = 10  # sklearn randomized_svd default (extmath.py:535)
+N_ITER = 7          # TruncatedSVD(n_iter=7), sif_functions.py:65
+PC_SEED = 0         # random_state=0, sif_functions.py:65
+
+_omega_cache: dict = {}
+
+
+def omega(rows: int, k: int, device) -> torch.Tensor:
+    """RandomState(0).normal(size=(rows, k)) as f64 on `device` (cached)."""
+    key = (rows, k, str(device))
+    t = _omega_cache.get(key)
+    if t is None:
+        host = L.host_randn(PC_SEED, rows * k).reshape(rows, k)
+        t = torch.from_numpy(host).to(device)
+        if len(_omega_cache) > 16:
+            _omega_cache.clear()
+        _omega_cache[key] = t
+    return t
+
+
+def narrow_ids(ids: torch.Tensor) -> torch.Tensor:
+    """int64 reference ids -> int32 device ids (range-checked)."""
+    if ids.dtype == torch.int32:
+        return ids.contiguous()
+    if ids.numel():
+        lo, hi = int(ids.min()), int(ids.max())
+        if lo < -(2 ** 31) or hi >= 2 ** 31:
+            raise IndexError("token id out of int32 range")
+    return ids.to(torch.int32).contiguous()
+
+
+def check_flag(flag: torch.Tensor, V: int):
+    if int(flag.item()) & L.MMB_FLAG_ID_RANGE:
+        raise IndexError(f"token id out of bounds for a vocabulary of size {V}")
+
+
+# ------------------------------------------------------------------ a1
+def seq2weight(seq32: torch.Tensor, sel: torch.Tensor | None, wtab64: torch.Tensor,
+               flag: torch.Tensor | None = None) -> torch.Tensor:
+    n, l = seq32.shape
+    w = torch.empty((n, l), dtype=torch.float32, device=seq32.device)
+    L.call("mmb_seq2weight", L.ptr(seq32), L.ptr(sel), n, l, L.ptr(wtab64), wtab64.numel(),
+           L.ptr(w), L.ptr(flag), L.stream_ptr())
+    return w
+
+
+# ------------------------------------------------------------------ a1+a2
+def weighted_sum(table: torch.Tensor, ids32: torch.Tensor, w: torch.Tensor | None = None,
+                 wtab32: torch.Tensor | None = None, flag: torch.Tensor | None = None,
+                 x_out: bool = False):
+    """Returns (num [N,D], cnt [N]) or x [N,D] (= num/cnt) if x_out."""
+    n, l = ids32.shape
+    V, D = table.shape
+    dev = table.device
+    if x_out:
+        x = torch.empty((n, D), dtype=torch.float32, device=dev)
+        L.call("mmb_sif_wavg", L.ptr(table), V, D, L.ptr(ids32), n, l, L.ptr(w), L.ptr(wtab32),
+               L.ptr(x), None, None, L.ptr(flag), L.stream_ptr())
+        return x
+    num = torch.empty((n, D), dtype=torch.float32, device=dev)
+    cnt = torch.empty((n,), dtype=torch.float32, device=dev)
+    L.call("mmb_sif_wavg", L.ptr(table), V, D, L.ptr(ids32), n, l, L.ptr(w), L.ptr(wtab32),
+           None, L.ptr(num), L.ptr(cnt), L.ptr(flag), L.stream_ptr())
+    return num, cnt
+
+
+# ------------------------------------------------------------------ a3
+class GramWorkspace:
+    """Scratch for mmb_gram sized for up to `n` rows (re-used across calls)."""
+
+    def __init__(self, n: int, d: int, device):
+        nbytes = L.query("mmb_gram_workspace_bytes", n, d)
+        self.buf = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=device)
+        self.n, self.d = n, d
+
+    def fits(self, n, d):
+        return L.query("mmb_gram_workspace_bytes", n, d) <= self.buf.numel()
+
+
+def gram(num: torch.Tensor, cnt: torch.Tensor | None, G: torch.Tensor | None = None,
+         accumulate: bool = False, ws: GramWorkspace | None = None) -> torch.Tensor:
+    n, d = num.shape
+    if G is None:
+        G = torch.empty((d, d), dtype=torch.float64, device=num.device)
+    if ws is None or not ws.fits(n, d):
+        ws = GramWorkspace(n, d, num.device)
+    L.call("mmb_gram", L.ptr(num), L.ptr(cnt), n, d, L.ptr(G), int(accumulate), L.ptr(ws.buf),
+           L.stream_ptr())
+    return G
+
+
+def xt_omega(num, cnt, omega_rows: torch.Tensor) -> torch.Tensor:
+    n, d = num.shape
+    k = omega_rows.shape[1]
+    z0 = torch.empty((d, k), dtype=torch.float64, device=num.device)
+    L.call("mmb_xt_omega", L.ptr(num), L.ptr(cnt), n, d, L.ptr(omega_rows), k, L.ptr(z0),
+           L.stream_ptr())
+    return z0
+
+
+def pc_start_block(n_total: int, d: int, npc: int, device, num=None, cnt=None, row0: int = 0,
+                   n_total_rows_omega: int | None = None):
+    """Z0 of sklearn's randomized SVD.  Direct branch: Omega [d,k].  Transposed
+    branch (n_total < d): X^T Omega_n for this shard's rows [row0, row0+n)."""
+    k = npc + N_OVERSAMPLES
+    if n_total >= d:
+        return omega(d, k, device), False
+    om = omega(n_total, k, device)[row0:row0 + num.shape[0]].contiguous()
+    return xt_omega(num, cnt, om), True
+
+
+def pc_solve(G: torch.Tensor, z0: torch.Tensor, npc: int, transposed: bool,
+             n_iter: int = N_ITER) -> torch.Tensor:
+    d = G.shape[0]
+    k = z0.shape[1]
+    pc = torch.empty((npc, d), dtype=torch.float64, device=G.device)
+    L.call("mmb_pc_solve", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed), L.ptr(pc),
+           L.stream_ptr())
+    return pc
+
+
+# ------------------------------------------------------------------ a4
+def remove_pc(num, cnt, pc: torch.Tensor, out_dtype=torch.float32, out=None) -> torch.Tensor:
+    n, d = num.shape
+    if out is None:
+        out = torch.empty((n, d), dtype=out_dtype, device=num.device)
+    o32 = L.ptr(out) if out.dtype == torch.float32 else None
+    o64 = L.ptr(out) if out.dtype == torch.float64 else None
+    L.call("mmb_pc_remove", L.ptr(num), L.ptr(cnt), n, d, L.ptr(pc), pc.shape[0], o32, o64,
+           L.stream_ptr())
+    return out
+
+
+def sif_embeddings(table, ids, wtab32=None, w=None, npc: int = 1, out_dtype=torch.float32,
+                   check_ids: bool = True, allreduce=None, n_total=None, row0: int = 0):
+    """a1-a5 fused on device: weighted average, Gram (+ optional all-reduce
+    across ranks), randomized-SVD PC, removal.  Returns (emb [N,D], pc)."""
+    ids32 = narrow_ids(ids)
+    flag = torch.zeros(1, dtype=torch.int32, device=table.device) if check_ids else None
+    num, cnt = weighted_sum(table, ids32, w=w, wtab32=wtab32, flag=flag)
+    G = gram(num, cnt)
+    n_total = num.shape[0] if n_total is None else n_total
+    z0, transposed = pc_start_block(n_total, table.shape[1], npc, table.device, num, cnt, row0)
+    if allreduce is not None:
+        allreduce(G)
+        if transposed:
+            allreduce(z0)
+    pc = pc_solve(G, z0, npc, transposed)
+    out = remove_pc(num, cnt, pc, out_dtype)
+    if check_ids:
+        check_flag(flag, table.shape[0])
+    return out, pc
+
+
+# ------------------------------------------------------------------ a7 / a8
+def calc_weights(x: torch.Tensor, b_mean: torch.Tensor, b_log_sigma: torch.Tensor):
+    x = x.contiguous()
+    f = x.shape[-1]
+    qm = torch.empty_like(x)
+    qs = torch.empty_like(x)
+    L.call("mmb_calc_weights", L.ptr(x), x.numel() // f, f, L.ptr(b_mean.contiguous()),
+           L.ptr(b_log_sigma.contiguous()), L.ptr(qm), L.ptr(qs), L.stream_ptr())
+    return qm, qs
+
+
+def mm2_dims(d, a, vd):
+    return L.query("mmb_mm2_k", d, a, vd), L.query("mmb_mm2_ldw", d)
+
+
+class MMB2Projection:
+    """Merged [Kp, ldw] projection of the six generators (sif2.py:167-205)."""
+
+    def __init__(self, networks: dict, d: int, a: int, vd: int, t: int, device):
+        self.d, self.a, self.vd, self.t = d, a, vd, t
+        self.kp, self.ldw = mm2_dims(d, a, vd)
+        self.wm = torch.empty((self.kp, self.ldw), dtype=torch.float32, device=device)
+        self.c0 = torch.empty((self.ldw,), dtype=torch.float32, device=device)
+        self.params = []
+        for k in MMB2_KEYS:  # KeyError for a missing combination, like sif2.py:182
+            mu, ls = networks[k]
+            self.params.append(tuple(p.detach().to(device=device, dtype=torch.float32).contiguous()
+                                     for p in (mu.weight, mu.bias, ls.weight, ls.bias)))
+        self.refresh()
+
+    def refresh(self):
+        arr = lambda i: (ctypes_ptr_array([p[i].data_ptr() for p in self.params]))
+        L.call("mmb_mm2_prepare", arr(0), arr(1), arr(2), arr(3), self.d, self.a, self.vd, self.t,
+               L.ptr(self.wm), self.ldw, L.ptr(self.c0), L.stream_ptr())
+
+
+def ctypes_ptr_array(ptrs):
+    import ctypes
+
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=None,
+               text_dense=None, emb_dense=None, w_dense=None, flag=None, out=None):
+    kp, _ = mm2_dims(d, a, vd)
+    dev = audio.device
+    if out is None:
+        out = (torch.empty((n, d), dtype=torch.float32, device=dev),
+               torch.empty((n, kp), dtype=torch.float32, device=dev),
+               torch.empty((2, n), dtype=torch.float32, device=dev))
+    num, s, aux = out
+    V = table.shape[0] if table is not None else 0
+    L.call("mmb_mm2_stream", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32), L.ptr(text_dense),
+           L.ptr(emb_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
+           L.ptr(num), L.ptr(s), L.ptr(aux), L.ptr(flag), L.stream_ptr())
+    return num, s, aux
+
+
+def mm2_project(s, num, aux, proj: MMB2Projection, out=None):
+    n = num.shape[0]
+    if out is None:
+        out = torch.empty((n, proj.d), dtype=torch.float32, device=num.device)
+    L.call("mmb_mm2_project", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wm), proj.ldw,
+           L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
+    return out
+
+
+class FusedStep:
+    """One pass of the north-star hot path over a batch of utterances resident
+    in HBM (bench 'step'): both the SIF text embedding (a1-a5, PC-removed) and
+    the closed-form MMB2 embedding (a6-a8) of every utterance.
+
+      mm2_stream   ids/table/wtab + audio + visual -> num, s, aux  (HBM-bound)
+      gram         num/cnt -> G (fp64 MFMA)            [+ RCCL all-reduce of G]
+      pc_solve     G -> pc (1 workgroup)
+      pc_remove    num/cnt, pc -> sif                    (HBM-bound)
+      mm2_prepare  generator weights -> Wm, c0
+      mm2_project  s, num, aux, Wm -> mmb2 (fp32 MFMA + fused normalisation)
+    """
+
+    def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
+                 n_total: int | None = None, row0: int = 0):
+        self.inp = inputs
+        self.ids = inputs["ids"]
+        self.n, self.t = self.ids.shape
+        self.table = inputs["table"]
+        self.V, self.d = self.table.shape
+        self.a = inputs["audio"].shape[-1]
+        self.vd = inputs["visual"].shape[-1]
+        dev = self.table.device
+        self.proj = MMB2Projection(networks, self.d, self.a, self.vd, self.t, dev)
+        kp = self.proj.kp
+        self.num = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
+        self.s = torch.empty((self.n, kp), dtype=torch.float32, device=dev)
+        self.aux = torch.empty((2, self.n), dtype=torch.float32, device=dev)
+        self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
+        self.gws = GramWorkspace(self.n, self.d, dev)
+        self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
+        self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
+        self.npc = npc
+        self.allreduce = allreduce
+        self.n_total = self.n if n_total is None else n_total
+        self.row0 = row0
+        if self.n_total >= self.d:
+            self.z0 = omega(self.d, npc + N_OVERSAMPLES, dev)
+            self.transposed = False
+        else:
+            self.z0 = None
+            self.transposed = True
+        self.flag = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def run(self):
+        mm2_stream(self.n, self.t, self.d, self.a, self.vd, self.inp["audio"], self.inp["visual"],
+                   ids32=self.ids, table=self.table, wtab32=self.inp["wtab"], flag=self.flag,
+                   out=(self.num, self.s, self.aux))
+        cnt = self.aux[0]
+        gram(self.num, cnt, self.G, ws=self.gws)
+        z0 = self.z0
+        if self.transposed:
+            om = omega(self.n_total, self.npc + N_OVERSAMPLES, self.num.device)
+            z0 = xt_omega(self.num, cnt, om[self.row0:self.row0 + self.n].contiguous())
+        if self.allreduce is not None:
+            self.allreduce(self.G)
+            if self.transposed:
+                self.allreduce(z0)
+        pc = pc_solve(self.G, z0, self.npc, self.transposed)
+        remove_pc(self.num, cnt, pc, out=self.sif)
+        self.proj.refresh()
+        mm2_project(self.s, self.num, self.aux, self.proj, out=self.mmb2)
+        self.pc = pc
+        return self.sif, self.mmb2

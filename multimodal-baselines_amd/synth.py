@@ -1,0 +1,111 @@
+"""Seeded synthetic inputs of the reference's shapes.
+
+The reference ships no GloVe table, no h5 features and no MOSI weights
+(`/root/reference/.MISSING_LARGE_BLOBS:1-3`), so every workload here is
+synthetic and fully determined by a seed:
+
+* word table   ``E[v] = noise*z_v + common*g`` (one shared direction ``g`` so
+  the SIF sentence averages have a dominant first PC, as GloVe averages do —
+  the reason SIF removes it, `sif_functions.py:58-81`); row 0 (pad/OOV) = 0.
+* token ids    Zipf(s) over ``[1, V)``; optional ragged lengths padded with id 0
+  (the reference pads with 0, `simplesif.py:36-40`).
+* word weights ``a / (a + p(w))`` with ``a = 1e-3`` (`sif.py:14-32`), ``p`` the
+  same Zipf law; ``weights[0]`` configurable (POM ships 1.0, `pom_word_weights.npy`).
+* audio/visual dense ``[N, T, F]`` streams, U(-1, 1), optional -10 pads
+  (`utils.py:188-189`).
+
+Two back ends with the same recipe: numpy (host fixtures, CPU tests) and torch
+on a device (bench: generated in HBM so no H2D sits in the timed region).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SIF_A = 1e-3  # sif.py:14 default `a`
+
+
+def zipf_probs(V: int, s: float = 1.1) -> np.ndarray:
+    """p(w) for w in [1, V) normalised; index 0 gets probability 0."""
+    r = np.arange(1, V, dtype=np.float64)
+    p = r ** (-s)
+    p /= p.sum()
+    return np.concatenate([[0.0], p])
+
+
+def sif_weights(V: int, s: float = 1.1, w0: float = 1.0, a: float = SIF_A) -> np.ndarray:
+    """SIF weight table a/(a+p(w)) (sif.py:30) as float64, like pom_word_weights.npy."""
+    p = zipf_probs(V, s)
+    w = a / (a + p)
+    w[0] = w0
+    return w
+
+
+def word_table(V: int, D: int = 300, seed: int = 0, noise: float = 0.4,
+               common: float = 0.3) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    g = rng.standard_normal(D)
+    E = noise * rng.standard_normal((V, D)) + common * g
+    E = E.astype(np.float32)
+    E[0] = 0.0
+    return E
+
+
+def token_ids(N: int, L: int, V: int, seed: int = 0, s: float = 1.1,
+              ragged: bool = False, min_len: int = 1) -> np.ndarray:
+    """int64 ids [N, L] (the reference id dtype, pom_*_ids.npy)."""
+    rng = np.random.default_rng(seed)
+    cdf = np.cumsum(zipf_probs(V, s)[1:])
+    u = rng.random((N, L))
+    ids = np.searchsorted(cdf, u * cdf[-1], side="right") + 1
+    ids = np.minimum(ids, V - 1).astype(np.int64)
+    if ragged:
+        lens = rng.integers(min_len, L + 1, size=N)
+        ids[np.arange(L)[None, :] >= lens[:, None]] = 0
+    return ids
+
+
+def frames(N: int, T: int, F: int, seed: int = 0, pad_frac: float = 0.0) -> np.ndarray:
+    """float32 [N, T, F] U(-1,1); trailing pad frames set to -10 (utils.py:188-189)."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-1.0, 1.0, size=(N, T, F)).astype(np.float32)
+    if pad_frac > 0:
+        npad = rng.integers(0, max(1, int(T * pad_frac)) + 1, size=N)
+        for i in range(N):
+            if npad[i]:
+                x[i, T - npad[i]:, :] = -10.0
+    return x
+
+
+# ---------------------------------------------------------------- device side
+def device_workload(N: int, T: int, V: int, D: int = 300, A: int = 300, Vd: int = 300,
+                    seed: int = 0, device="cuda", s: float = 1.1, w0: float = 1.0):
+    """Config-3 workload generated directly in device memory (torch RNG).
+
+    Returns dict of device tensors: table [V,D] f32, wtab [V] f32 (the f32
+    rounding of the f64 SIF weights, as `simplesif.py:315` does), ids [N,T]
+    int32, audio [N,T,A] f32, visual [N,T,Vd] f32.
+    """
+    import torch
+
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    g = torch.randn(D, generator=gen, device=device, dtype=torch.float32)
+    table = torch.randn(V, D, generator=gen, device=device, dtype=torch.float32)
+    table.mul_(0.4).add_(0.3 * g)
+    table[0].zero_()
+    p = torch.tensor(zipf_probs(V, s), device=device, dtype=torch.float64)
+    wtab = (SIF_A / (SIF_A + p)).to(torch.float32)
+    wtab[0] = w0
+    cdf = torch.cumsum(p[1:], 0)
+    ids = torch.empty(N, T, device=device, dtype=torch.int32)
+    chunk = 1 << 22
+    flat = ids.view(-1)
+    for o in range(0, flat.numel(), chunk):
+        n = min(chunk, flat.numel() - o)
+        u = torch.rand(n, generator=gen, device=device, dtype=torch.float64) * cdf[-1]
+        flat[o:o + n] = (torch.searchsorted(cdf, u, right=True) + 1).clamp_(max=V - 1).to(torch.int32)
+    audio = torch.empty(N, T, A, device=device, dtype=torch.float32)
+    visual = torch.empty(N, T, Vd, device=device, dtype=torch.float32)
+    audio.uniform_(-1.0, 1.0, generator=gen)
+    visual.uniform_(-1.0, 1.0, generator=gen)
+    return {"table": table, "wtab": wtab, "ids": ids, "audio": audio, "visual": visual}

@@ -1,0 +1,126 @@
+"""CPU restatement of the SIF text-embedding path (a1-a5) — TEST INFRASTRUCTURE ONLY.
+
+Follows `/root/reference/sif_functions.py` and `/root/reference/sif.py`.  The PC
+step restates scikit-learn's `TruncatedSVD(algorithm='randomized')`
+(third-party; the reference pins no version — this image has scikit-learn
+1.7.2: `sklearn/decomposition/_truncated_svd.py:fit_transform`,
+`sklearn/utils/extmath.py:_randomized_range_finder` / `_randomized_svd`).
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy import linalg
+
+
+def seq2weight(seq, mask, weight4ind):
+    """sif_functions.py:8-15 — per-token weight gather, f64 table -> f32 output.
+
+    Vectorised form of the reference double loop: weight = table[id] where
+    mask > 0 and id >= 0, else 0.
+    """
+    seq = np.asarray(seq)
+    sel = (np.asarray(mask) > 0) & (seq >= 0)
+    out = np.zeros(seq.shape, dtype=np.float32)
+    out[sel] = np.asarray(weight4ind)[seq[sel]]
+    return out
+
+
+def seq2weight_loop(seq, mask, weight4ind):
+    """The literal loop of sif_functions.py:10-13 (small inputs only)."""
+    w = np.zeros(seq.shape).astype("float32")
+    for i in range(seq.shape[0]):
+        for j in range(seq.shape[1]):
+            if mask[i, j] > 0 and seq[i, j] >= 0:
+                w[i, j] = weight4ind[seq[i, j]]
+    return w
+
+
+def get_weighted_average(We, x, w):
+    """sif_functions.py:28-56 — emb[i] = w[i].dot(We[x[i]]) / count_nonzero(w[i]).
+
+    Output float64 (np.zeros default, :37); each row is computed in the table's
+    dtype (f32 sgemv for an f32 table) exactly as the reference row loop does.
+    Negative ids wrap (numpy fancy indexing) — with weight 0 they add nothing.
+    """
+    n = x.shape[0]
+    emb = np.zeros((n, We.shape[1]))
+    for i in range(n):
+        emb[i, :] = w[i, :].dot(We[x[i, :], :]) / np.count_nonzero(w[i, :])
+    return emb
+
+
+# --------------------------------------------------------------------- PC (a3)
+def randomized_svd_components(M, n_components, n_oversamples=10, n_iter=7, random_state=0):
+    """Restates sklearn 1.7.2 `_randomized_svd` + TruncatedSVD's svd_flip.
+
+    * transpose when n_samples < n_features (extmath.py:562-566);
+    * Q ~ RandomState(seed).normal(size=(M.shape[1], k+p)), cast to M's float
+      dtype (extmath.py:297-301);
+    * n_iter rounds of LU(permute_l) normalised power iteration
+      (normalizer 'auto' -> 'LU' for n_iter > 2, extmath.py:313-352);
+    * QR, B = Q^T M, SVD of B (gesdd), U = Q Uhat (extmath.py:354-590);
+    * TruncatedSVD passes flip_sign=False then svd_flip(U, VT,
+      u_based_decision=False) (_truncated_svd.py:244-253).
+    Returns components_ [n_components, n_features].
+    """
+    rs = np.random.RandomState(random_state)
+    A = M
+    n_samples, n_features = A.shape
+    k = n_components + n_oversamples
+    transpose = n_samples < n_features
+    if transpose:
+        A = A.T
+    Q = rs.normal(size=(A.shape[1], k))
+    if A.dtype.kind == "f":
+        Q = Q.astype(A.dtype, copy=False)
+    for _ in range(n_iter):
+        Q, _ = linalg.lu(A @ Q, permute_l=True, check_finite=False)
+        Q, _ = linalg.lu(A.T @ Q, permute_l=True, check_finite=False)
+    Q, _ = linalg.qr(A @ Q, mode="economic", check_finite=False)
+    B = Q.T @ A
+    Uhat, s, Vt = linalg.svd(B, full_matrices=False, lapack_driver="gesdd")
+    U = Q @ Uhat
+    if transpose:
+        U, Vt = Vt[:n_components, :].T, U[:, :n_components].T
+    else:
+        U, Vt = U[:, :n_components], Vt[:n_components, :]
+    # svd_flip(u, v, u_based_decision=False): largest |v| entry of each row > 0
+    idx = np.argmax(np.abs(Vt), axis=1)
+    signs = np.sign(Vt[np.arange(Vt.shape[0]), idx])
+    return Vt * signs[:, None]
+
+
+def compute_pc(X, npc=1):
+    """sif_functions.py:58-67 (uncentred; TruncatedSVD(npc, n_iter=7, random_state=0))."""
+    return randomized_svd_components(np.asarray(X), npc, n_oversamples=10, n_iter=7,
+                                     random_state=0)
+
+
+def remove_pc(X, npc=1):
+    """sif_functions.py:69-81."""
+    pc = compute_pc(X, npc)
+    if npc == 1:
+        return X - X.dot(pc.transpose()) * pc
+    return X - X.dot(pc.transpose()).dot(pc)
+
+
+def SIF_embedding(We, x, w, rmpc=1):
+    """sif_functions.py:84-96."""
+    emb = get_weighted_average(We, x, w)
+    if rmpc > 0:
+        emb = remove_pc(emb, rmpc)
+    return emb
+
+
+def get_sentence_embeddings(word_embeddings, weights, text):
+    """sif.py:78-94 — mask = ones, rmpc = 1."""
+    w = seq2weight(text, np.ones(text.shape), weights)
+    return SIF_embedding(word_embeddings, text, w, 1)
+
+
+def exact_top_pc(X, npc=1):
+    """Exact top right singular vectors (for the spectral-gap discussion only)."""
+    _, _, vt = np.linalg.svd(np.asarray(X, np.float64), full_matrices=False)
+    v = vt[:npc]
+    idx = np.argmax(np.abs(v), axis=1)
+    return v * np.sign(v[np.arange(npc), idx])[:, None]

@@ -1,0 +1,146 @@
+"""GPU parity: closed-form MMB2 (a7/a8) through libmmb vs the reference fixtures and the oracle.
+
+Bar: 1e-5 row-relative against the reference's float64 evaluation of
+sif2.estimate_embedding_overall_gpu2 (the reference's own fp32 run meets the
+same bar, test_oracle_golden.py::test_mmb2_oracle).
+"""
+import numpy as np
+import pytest
+import torch
+
+import models
+import pipeline as P
+import sif2
+import synth
+from oracle import mmb2_oracle as M
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _inputs(z, dev):
+    A, Vd, V = int(z["A"]), int(z["Vd"]), int(z["V"])
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None, frozen_weights=True)
+    E = synth.word_table(V, 300, seed=int(z["table_seed"]))
+    ids = z["ids"]
+    N, T = ids.shape
+    pe = float(z["pad_frac"])
+    audio = synth.frames(N, T, A, seed=int(z["audio_seed"]), pad_frac=pe)
+    visual = synth.frames(N, T, Vd, seed=int(z["visual_seed"]), pad_frac=pe)
+    return gen, E, ids, audio, visual, z["weights"]
+
+
+def _drop_in_call(gen, E, ids, audio, visual, weights, dev):
+    """The --time_test call site (simplesif.py:820-875) with our sif2."""
+    word_embeddings = torch.tensor(E, device=dev)
+    wt = torch.tensor(weights, device=dev, dtype=torch.float32)
+    text_id = torch.as_tensor(ids, dtype=torch.long, device=dev)
+    text = word_embeddings[text_id]
+    au = torch.tensor(audio, device=dev)
+    vi = torch.tensor(visual, device=dev)
+    data = {"text": text, "audio": au, "visual": vi,
+            "audiovisual": torch.cat([au, vi], -1), "textaudio": torch.cat([text, au], -1),
+            "textvisual": torch.cat([text, vi], -1),
+            "textaudiovisual": torch.cat([text, au, vi], -1)}
+    masks = {k: None for k in list(data) + list(sif2.KEYS)}
+    g = gen.to(dev)
+    nets = {k: (g.embed2out[k]["mu"], g.embed2out[k]["log_sigma"]) for k in sif2.KEYS}
+    sw = torch.gather(wt.expand(len(ids), -1), 1, text_id) * (text_id >= 0)
+    with torch.no_grad():
+        return sif2.estimate_embedding_overall_gpu2(data, masks, nets, sw, text)
+
+
+@pytest.mark.parametrize("case", ["g4_mmb2_mosi", "g4_mmb2_syn"])
+def test_gpu2_drop_in_vs_reference(gpu, golden, case):
+    z = golden(case)
+    gen, E, ids, audio, visual, weights = _inputs(z, gpu)
+    cs = _drop_in_call(gen, E, ids, audio, visual, weights, gpu)
+    assert cs.shape == (len(ids), 300) and cs.dtype == torch.float32
+    assert M.row_rel_err(cs.cpu().numpy(), z["cs_f64"]) < TOL
+
+
+@pytest.mark.parametrize("case", ["g4_mmb2_mosi", "g4_mmb2_syn"])
+def test_fused_id_path_equals_dense_path(gpu, golden, case):
+    z = golden(case)
+    gen, E, ids, audio, visual, weights = _inputs(z, gpu)
+    dense = _drop_in_call(gen, E, ids, audio, visual, weights, gpu)
+    n, t = ids.shape
+    A, Vd = audio.shape[-1], visual.shape[-1]
+    table = torch.tensor(E, device=gpu)
+    wtab = torch.tensor(weights, device=gpu, dtype=torch.float32)
+    ids32 = torch.as_tensor(ids, dtype=torch.int32, device=gpu)
+    au, vi = torch.tensor(audio, device=gpu), torch.tensor(visual, device=gpu)
+    proj = P.MMB2Projection(gen.to(gpu).networks(), 300, A, Vd, t, gpu)
+    num, s, aux = P.mm2_stream(n, t, 300, A, Vd, au, vi, ids32=ids32, table=table, wtab32=wtab)
+    fused = P.mm2_project(s, num, aux, proj)
+    assert torch.equal(fused, dense)
+
+
+def test_calc_weights(gpu, golden):
+    z = golden("g4_mmb2_mosi")
+    gen, E, ids, audio, visual, weights = _inputs(z, gpu)
+    m = gen.embed2out["audio"]
+    qm, qs = sif2.calc_weights(torch.tensor(audio[:4], device=gpu), m["mu"].bias.to(gpu),
+                               m["log_sigma"].bias.to(gpu), None)
+    np.testing.assert_allclose(qm.cpu().numpy(), z["calc_qm_audio"], rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(qs.cpu().numpy(), z["calc_qs_audio"], rtol=2e-6, atol=1e-5)
+
+
+def test_missing_combination_raises(gpu, golden):
+    z = golden("g4_mmb2_mosi")
+    gen, E, ids, audio, visual, weights = _inputs(z, gpu)
+    with pytest.raises(KeyError):
+        sif2.estimate_embedding_overall_gpu2({}, {}, {"audio": None}, None, None)
+
+
+def test_single_utterance_errors_like_reference(gpu, golden):
+    z = golden("g4_mmb2_mosi")
+    gen, E, ids, audio, visual, weights = _inputs(z, gpu)
+    with pytest.raises(IndexError):
+        _drop_in_call(gen, E, ids[:1], audio[:1], visual[:1], weights, gpu)
+
+
+@pytest.mark.parametrize("N,T,A,Vd", [(2048, 40, 300, 300), (1000, 20, 78, 50)])
+def test_fused_step_vs_oracle(gpu, N, T, A, Vd):
+    """Both outputs of the bench step against the oracle at a mid size
+    (incl. feature widths that are not multiples of 4: scalar-load variants)."""
+    from oracle import sif_oracle as O
+
+    V = 30_000
+    torch.manual_seed(1)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None)
+    E = synth.word_table(V, 300, seed=2)
+    wt = synth.sif_weights(V, w0=1.0)
+    ids = synth.token_ids(N, T, V, seed=3, ragged=True)
+    audio = synth.frames(N, T, A, seed=4, pad_frac=0.2)
+    visual = synth.frames(N, T, Vd, seed=5, pad_frac=0.2)
+    inputs = {"table": torch.tensor(E, device=gpu),
+              "wtab": torch.tensor(wt, device=gpu, dtype=torch.float32),
+              "ids": torch.as_tensor(ids, dtype=torch.int32, device=gpu),
+              "audio": torch.tensor(audio, device=gpu), "visual": torch.tensor(visual, device=gpu)}
+    step = P.FusedStep(inputs, gen.to(gpu).networks())
+    sif_out, mm2_out = step.run()
+    ref_sif = O.get_sentence_embeddings(E, wt, ids)
+    assert M.row_rel_err(sif_out.cpu().numpy(), ref_sif) < TOL
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    text = E[ids]
+    ref_mm2 = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                                 M.params_from_module(gen.cpu()), sw, text)
+    assert M.row_rel_err(mm2_out.cpu().numpy(), ref_mm2) < TOL
+
+
+def test_fused_step_large_properties(gpu):
+    """At 100k utterances x 40 frames x 3 x 300: unit rows, finite, deterministic."""
+    N, T, V = 100_000, 40, 200_000
+    inp = synth.device_workload(N, T, V, seed=9, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks())
+    s1, m1 = [t.clone() for t in step.run()]
+    s2, m2 = step.run()
+    assert torch.equal(s1, s2) and torch.equal(m1, m2)
+    assert torch.isfinite(m1).all() and torch.isfinite(s1).all()
+    norms = torch.linalg.norm(m1.double(), dim=1)
+    assert (norms - 1).abs().max().item() < 1e-5

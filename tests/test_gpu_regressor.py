@@ -1,0 +1,122 @@
+"""GPU parity: the sentiment regressor (a10-a12) vs the reference's recorded runs.
+
+* one SGD step (forward, L1 backward, update) vs torch autograd + optim.SGD;
+* a 20-epoch train_sentiment_for_latents run from the same torch seed: the
+  same mini-batch order (global RNG consumed identically), so loss curves and
+  final weights track the reference's to fp32 rounding.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import mmb_lib as L
+import sentiment_model as SM
+
+pytestmark = pytest.mark.gpu
+
+
+def _train_steps(gpu, x, y, w1, b1, w2, b2, lr, perm=None, epochs=1, batch=32):
+    n = x.shape[0]
+    lat = torch.tensor(x, device=gpu)
+    lab = torch.tensor(y, device=gpu).reshape(n, -1).contiguous()
+    o = lab.shape[1]
+    h, d = w1.shape
+    P = [torch.tensor(a, device=gpu).contiguous() for a in (w1, b1, w2, b2)]
+    if perm is None:
+        perm = np.tile(np.arange(n), epochs)
+    perm = torch.as_tensor(perm, dtype=torch.int64, device=gpu)
+    spe = (n + batch - 1) // batch
+    sl = torch.empty(spe * epochs, dtype=torch.float32, device=gpu)
+    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
+    L.call("mmb_mlp_train", L.ptr(lat), L.ptr(lab), L.ptr(perm), n, epochs, batch, d, h, o,
+           float(lr), *[L.ptr(p) for p in P], L.ptr(sl), L.ptr(ws), L.stream_ptr())
+    return [p.cpu().numpy() for p in P], sl.cpu().numpy()
+
+
+def test_one_sgd_step(gpu, golden):
+    z = golden("g5_senti_step")
+    (w1, b1, w2, b2), sl = _train_steps(gpu, z["x"], z["y"], z["w1"], z["b1"], z["w2"], z["b2"], 0.1)
+    assert abs(sl[0] - float(z["loss"])) < 1e-6 * max(1.0, abs(float(z["loss"])))
+    np.testing.assert_allclose(w1, z["nw1"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(b1, z["nb1"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(w2, z["nw2"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(b2, z["nb2"], rtol=1e-5, atol=1e-6)
+
+
+def test_forward(gpu, golden):
+    z = golden("g5_senti_step")
+    m = SM.SentimentModel(300, 100, 1).to(gpu)
+    with torch.no_grad():
+        m.hidden1.weight.copy_(torch.tensor(z["w1"]))
+        m.hidden1.bias.copy_(torch.tensor(z["b1"]))
+        m.out.weight.copy_(torch.tensor(z["w2"]))
+        m.out.bias.copy_(torch.tensor(z["b2"]))
+    y = m(torch.tensor(z["x"], device=gpu))
+    assert y.shape == (32,)
+    np.testing.assert_allclose(y.cpu().numpy(), z["pred"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("h,o,n", [(150, 1, 77), (100, 7, 64), (60, 3, 33)])
+def test_multi_step_vs_torch(gpu, h, o, n):
+    """Several epochs incl. a ragged last batch, other widths, multi-output heads."""
+    rng = np.random.default_rng(h + o)
+    x = rng.standard_normal((n, 300)).astype(np.float32)
+    y = rng.uniform(-3, 3, (n, o)).astype(np.float32)
+    torch.manual_seed(h)
+    ref = torch.nn.Sequential(torch.nn.Linear(300, h), torch.nn.ReLU(), torch.nn.Linear(h, o))
+    init = [p.detach().numpy().copy() for p in ref.parameters()]
+    perm = np.concatenate([rng.permutation(n) for _ in range(3)])
+    opt = torch.optim.SGD(ref.parameters(), lr=0.05)
+    losses = []
+    for e in range(3):
+        order = perm[e * n:(e + 1) * n]
+        for s in range(0, n, 32):
+            idx = order[s:s + 32]
+            opt.zero_grad()
+            out = ref(torch.tensor(x[idx]))
+            loss = torch.nn.L1Loss(reduction="none")(out, torch.tensor(y[idx])).mean()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+    (w1, b1, w2, b2), sl = _train_steps(gpu, x, y if o > 1 else y[:, 0], *init, 0.05, perm=perm,
+                                        epochs=3)
+    np.testing.assert_allclose(sl, losses, rtol=1e-4, atol=1e-5)
+    got = [w1, b1, w2, b2]
+    for g, r in zip(got, ref.parameters()):
+        np.testing.assert_allclose(g, r.detach().numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_train_for_latents_matches_reference_run(gpu, golden):
+    z = golden("g5_senti_train")
+    with open(os.path.join(os.path.dirname(__file__), "golden", "g5_senti_train_metrics.json")) as f:
+        ref_metrics = json.load(f)
+    args = {"sentiment_hidden_size": 100, "n_sentiment_epochs": 20, "sentiment_lr": 0.1,
+            "early_stopping": False, "dataset": "mosi", "lr_decay": 0.5}
+    lat = tuple(torch.tensor(z[k]) for k in ("lat_train", "lat_valid", "lat_test"))
+    labels = (z["y_train"], z["y_valid"], z["y_test"])
+    captured = {}
+    orig = SM.train_sentiment
+
+    def spy(*a, **k):
+        tl, vl = orig(*a, **k)
+        captured["train"], captured["valid"] = tl, vl
+        captured["model"] = {kk: v.detach().cpu().numpy() for kk, v in a[1].state_dict().items()}
+        return tl, vl
+
+    SM.train_sentiment = spy
+    try:
+        torch.manual_seed(int(z["seed"]))
+        results = SM.train_sentiment_for_latents(args, lat, labels, gpu)
+    finally:
+        SM.train_sentiment = orig
+    np.testing.assert_allclose(captured["train"], z["train_losses"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(captured["valid"], z["valid_losses"], rtol=1e-4, atol=1e-6)
+    for k, v in captured["model"].items():
+        np.testing.assert_allclose(v, z["final_" + k.replace(".", "_")], rtol=1e-3, atol=1e-5)
+    after = ref_metrics["after"]
+    assert abs(results["mae"] - after["mae"]) < 1e-4
+    assert abs(results["corr"] - after["corr"]) < 1e-4
+    assert results["accuracy"] == after["accuracy"]

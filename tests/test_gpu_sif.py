@@ -1,0 +1,137 @@
+"""GPU parity: SIF text path (a1-a5) through libmmb vs the reference fixtures and the oracle.
+
+Bars (BASELINE.json north_star): a1 bit-exact; embeddings within
+1e-5 row-relative (max_j |y - y_ref| / max_j |y_ref|) of the reference f64
+output; the PC within 1e-8 of the reference's randomized-SVD PC.
+"""
+import numpy as np
+import pytest
+import torch
+
+import pipeline as P
+import sif
+import sif_functions as SF
+import synth
+from oracle import mmb2_oracle as M
+from oracle import sif_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIF_CASES = ["g1_pom_valid", "g1_pom_test", "g2_mosi", "g3_gap"]
+EMB_TOL = 1e-5
+
+
+def regen_table(z):
+    return synth.word_table(int(z["V"]), int(z["D"]), seed=int(z["table_seed"]),
+                            common=float(z["common"]))
+
+
+@pytest.mark.parametrize("case", SIF_CASES)
+def test_seq2weight_bit_exact(gpu, golden, case):
+    z = golden(case)
+    w = sif.get_sentence_word_weights(z["ids"], z["weights"])
+    assert w.dtype == np.float32 and np.array_equal(w, z["w"])
+
+
+def test_seq2weight_mask_and_negative_ids(gpu, golden):
+    z = golden("g1c_seq2weight")
+    w = SF.seq2weight(z["seq"], z["mask"], z["weights"])
+    assert np.array_equal(w, z["w"])
+
+
+def test_seq2weight_out_of_range_raises(gpu):
+    with pytest.raises(IndexError):
+        SF.seq2weight(np.array([[0, 5]]), np.ones((1, 2)), np.ones(5))
+
+
+@pytest.mark.parametrize("case", SIF_CASES)
+def test_weighted_average(gpu, golden, case):
+    z = golden(case)
+    emb = SF.get_weighted_average(regen_table(z), z["ids"], z["w"])
+    assert emb.dtype == np.float64 and emb.shape == z["emb"].shape
+    assert M.row_rel_err(emb, z["emb"]) < 2e-6
+
+
+def test_weighted_average_negative_ids_wrap(gpu, golden):
+    z = golden("g1c_seq2weight")
+    emb = SF.get_weighted_average(regen_table(z), z["seq"], z["w"])
+    assert M.row_rel_err(emb, z["emb"]) < 2e-6
+
+
+@pytest.mark.parametrize("case", SIF_CASES + ["g3b_npc2"])
+def test_compute_pc_replays_randomized_svd(gpu, golden, case):
+    """Device PC from the Gram == sklearn's randomized PC, also without a gap (g3)."""
+    z = golden(case)
+    npc = z["pc"].shape[0]
+    pc = SF.compute_pc(z["emb"].astype(np.float64), npc)
+    assert pc.shape == z["pc"].shape
+    assert np.abs(pc - z["pc"]).max() < 1e-8
+
+
+@pytest.mark.parametrize("case", SIF_CASES)
+def test_sentence_embeddings_end_to_end(gpu, golden, case):
+    z = golden(case)
+    out = sif.get_sentence_embeddings(regen_table(z), z["weights"], z["ids"])
+    assert out.dtype == np.float64
+    assert M.row_rel_err(out, z["out"]) < EMB_TOL
+
+
+def test_sif_embedding_with_given_weights(gpu, golden):
+    z = golden("g2_mosi")
+    p = SF.Params()
+    p.rmpc = 1
+    out = SF.SIF_embedding(regen_table(z), z["ids"], z["w"], p)
+    assert M.row_rel_err(out, z["out"]) < EMB_TOL
+    p.rmpc = 0
+    emb = SF.SIF_embedding(regen_table(z), z["ids"], z["w"], p)
+    assert M.row_rel_err(emb, z["emb"]) < 2e-6
+
+
+def test_remove_pc_npc2(gpu, golden):
+    z = golden("g3b_npc2")
+    out = SF.remove_pc(z["emb"].astype(np.float64), 2)
+    assert M.row_rel_err(out, z["out"]) < 1e-9
+
+
+def test_empty_and_single_token_utterances(gpu):
+    """Ragged edge cases: length-1 rows and rows of pure padding (count 0 -> nan, as numpy)."""
+    V = 500
+    E = synth.word_table(V, 300, seed=3)
+    wt = synth.sif_weights(V, w0=0.0)
+    ids = synth.token_ids(400, 12, V, seed=4, ragged=True)
+    ids[0, 1:] = 0
+    ids[1, :] = 0
+    w = O.seq2weight(ids, np.ones(ids.shape), wt)
+    ref = O.get_weighted_average(E, ids, w)  # row 1: 0/0 -> nan
+    got = SF.get_weighted_average(E, ids, w)
+    assert np.isnan(got[1]).all() and np.isnan(ref[1]).all()
+    ok = ~np.isnan(ref).any(axis=1)
+    assert M.row_rel_err(got[ok], ref[ok]) < 2e-6
+
+
+@pytest.mark.parametrize("N,L,V", [(3000, 40, 20000), (700, 256, 5000)])
+def test_sif_vs_oracle_mid_size(gpu, N, L, V):
+    E = synth.word_table(V, 300, seed=N)
+    wt = synth.sif_weights(V, w0=1.0)
+    ids = synth.token_ids(N, L, V, seed=L, ragged=True)
+    ref = O.get_sentence_embeddings(E, wt, ids)
+    got = sif.get_sentence_embeddings(E, wt, ids)
+    assert M.row_rel_err(got, ref) < EMB_TOL
+
+
+def test_device_sif_properties_large(gpu):
+    """Size-independent properties at a large N: the output is orthogonal to the
+    removed PC, removal is idempotent, and two runs are bit-identical."""
+    N, L, V = 200_000, 40, 100_000
+    inp = synth.device_workload(N, L, V, A=4, Vd=4, seed=5, device=gpu)
+    out1, pc = P.sif_embeddings(inp["table"], inp["ids"], wtab32=inp["wtab"], npc=1,
+                                out_dtype=torch.float64)
+    out2, _ = P.sif_embeddings(inp["table"], inp["ids"], wtab32=inp["wtab"], npc=1,
+                               out_dtype=torch.float64)
+    assert torch.equal(out1, out2)
+    proj = (out1 @ pc.T).abs().max().item()
+    assert proj < 1e-10 * out1.abs().max().item() * 300
+    assert abs(torch.linalg.norm(pc).item() - 1.0) < 1e-12
+    # idempotence: removing the same pc again changes nothing beyond rounding
+    again = out1 - (out1 @ pc.T) * pc
+    assert (again - out1).abs().max().item() < 1e-12

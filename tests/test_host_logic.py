@@ -1,0 +1,61 @@
+"""CPU: host-side logic of the drop-in (no GPU needed)."""
+import numpy as np
+import pytest
+import torch
+from torch.utils.data import DataLoader
+
+import models
+import sentiment_model as SM
+
+
+def test_mmb2_parameter_layout_and_init_order():
+    torch.manual_seed(0)
+    g = models.AudioVisualGeneratorMultimodal(300, 76, 48, norm=None)
+    assert list(g.embed2out.keys()) == list(models.MMB2_KEYS)
+    widths = {k: g.embed2out[k]["mu"].weight.shape[0] for k in models.MMB2_KEYS}
+    assert widths == {"audio": 76, "visual": 48, "audiovisual": 124, "textaudio": 376,
+                      "textvisual": 348, "textaudiovisual": 424}
+    assert all(g.embed2out[k]["mu"].weight.shape[1] == 300 for k in models.MMB2_KEYS)
+    g1 = models.AudioVisualGeneratorMultimodal(300, 76, 48, unimodal=True)
+    assert list(g1.embed2out.keys()) == ["audio", "visual"]
+
+
+def test_combo_segments_follow_cat_order():
+    assert models.combo_dims("textaudiovisual", 300, 76, 48) == [("text", 300), ("audio", 76),
+                                                                   ("visual", 48)]
+    assert models.combo_dims("audiovisual", 300, 76, 48) == [("audio", 76), ("visual", 48)]
+
+
+@pytest.mark.parametrize("n,bs", [(1284, 32), (229, 32), (33, 32), (5, 32)])
+def test_loader_emulation_consumes_rng_like_iteration(n, bs):
+    data = SM.SentimentData(np.arange(n, dtype=np.float32), torch.device("cpu"))
+    loader = DataLoader(data, batch_size=bs, shuffle=True)
+    torch.manual_seed(7)
+    real = [[j.clone() for j, _ in loader] for _ in range(3)]
+    after_real = torch.rand(4)
+    torch.manual_seed(7)
+    emu = [SM._epoch_batches(loader) for _ in range(3)]
+    after_emu = torch.rand(4)
+    assert torch.equal(after_real, after_emu)
+    for r, e in zip(real, emu):
+        assert len(r) == len(e)
+        for a, b in zip(r, e):
+            assert torch.equal(a, b)
+
+
+def test_f32_epoch_mean_matches_tensor_arithmetic():
+    vals = np.random.default_rng(0).random(41).astype(np.float32)
+    acc = 0
+    for v in vals:
+        acc = acc + torch.tensor(v)
+    ref = float(acc / 41)
+    assert SM._f32_mean_of(vals, 41) == ref
+
+
+def test_sentiment_model_init_matches_reference_order():
+    torch.manual_seed(3)
+    m = SM.SentimentModel(300, 100, 1)
+    torch.manual_seed(3)
+    h = torch.nn.Linear(300, 100)
+    o = torch.nn.Linear(100, 1)
+    assert torch.equal(m.hidden1.weight, h.weight) and torch.equal(m.out.bias, o.bias)

@@ -1,0 +1,74 @@
+"""CPU: the C-ABI library loads and exports every symbol include/mmb.h declares.
+
+No compute calls here (no GPU in the build container) except the host-only
+RNG helper, which is checked bit for bit against numpy's legacy RandomState.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import mmb_lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mmb.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mmb_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    assert "mmb_sif_wavg" in names and "mmb_pc_solve" in names and "mmb_mlp_train" in names
+    assert len(names) >= 19
+
+
+def test_library_exports_every_declared_symbol():
+    lib = mmb_lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), f"{name} declared in mmb.h but not exported"
+
+
+def test_ctypes_signatures_cover_header():
+    assert set(declared_functions()) == set(mmb_lib.SIGNATURES)
+
+
+def test_exports_are_c_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", mmb_lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (mmb_\w+)", out))
+    assert set(declared_functions()) <= exported  # unmangled extern "C"
+
+
+def test_library_carries_gfx950_code_objects():
+    data = open(mmb_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version_and_shape_helpers():
+    assert mmb_lib.query("mmb_version") >= 100
+    assert mmb_lib.query("mmb_mm2_k", 300, 300, 300) == 1824
+    assert mmb_lib.query("mmb_mm2_k", 300, 76, 48) == 864
+    assert mmb_lib.query("mmb_mm2_ldw", 300) == 320
+    assert mmb_lib.query("mmb_gram_workspace_bytes", 1_000_000, 300) > 0
+    assert mmb_lib.query("mmb_mlp_workspace_bytes", 300, 100) == 4 * 10 * 64 * 16 * 4
+
+
+@pytest.mark.parametrize("seed,rows,k", [(0, 300, 11), (0, 64, 11), (0, 1, 12), (7, 1000, 3)])
+def test_host_randn_matches_numpy_randomstate(seed, rows, k):
+    got = mmb_lib.host_randn(seed, rows * k)
+    ref = np.random.RandomState(seed).normal(size=(rows, k)).ravel()
+    assert np.array_equal(got, ref)
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    # argument validation happens before any launch
+    with pytest.raises(mmb_lib.MMBError):
+        mmb_lib.call("mmb_pc_solve", None, 300, None, 11, 1, 7, 0, None, None)
+    with pytest.raises(mmb_lib.MMBError):
+        mmb_lib.call("mmb_host_randn", 0, -1, None)
