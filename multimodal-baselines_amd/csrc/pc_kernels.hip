@@ -151,22 +151,40 @@ __device__ void orth_wave(double* Z, int D, int k, int lane) {
   }
 }
 
-// GZ = G Z, thread p owns row p.  G symmetric: read column p (coalesced across p).
+// GZ = G Z.  Thread (g, p) owns row p and column group g (MC columns), so
+// every thread of the workgroup works (D=300: 3 groups of 4 of the 11
+// columns).  G symmetric: read column p (coalesced across p; the groups
+// re-read it from L1).  Z is read from LDS as a broadcast.
+template <int MC>
+__device__ void gz_product_mc(const double* __restrict__ G, const double* Z, double* GZ, int D,
+                              int k, int groups) {
+  const int t = threadIdx.x;
+  const int g = t / D, p = t - g * D;
+  if (g >= groups) return;
+  const int j0 = g * MC;
+  double acc[MC];
+#pragma unroll
+  for (int j = 0; j < MC; ++j) acc[j] = 0.0;
+  const double* gcol = G + p;
+  const double* zr = Z + j0;
+#pragma unroll 4
+  for (int q = 0; q < D; ++q) {
+    const double gq = gcol[static_cast<int64_t>(q) * D];
+#pragma unroll
+    for (int j = 0; j < MC; ++j)
+      if (j0 + j < k) acc[j] = fma(gq, zr[q * k + j], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < MC; ++j)
+    if (j0 + j < k) GZ[p * k + j0 + j] = acc[j];
+}
+
 __device__ void gz_product(const double* __restrict__ G, const double* Z, double* GZ, int D, int k) {
-  const int p = threadIdx.x;
-  if (p < D) {
-    double acc[kMaxK];
-#pragma unroll
-    for (int j = 0; j < kMaxK; ++j) acc[j] = 0.0;
-    for (int q = 0; q < D; ++q) {
-      const double gq = G[static_cast<int64_t>(q) * D + p];
-#pragma unroll
-      for (int j = 0; j < kMaxK; ++j)
-        if (j < k) acc[j] = fma(gq, Z[q * k + j], acc[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < kMaxK; ++j)
-      if (j < k) GZ[p * k + j] = acc[j];
+  const int maxg = kSolveNT / D;  // >= 2 for D <= 512
+  if (maxg >= 3 && k <= 12) {
+    gz_product_mc<4>(G, Z, GZ, D, k, (k + 3) / 4);
+  } else {
+    gz_product_mc<8>(G, Z, GZ, D, k, (k + 7) / 8);
   }
 }
 
@@ -186,7 +204,7 @@ __device__ void small_gram(const double* X, const double* Y, double* M, int D, i
 __device__ void jacobi_wave(double* A, double* V, int k, int lane) {
   for (int r = lane; r < k * k; r += kWave) V[r] = (r / k == r % k) ? 1.0 : 0.0;
   wave_lds_sync();
-  for (int sweep = 0; sweep < 64; ++sweep) {
+  for (int sweep = 0; sweep < 40; ++sweep) {
     double off = 0.0, dia = 0.0;
     for (int r = lane; r < k * k; r += kWave) {
       const int i = r / k, j = r % k;
@@ -196,12 +214,15 @@ __device__ void jacobi_wave(double* A, double* V, int k, int lane) {
     }
     off = wave_sum(off);
     dia = wave_sum(dia);
-    if (off <= 1e-34 * dia) break;
+    // converged when the off-diagonal mass is at fp64 rounding level
+    // (|a_pq| ~ 1e-15 |lambda|); a tighter bar is unreachable and only spins
+    if (off <= 1e-30 * dia) break;
     for (int p = 0; p < k - 1; ++p) {
       for (int q = p + 1; q < k; ++q) {
         const double apq = A[p * k + q];
-        if (apq == 0.0) continue;
         const double app = A[p * k + p], aqq = A[q * k + q];
+        // negligible next to both diagonal entries: rotating would change nothing
+        if (fabs(apq) <= 1e-18 * (fabs(app) + fabs(aqq))) continue;
         const double theta = (aqq - app) / (2.0 * apq);
         double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
         if (theta < 0.0) t = -t;

@@ -153,6 +153,40 @@ def remove_pc(num, cnt, pc: torch.Tensor, out_dtype=torch.float32, out=None) -> 
     return out
 
 
+class DeviceOps:
+    """The libmmb kernels global_pc() composes (tests substitute CPU doubles)."""
+
+    gram = staticmethod(lambda num, cnt, G=None, ws=None: gram(num, cnt, G, ws=ws))
+    omega = staticmethod(omega)
+    xt_omega = staticmethod(xt_omega)
+    pc_solve = staticmethod(pc_solve)
+
+
+def global_pc(num, cnt, npc: int, n_total: int, row0: int = 0, allreduce=None, ops=DeviceOps,
+              G=None, ws=None):
+    """The PC of ALL utterances across ranks (a3), from this rank's rows
+    [row0, row0 + n) of X = num / cnt.
+
+    Only the Gram (d x d f64) — and, in sklearn's transposed branch (fewer
+    utterances than features), the start block X^T Omega (d x k) — cross
+    ranks, each as one all-reduce (sum).  Every rank then runs the same
+    deterministic solve, so the PC is identical everywhere with no broadcast.
+    """
+    n, d = num.shape
+    k = npc + N_OVERSAMPLES
+    G = ops.gram(num, cnt, G, ws)
+    if n_total >= d:
+        z0, transposed = ops.omega(d, k, num.device), False
+    else:
+        om = ops.omega(n_total, k, num.device)[row0:row0 + n].contiguous()
+        z0, transposed = ops.xt_omega(num, cnt, om), True
+    if allreduce is not None:
+        allreduce(G)
+        if transposed:
+            allreduce(z0)
+    return ops.pc_solve(G, z0, npc, transposed)
+
+
 def sif_embeddings(table, ids, wtab32=None, w=None, npc: int = 1, out_dtype=torch.float32,
                    check_ids: bool = True, allreduce=None, n_total=None, row0: int = 0):
     """a1-a5 fused on device: weighted average, Gram (+ optional all-reduce
@@ -160,14 +194,8 @@ def sif_embeddings(table, ids, wtab32=None, w=None, npc: int = 1, out_dtype=torc
     ids32 = narrow_ids(ids)
     flag = torch.zeros(1, dtype=torch.int32, device=table.device) if check_ids else None
     num, cnt = weighted_sum(table, ids32, w=w, wtab32=wtab32, flag=flag)
-    G = gram(num, cnt)
     n_total = num.shape[0] if n_total is None else n_total
-    z0, transposed = pc_start_block(n_total, table.shape[1], npc, table.device, num, cnt, row0)
-    if allreduce is not None:
-        allreduce(G)
-        if transposed:
-            allreduce(z0)
-    pc = pc_solve(G, z0, npc, transposed)
+    pc = global_pc(num, cnt, npc, n_total, row0, allreduce)
     out = remove_pc(num, cnt, pc, out_dtype)
     if check_ids:
         check_flag(flag, table.shape[0])
@@ -277,12 +305,6 @@ class FusedStep:
         self.allreduce = allreduce
         self.n_total = self.n if n_total is None else n_total
         self.row0 = row0
-        if self.n_total >= self.d:
-            self.z0 = omega(self.d, npc + N_OVERSAMPLES, dev)
-            self.transposed = False
-        else:
-            self.z0 = None
-            self.transposed = True
         self.flag = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def run(self):
@@ -290,16 +312,8 @@ class FusedStep:
                    ids32=self.ids, table=self.table, wtab32=self.inp["wtab"], flag=self.flag,
                    out=(self.num, self.s, self.aux))
         cnt = self.aux[0]
-        gram(self.num, cnt, self.G, ws=self.gws)
-        z0 = self.z0
-        if self.transposed:
-            om = omega(self.n_total, self.npc + N_OVERSAMPLES, self.num.device)
-            z0 = xt_omega(self.num, cnt, om[self.row0:self.row0 + self.n].contiguous())
-        if self.allreduce is not None:
-            self.allreduce(self.G)
-            if self.transposed:
-                self.allreduce(z0)
-        pc = pc_solve(self.G, z0, self.npc, self.transposed)
+        pc = global_pc(self.num, cnt, self.npc, self.n_total, self.row0, self.allreduce,
+                       G=self.G, ws=self.gws)
         remove_pc(self.num, cnt, pc, out=self.sif)
         self.proj.refresh()
         mm2_project(self.s, self.num, self.aux, self.proj, out=self.mmb2)

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_profile.sh session into profiles/<tag>_*.
+
+* kernel stats (rocprofv3 --kernel-trace --stats) with short names;
+* HBM traffic per launch of each libmmb kernel from the two PMC passes:
+  FETCH_SIZE and WRITE_SIZE are KB; on gfx950 FETCH_SIZE counts exactly half
+  the bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM), so
+      hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+  (an upper estimate for narrower accesses, which that section leaves
+  uncalibrated);
+* the bench JSON line of the session.
+
+Usage: python tools/summarize_profile.py gpurun_out/r01 r01
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+
+def short(name):
+    name = re.sub(r"\(.*", "", name)
+    name = name.replace("void ", "").replace("mmb::", "")
+    return name[:70]
+
+
+def main(src, tag):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    lines = [f"# rocprofv3 summary — {tag}", ""]
+    bench = json.load(open(os.path.join(src, "bench.json")))
+    lines += ["## bench line", "", "```json", json.dumps(bench, indent=1), "```", ""]
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    lines += ["## kernel stats (`rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 "
+              "--warmup 3 --no-cpu-baseline`)", "",
+              "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
+    for r in stats:
+        lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
+                     f"{float(r['Percentage']):.2f} |")
+    lines.append("")
+
+    def pmc(path):
+        out = {}
+        for r in csv.DictReader(open(path)):
+            k = short(r["Kernel_Name"])
+            if "mmb" not in r["Kernel_Name"]:
+                continue
+            out.setdefault(k, []).append(float(r["Counter_Value"]))
+        return out
+
+    fetch = pmc(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
+    write = pmc(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    lines += ["## HBM traffic per launch (PMC; `(2*FETCH_SIZE + WRITE_SIZE) * 1024`)", "",
+              "| kernel | launches | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch |",
+              "|---|---|---|---|---|"]
+    traffic = {}
+    for k in sorted(fetch):
+        f = sum(fetch[k]) / len(fetch[k])
+        w = sum(write.get(k, [0.0])) / max(1, len(write.get(k, [0.0])))
+        b = (2 * f + w) * 1024
+        traffic[k] = b
+        lines.append(f"| `{k}` | {len(fetch[k])} | {f:.0f} | {w:.0f} | {b:.4g} |")
+    lines.append("")
+    stream = [v for k, v in traffic.items() if "utt_stream_kernel" in k]
+    cfg = bench["config"]
+    tj = {"tag": tag, "utts_per_launch": cfg["utts_per_gpu"], "tokens": cfg["tokens"],
+          "mm2_stream_hbm_bytes_per_launch": stream[0] if stream else None,
+          "per_kernel_hbm_bytes_per_launch": traffic}
+    with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
+        f.write("\n".join(lines))
+    with open(os.path.join(prof, f"{tag}_traffic.json"), "w") as f:
+        json.dump(tj, f, indent=1)
+    with open(os.path.join(prof, "traffic_latest.json"), "w") as f:
+        json.dump(tj, f, indent=1)
+    with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w") as f:
+        w = csv.writer(f)
+        w.writerow(["kernel", "calls", "avg_ns", "total_ns", "percent"])
+        for r in stats:
+            w.writerow([short(r["Name"]), r["Calls"], r["AverageNs"], r["TotalDurationNs"], r["Percentage"]])
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
