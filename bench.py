@@ -56,7 +56,9 @@ def cpu_baseline(inp, gen, n_sample):
     from oracle import mmb2_oracle as M
     from oracle import sif_oracle as O
 
-    cores = len(os.sched_getaffinity(0))
+    import torch
+
+    cores = torch.get_num_threads()  # the BLAS/OpenMP threads actually used (OMP_NUM_THREADS)
     n = n_sample
     table = inp["table"].cpu().numpy()
     wt = inp["wtab"].double().cpu().numpy()
@@ -87,7 +89,7 @@ def main():
     ap.add_argument("--utts-per-gpu", type=int, default=1_000_000)
     ap.add_argument("--tokens", type=int, default=40)
     ap.add_argument("--vocab", type=int, default=400_000)
-    ap.add_argument("--cpu-sample", type=int, default=4096)
+    ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
@@ -130,6 +132,8 @@ def main():
 
     # timed region: K steps, barrier + sync on both sides; HIP events on the
     # launch stream around the dominant kernel (mm2_stream) of every step
+    assert U * world >= D  # sklearn's direct (non-transposed) randomized-SVD branch
+    z0 = P.omega(D, 1 + P.N_OVERSAMPLES, dev)
     E = lambda: torch.cuda.Event(enable_timing=True)
     ev = [[E() for _ in range(7)] for _ in range(args.steps)]
     if world > 1:
@@ -148,7 +152,7 @@ def main():
         e[2].record()
         allreduce(step.G)
         e[3].record()
-        pc = P.pc_solve(step.G, step.z0, 1, False)
+        pc = P.pc_solve(step.G, z0, 1, False)
         e[4].record()
         P.remove_pc(step.num, cnt, pc, out=step.sif)
         e[5].record()

@@ -277,6 +277,167 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-utterance variant (tokens/frames <= 64, widths % 4 == 0, <= 512):
+// the fast path for MOSI / synthetic shapes.  One wave owns one utterance:
+// lane t stages token t (id, weight) in registers and the loop broadcasts it
+// with v_readlane, lane l owns float4 columns l and l+64 of every row for the
+// whole utterance, so there is no LDS, no barrier and no cross-lane reduction
+// of the sums — only independent 16-B loads (3 rows per frame in MMB2 mode)
+// that the compiler keeps in flight across unrolled frames.
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void fma4(float4& acc, float w, float4 v) {
+  acc.x = fmaf(w, v.x, acc.x); acc.y = fmaf(w, v.y, acc.y);
+  acc.z = fmaf(w, v.z, acc.z); acc.w = fmaf(w, v.w, acc.w);
+}
+__device__ __forceinline__ void add4(float4& acc, float4 v) {
+  acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+}
+__device__ __forceinline__ void sq4(float4& acc, float4 v) {
+  acc.x = fmaf(v.x, v.x, acc.x); acc.y = fmaf(v.y, v.y, acc.y);
+  acc.z = fmaf(v.z, v.z, acc.z); acc.w = fmaf(v.w, v.w, acc.w);
+}
+__device__ __forceinline__ float4 div4(float4 v, float c) {
+  return make_float4(v.x / c, v.y / c, v.z / c, v.w / c);
+}
+
+template <bool MM2, int CT, int CA, int CV>
+__global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  const int UT = a.D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
+  const float* tsrc = a.ids ? a.table : a.text_dense;
+  const float* esrc = a.ids ? a.table : a.emb_dense;
+  const bool split_emb = MM2 && (esrc != tsrc);
+  const bool gather = a.ids != nullptr;
+
+  for (int64_t i = wid; i < a.N; i += nw) {
+    // stage: lane t <- token t (row id or -1, weight)
+    int rid = -1;
+    float w = 0.f;
+    if (lane < a.L) {
+      int64_t off;
+      stage_token(a, i, lane, off, w);
+      rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
+    }
+    const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+    const float sw = wave_sum(w);
+
+    float4 num[CT], sx[CT], sxx[CT], sa[CA], saa[CA], sv[CV], svv[CV];
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < CT; ++c) num[c] = sx[c] = sxx[c] = z4;
+#pragma unroll
+    for (int c = 0; c < CA; ++c) sa[c] = saa[c] = z4;
+#pragma unroll
+    for (int c = 0; c < CV; ++c) sv[c] = svv[c] = z4;
+    const float* abase = a.audio + i * a.L * a.A;
+    const float* vbase = a.visual + i * a.L * a.Vd;
+    const int64_t dbase = i * a.L;
+
+#pragma unroll 2
+    for (int t = 0; t < a.L; ++t) {
+      const int r = __builtin_amdgcn_readlane(rid, t);
+      const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+      if (r >= 0 && (MM2 || wt != 0.f)) {
+        const int64_t o = (gather ? static_cast<int64_t>(r) : dbase + r) * a.D;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const int u = lane + kWave * c;
+          if (u < UT) {
+            const float4 v = ld4(tsrc + o + 4 * u);
+            if (split_emb) {
+              fma4(num[c], wt, ld4(esrc + o + 4 * u));
+            } else {
+              fma4(num[c], wt, v);
+            }
+            if constexpr (MM2) {
+              add4(sx[c], v);
+              sq4(sxx[c], v);
+            }
+          }
+        }
+      }
+      if constexpr (MM2) {
+#pragma unroll
+        for (int c = 0; c < CA; ++c) {
+          const int u = lane + kWave * c;
+          if (u < UA) {
+            const float4 v = ld4(abase + static_cast<int64_t>(t) * a.A + 4 * u);
+            add4(sa[c], v);
+            sq4(saa[c], v);
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CV; ++c) {
+          const int u = lane + kWave * c;
+          if (u < UV) {
+            const float4 v = ld4(vbase + static_cast<int64_t>(t) * a.Vd + 4 * u);
+            add4(sv[c], v);
+            sq4(svv[c], v);
+          }
+        }
+      }
+    }
+
+    if constexpr (MM2) {
+      float* srow = a.s_out + i * a.Kp;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UT) {
+          st4(a.num_out + i * a.D + 4 * u, num[c]);
+          st4(srow + 4 * u, sx[c]);
+          st4(srow + a.D + 4 * u, sxx[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UA) {
+          st4(srow + 2 * a.D + 4 * u, sa[c]);
+          st4(srow + 2 * a.D + a.A + 4 * u, saa[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CV; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UV) {
+          st4(srow + 2 * (a.D + a.A) + 4 * u, sv[c]);
+          st4(srow + 2 * (a.D + a.A) + a.Vd + 4 * u, svv[c]);
+        }
+      }
+      const int k = 2 * (a.D + a.A + a.Vd);
+      for (int f = k + lane; f < a.Kp; f += kWave) srow[f] = 0.f;
+      if (lane == 0) {
+        a.aux_out[i] = cnt;
+        a.aux_out[a.N + i] = sw;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UT) {
+          if (a.num_out) st4(a.num_out + i * a.D + 4 * u, num[c]);
+          if (a.x_out) st4(a.x_out + i * a.D + 4 * u, div4(num[c], cnt));
+        }
+      }
+      if (lane == 0 && a.cnt_out) a.cnt_out[i] = cnt;
+    }
+  }
+}
+
+template <bool MM2, int CT, int CA, int CV>
+static int launch_wave(const StreamArgs& a, hipStream_t stream) {
+  const int64_t blocks = ceil_div(a.N, 4);
+  const int grid = static_cast<int>(blocks < 256 * 8 ? blocks : 256 * 8);
+  utt_wave_kernel<MM2, CT, CA, CV><<<grid, 256, 0, stream>>>(a);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
 __global__ void seq2weight_kernel(const int32_t* __restrict__ seq, const uint8_t* __restrict__ sel,
                                   int64_t total, const double* __restrict__ wtab, int64_t V,
                                   float* __restrict__ w, int32_t* flag) {
@@ -348,6 +509,10 @@ extern "C" int mmb_sif_wavg(const float* table, int64_t v, int d, const int32_t*
   a.N = n; a.L = l; a.D = d;
   a.x_out = x_out; a.num_out = num_out; a.cnt_out = cnt_out; a.flag = flag;
   const bool v4 = (d % 4 == 0) && aligned16(table);
+  if (v4 && l <= kWave && d <= 512 && (x_out == nullptr || aligned16(x_out)) &&
+      (num_out == nullptr || aligned16(num_out))) {
+    return d <= 256 ? launch_wave<false, 1, 1, 1>(a, stream) : launch_wave<false, 2, 1, 1>(a, stream);
+  }
   MMB_REQUIRE(d / (v4 ? 4 : 1) <= kNT && d <= kRedFloats);
   return v4 ? launch_stream<false, 4, 1, 1>(a, stream) : launch_stream<false, 1, 1, 1>(a, stream);
 }
@@ -391,6 +556,20 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   const bool vt = (d % 4 == 0) && (ids ? aligned16(table) : (aligned16(text_dense) && aligned16(emb_dense)));
   const bool va = (a_ % 4 == 0) && aligned16(audio);
   const bool vv = (vd % 4 == 0) && aligned16(visual);
+  if (vt && va && vv && t <= kWave && d <= 512 && a_ <= 512 && vd <= 512 && aligned16(num_out) &&
+      aligned16(s_out)) {
+    const int sel = (d > 256 ? 4 : 0) | (a_ > 256 ? 2 : 0) | (vd > 256 ? 1 : 0);
+    switch (sel) {
+      case 7: return launch_wave<true, 2, 2, 2>(s, stream);
+      case 6: return launch_wave<true, 2, 2, 1>(s, stream);
+      case 5: return launch_wave<true, 2, 1, 2>(s, stream);
+      case 4: return launch_wave<true, 2, 1, 1>(s, stream);
+      case 3: return launch_wave<true, 1, 2, 2>(s, stream);
+      case 2: return launch_wave<true, 1, 2, 1>(s, stream);
+      case 1: return launch_wave<true, 1, 1, 2>(s, stream);
+      default: return launch_wave<true, 1, 1, 1>(s, stream);
+    }
+  }
   MMB_REQUIRE(d / (vt ? 4 : 1) <= kNT && a_ / (va ? 4 : 1) <= kNT && vd / (vv ? 4 : 1) <= kNT);
   const int sel = (vt ? 4 : 0) | (va ? 2 : 0) | (vv ? 1 : 0);
   switch (sel) {

@@ -118,6 +118,78 @@ def get_sentence_embeddings(word_embeddings, weights, text):
     return SIF_embedding(word_embeddings, text, w, 1)
 
 
+def _orth(Z):
+    """Modified Gram-Schmidt, twice (the device solver's orthonormalisation)."""
+    Z = np.array(Z, dtype=np.float64, copy=True)
+    for j in range(Z.shape[1]):
+        for _ in range(2):
+            for i in range(j):
+                Z[:, j] -= (Z[:, i] @ Z[:, j]) * Z[:, i]
+        Z[:, j] /= np.linalg.norm(Z[:, j])
+    return Z
+
+
+def pc_from_gram(G, z0, npc=1, transposed=False, n_iter=7):
+    """CPU restatement of the DEVICE solver (csrc/pc_kernels.hip, mmb_pc_solve):
+    sklearn's randomized SVD evaluated from the Gram G = X^T X alone.
+
+    The reference's iterations build span(G^n_iter Omega) (direct branch) or
+    span(G^n_iter X^T Omega) (transposed branch, n < d): LU / QR normalisers
+    only right-multiply the block, so the span is exact algebra.  Direct: the
+    top right singular vectors of Q^T X, Q = orth(X Z), solve
+    (Z^T G^2 Z) y = s^2 (Z^T G Z) y, v = G Z y.  Transposed: v = Z u, u the
+    top eigenvectors of Z^T G Z.  svd_flip(u_based_decision=False) at the end.
+    """
+    G = np.asarray(G, np.float64)
+    Z = _orth(z0)
+    for _ in range(n_iter):
+        Z = _orth(G @ Z)
+    GZ = G @ Z
+    if transposed:
+        lam, U = np.linalg.eigh(Z.T @ GZ)
+        V = Z @ U[:, ::-1][:, :npc]
+    else:
+        W = Z.T @ GZ
+        H = GZ.T @ GZ
+        Li = np.linalg.inv(np.linalg.cholesky(0.5 * (W + W.T)))
+        lam, U = np.linalg.eigh(Li @ (0.5 * (H + H.T)) @ Li.T)
+        V = GZ @ (Li.T @ U[:, ::-1][:, :npc])
+    V = (V / np.linalg.norm(V, axis=0)).T
+    idx = np.argmax(np.abs(V), axis=1)
+    return V * np.sign(V[np.arange(V.shape[0]), idx])[:, None]
+
+
+class CPUOps:
+    """CPU doubles of the libmmb kernels that pipeline.global_pc composes
+    (torch CPU tensors in/out) — lets the multi-rank orchestration run under
+    gloo in tests."""
+
+    @staticmethod
+    def gram(num, cnt, G=None, ws=None):
+        import torch
+
+        x = (num / cnt[:, None]) if cnt is not None else num
+        x = x.to(torch.float64)
+        return x.T @ x
+
+    @staticmethod
+    def omega(rows, k, device=None):
+        import torch
+
+        return torch.from_numpy(np.random.RandomState(0).normal(size=(rows, k)))
+
+    @staticmethod
+    def xt_omega(num, cnt, om):
+        x = (num / cnt[:, None]) if cnt is not None else num
+        return x.double().T @ om
+
+    @staticmethod
+    def pc_solve(G, z0, npc, transposed):
+        import torch
+
+        return torch.from_numpy(pc_from_gram(G.numpy(), z0.numpy(), npc, transposed))
+
+
 def exact_top_pc(X, npc=1):
     """Exact top right singular vectors (for the spectral-gap discussion only)."""
     _, _, vt = np.linalg.svd(np.asarray(X, np.float64), full_matrices=False)

@@ -119,6 +119,39 @@ def test_sif_vs_oracle_mid_size(gpu, N, L, V):
     assert M.row_rel_err(got, ref) < EMB_TOL
 
 
+@pytest.mark.parametrize("n_total,shards", [(5000, 4), (250, 2)])
+def test_sharded_equals_unsharded_on_one_gpu(gpu, n_total, shards):
+    """The multi-GPU decomposition on one device: per-shard Grams (and X^T Omega
+    rows in the transposed branch, n_total < 300) summed as the all-reduce
+    would, then the same solve — equals the unsharded PC and embeddings."""
+    import distributed as D
+
+    V = 8000
+    E = torch.tensor(synth.word_table(V, 300, seed=11), device=gpu)
+    wt = torch.tensor(synth.sif_weights(V), device=gpu, dtype=torch.float32)
+    ids = torch.as_tensor(synth.token_ids(n_total, 30, V, seed=12, ragged=True), device=gpu)
+    ref, pc_ref = P.sif_embeddings(E, ids, wtab32=wt, out_dtype=torch.float64)
+    k = 1 + P.N_OVERSAMPLES
+    parts, G, z0 = [], None, None
+    for r in range(shards):
+        row0, n = D.shard_range(n_total, shards, r)
+        num, cnt = P.weighted_sum(E, P.narrow_ids(ids[row0:row0 + n]), wtab32=wt)
+        g = P.gram(num, cnt)
+        G = g if G is None else G + g
+        if n_total < 300:
+            om = P.omega(n_total, k, gpu)[row0:row0 + n].contiguous()
+            zr = P.xt_omega(num, cnt, om)
+            z0 = zr if z0 is None else z0 + zr
+        parts.append((num, cnt))
+    transposed = n_total < 300
+    if not transposed:
+        z0 = P.omega(300, k, gpu)
+    pc = P.pc_solve(G, z0, 1, transposed)
+    assert (pc - pc_ref).abs().max().item() < 1e-10
+    out = torch.cat([P.remove_pc(num, cnt, pc, torch.float64) for num, cnt in parts])
+    assert M.row_rel_err(out.cpu().numpy(), ref.cpu().numpy()) < 1e-9
+
+
 def test_device_sif_properties_large(gpu):
     """Size-independent properties at a large N: the output is orthogonal to the
     removed PC, removal is idempotent, and two runs are bit-identical."""
