@@ -113,8 +113,9 @@ int mmb_calc_weights(const float* x, int64_t rows, int f, const float* b_mean,
  *   num[i,:d]  = sum_t w_t E_t                      (weighted text sum)
  *   s[i,:]     = [Sx_e | Sxx_e | Sx_a | Sxx_a | Sx_v | Sxx_v | 0-pad]  (sum
  *                over t of x and x^2 per feature; row stride mmb_mm2_k())
- *   aux[0][i]  = count_nonzero(w), aux[1][i] = sum_t w_t   (planar [2][n]:
- *                aux[0] is the SIF count the Gram / removal kernels take)
+ *   aux[0][i]  = count_nonzero(w), aux[1][i] = sum_t w_t, aux[2][i] = the
+ *                power-of-2 scale putting max|s[i,:]| in [2^14, 2^15) (planar
+ *                [3][n]; aux[0] is the SIF count the Gram / removal kernels take)
  * replaces the frame loops of sif2.estimate_embedding_overall_gpu2
  *   /root/reference/sif2.py:181-205 and the gathers at simplesif.py:862-871 */
 int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const float* wtab32,
@@ -136,7 +137,11 @@ int mmb_mm2_ldw(int d);
  * textaudiovisual (sif2.py:167-174).                                         */
 int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_mu,
                     const float* const* w_ls, const float* const* b_ls, int d, int a, int vd,
-                    int t, float* wm, int ldw, float* c0, hipStream_t stream);
+                    int t, float* wm, int ldw, float* c0, void* wsplit, hipStream_t stream);
+
+/* Bytes of the fp16 hi/lo split of wm written by mmb_mm2_prepare when wsplit
+ * is non-null (transposed [ldw][k] hi and lo planes + per-column 1/scale). */
+size_t mmb_mm2_split_bytes(int d, int a, int vd);
 
 /* cs = (num + s @ wm[:, :d] + c0) / (aux[1] + s @ wm[:, d] + c0[d]);
  * out = cs / ||cs||_2 (fp32 MFMA GEMM + fused epilogue).
@@ -144,6 +149,14 @@ int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_mu,
 int mmb_mm2_project(const float* s, const float* num, const float* aux, const float* wm,
                     int ldw, const float* c0, int64_t n, int k, int d, float* out,
                     hipStream_t stream);
+
+/* The same projection on the fp16 MFMA pipe: s (scaled per row by aux[2]) and
+ * wm (scaled per column) split into fp16 hi + lo, a*b ~ ah*bh + ah*bl + al*bh
+ * (3 f16 MFMAs, ~22-bit operands, fp32 accumulation).  wsplit from
+ * mmb_mm2_prepare.  The bench path.                                          */
+int mmb_mm2_project_x3(const float* s, const float* num, const float* aux, const void* wsplit,
+                       int ldw, const float* c0, int64_t n, int k, int d, float* out,
+                       hipStream_t stream);
 
 /* ---------------------------------------------------------------- a10/a11
  * SentimentModel(d -> h -> o): y = squeeze(W2 relu(W1 x + b1) + b2).

@@ -95,6 +95,157 @@ __global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ Gram v2
+// Upper triangle of G in 16x16 tiles (D <= 320: 20 tile rows, 210 tiles).  A
+// PAIR of 16-wave workgroups owns one contiguous row range: each stages the
+// range's rows once in LDS as f64 (16 rows per chunk, double-buffered, the
+// next chunk's global loads in flight during the current chunk's MFMAs) and
+// computes half of the tiles (~7 per wave, fp64 MFMA 16x16x4 — one k-step is
+// 4 rows).  The pair sits on one XCD (blocks b and b+8) so the second read of
+// the rows hits L2.  Per-range partials are summed in a fixed order.
+constexpr int kG2NT = 1024;
+constexpr int kG2Rows = 16;            // rows per LDS chunk (4 MFMA k-steps)
+constexpr int kG2Stride = 336;         // doubles per LDS row: 320 + 16 (rows alternate bank halves)
+constexpr int kG2MaxTiles = 8;         // tiles per wave
+
+__device__ __forceinline__ void tri_tile(int tau, int nt, int& ti, int& tj) {
+  int r = 0, rem = tau;
+  while (rem >= nt - r) {
+    rem -= nt - r;
+    ++r;
+  }
+  ti = r;
+  tj = r + rem;
+}
+
+__global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict__ num,
+                                                         const float* __restrict__ cnt, int64_t N,
+                                                         int D, int nt, int R, int64_t chunk,
+                                                         int xcd_map, double* __restrict__ part) {
+  extern __shared__ double s_x[];  // [2][kG2Rows][kG2Stride]
+  const int T = nt * (nt + 1) / 2;
+  int half, range;
+  if (xcd_map) {
+    const int b = blockIdx.x;
+    half = (b >> 3) & 1;
+    range = (b & 7) + 8 * (b >> 4);
+  } else {
+    half = blockIdx.x & 1;
+    range = blockIdx.x >> 1;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t0 = half * ((T + 1) / 2), t1 = half ? T : (T + 1) / 2;
+  // this wave's tiles: wave, wave+16, ... within [t0, t1)
+  int ti[kG2MaxTiles], tj[kG2MaxTiles];
+  int ntl = 0;
+#pragma unroll
+  for (int q = 0; q < kG2MaxTiles; ++q) {
+    const int tau = t0 + wave + (kG2NT / kWave) * q;
+    ti[q] = tj[q] = 0;
+    if (tau < t1) {
+      tri_tile(tau, nt, ti[q], tj[q]);
+      ntl = q + 1;
+    }
+  }
+  f64x4 acc[kG2MaxTiles];
+#pragma unroll
+  for (int q = 0; q < kG2MaxTiles; ++q) acc[q] = f64x4{0, 0, 0, 0};
+
+  const int64_t r0 = range * chunk;
+  const int64_t r1 = min(N, r0 + chunk);
+  const int nchunks = static_cast<int>(r1 > r0 ? (r1 - r0 + kG2Rows - 1) / kG2Rows : 0);
+  const int U = D >> 2;  // float4 units per row (D % 4 == 0)
+  // staging map: thread -> (row, float4 unit); 16 rows x 80 units (padded to 320 cols)
+  const int srow = tid / 80, sunit = tid % 80;  // tid < 1280 covers 16 x 80; 1024 threads: 2 passes
+  auto load_regs = [&](int c, float4 (&v)[2], float (&sc)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + kG2NT * q;
+      const int rr = idx / 80, uu = idx % 80;
+      const int64_t row = r0 + static_cast<int64_t>(c) * kG2Rows + rr;
+      v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      sc[q] = 1.f;
+      if (idx < kG2Rows * 80 && row < r1 && uu < U) {
+        v[q] = *reinterpret_cast<const float4*>(num + row * D + 4 * uu);
+        if (cnt) sc[q] = cnt[row];
+      }
+    }
+  };
+  auto store_lds = [&](int buf, const float4 (&v)[2], const float (&sc)[2]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int idx = tid + kG2NT * q;
+      if (idx < kG2Rows * 80) {
+        const int rr = idx / 80, uu = idx % 80;
+        double* dst = s_x + (buf * kG2Rows + rr) * kG2Stride + 4 * uu;
+        // x = num / count in f32 (sif_functions.py:55), then exact f64 widening
+        dst[0] = static_cast<double>(cnt ? v[q].x / sc[q] : v[q].x);
+        dst[1] = static_cast<double>(cnt ? v[q].y / sc[q] : v[q].y);
+        dst[2] = static_cast<double>(cnt ? v[q].z / sc[q] : v[q].z);
+        dst[3] = static_cast<double>(cnt ? v[q].w / sc[q] : v[q].w);
+      }
+    }
+  };
+  (void)srow;
+  (void)sunit;
+  float4 pv[2];
+  float psc[2];
+  if (nchunks > 0) {
+    load_regs(0, pv, psc);
+    store_lds(0, pv, psc);
+  }
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nchunks) load_regs(c + 1, pv, psc);
+    const double* xb = s_x + buf * kG2Rows * kG2Stride;
+#pragma unroll
+    for (int s = 0; s < kG2Rows / 4; ++s) {
+      const double* xr = xb + (4 * s + (lane >> 4)) * kG2Stride + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < kG2MaxTiles; ++q) {
+        if (q < ntl) {
+          const double a = xr[16 * ti[q]];
+          const double b = xr[16 * tj[q]];
+          acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[q], 0, 0, 0);
+        }
+      }
+    }
+    if (c + 1 < nchunks) store_lds(buf ^ 1, pv, psc);
+    __syncthreads();
+  }
+  // partial tiles: part[range][tau][16*16], C/D f64 layout col = lane&15, row = (lane>>4)+4*reg
+  double* pr = part + static_cast<int64_t>(range) * T * 256;
+#pragma unroll
+  for (int q = 0; q < kG2MaxTiles; ++q) {
+    if (q < ntl) {
+      const int tau = t0 + wave + (kG2NT / kWave) * q;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        pr[static_cast<int64_t>(tau) * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[q][reg];
+    }
+  }
+}
+
+__global__ void gram_tri_reduce_kernel(const double* __restrict__ part, int D, int nt, int R,
+                                       int accumulate, double* __restrict__ g) {
+  const int T = nt * (nt + 1) / 2;
+  const int64_t total = static_cast<int64_t>(D) * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int p = static_cast<int>(e / D), q = static_cast<int>(e % D);
+    if (p / 16 > q / 16) {
+      const int t = p; p = q; q = t;
+    }
+    const int bi = p / 16, bj = q / 16;
+    const int tau = bi * nt - bi * (bi - 1) / 2 + (bj - bi);
+    const int64_t off = static_cast<int64_t>(tau) * 256 + (p % 16) * 16 + (q % 16);
+    double sum = 0.0;
+    for (int r = 0; r < R; ++r) sum += part[static_cast<int64_t>(r) * T * 256 + off];
+    g[e] = accumulate ? g[e] + sum : sum;
+  }
+}
+
 // Fixed-order sum over the S row chunks (deterministic), mirrored to both halves.
 __global__ void gram_reduce_kernel(const double* __restrict__ part, int D, int nb, int npairs,
                                    int S, int accumulate, double* __restrict__ g) {
@@ -167,7 +318,7 @@ __device__ void gz_product_mc(const double* __restrict__ G, const double* Z, dou
   for (int j = 0; j < MC; ++j) acc[j] = 0.0;
   const double* gcol = G + p;
   const double* zr = Z + j0;
-#pragma unroll 4
+#pragma unroll 16
   for (int q = 0; q < D; ++q) {
     const double gq = gcol[static_cast<int64_t>(q) * D];
 #pragma unroll
@@ -258,6 +409,74 @@ __device__ void jacobi_wave(double* A, double* V, int k, int lane) {
   }
 }
 
+// Orthonormalise the columns of Z [D][k] with the whole workgroup:
+// column equilibration, then CholeskyQR twice (W = Z^T Z by all waves,
+// Cholesky + triangular inverse by one wave, Z <- Z L^{-T} row-parallel).
+// Falls back to wave-0 MGS^2 if a Cholesky pivot is not positive (only for
+// extreme ill-conditioning, kappa >~ 1e8).
+__device__ void orth_block(double* Z, int D, int k, double* sW, double* sL, double* sLi,
+                           int* s_fail) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  for (int pass = 0; pass < 3; ++pass) {
+    small_gram(Z, Z, sW, D, k);
+    if (tid == 0) *s_fail = 0;
+    __syncthreads();
+    if (pass == 0) {  // equilibrate: unit column norms
+      if (tid < D) {
+        for (int j = 0; j < k; ++j) Z[tid * k + j] *= 1.0 / sqrt(sW[j * k + j]);
+      }
+      __syncthreads();
+      continue;
+    }
+    if (wave == 0) {
+      for (int e = lane; e < k * k; e += kWave) sL[e] = 0.0;
+      wave_lds_sync();
+      for (int j = 0; j < k; ++j) {
+        if (lane == 0) {
+          double s = sW[j * k + j];
+          for (int m = 0; m < j; ++m) s -= sL[j * k + m] * sL[j * k + m];
+          if (!(s > 0.0)) *s_fail = 1;
+          sL[j * k + j] = sqrt(s > 0.0 ? s : 1.0);
+        }
+        wave_lds_sync();
+        if (lane > j && lane < k) {
+          double s = sW[lane * k + j];
+          for (int m = 0; m < j; ++m) s -= sL[lane * k + m] * sL[j * k + m];
+          sL[lane * k + j] = s / sL[j * k + j];
+        }
+        wave_lds_sync();
+      }
+      if (lane < k) {  // Linv column `lane`
+        const int c = lane;
+        for (int i = 0; i < k; ++i) {
+          double s = (i == c) ? 1.0 : 0.0;
+          for (int m = c; m < i; ++m) s -= sL[i * k + m] * sLi[m * k + c];
+          sLi[i * k + c] = (i < c) ? 0.0 : s / sL[i * k + i];
+        }
+      }
+    }
+    __syncthreads();
+    if (*s_fail) {
+      if (wave == 0) orth_wave(Z, D, k, lane);
+      __syncthreads();
+      return;
+    }
+    if (tid < D) {  // row p: z <- z L^{-T}, i.e. z_new[j] = sum_{m<=j} z[m] Linv[j][m]
+      double z[kMaxK];
+#pragma unroll
+      for (int m = 0; m < kMaxK; ++m) z[m] = (m < k) ? Z[tid * k + m] : 0.0;
+      for (int j = 0; j < k; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < kMaxK; ++m)
+          if (m <= j) s += z[m] * sLi[j * k + m];
+        Z[tid * k + j] = s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __device__ void symmetrize(double* M, int k) {
   for (int e = threadIdx.x; e < k * k; e += blockDim.x) {
     const int i = e / k, j = e % k;
@@ -284,17 +503,16 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __rest
   __shared__ int s_order[kMaxK];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
 
+  __shared__ int s_fail;
   for (int e = tid; e < D * k; e += kSolveNT) sZ[e] = z0[e];
   __syncthreads();
-  if (wave == 0) orth_wave(sZ, D, k, lane);
-  __syncthreads();
+  orth_block(sZ, D, k, sW, sL, sLi, &s_fail);
   for (int it = 0; it < n_iter; ++it) {
     gz_product(G, sZ, sGZ, D, k);
     __syncthreads();
     for (int e = tid; e < D * k; e += kSolveNT) sZ[e] = sGZ[e];
     __syncthreads();
-    if (wave == 0) orth_wave(sZ, D, k, lane);
-    __syncthreads();
+    orth_block(sZ, D, k, sW, sL, sLi, &s_fail);
   }
   gz_product(G, sZ, sGZ, D, k);
   __syncthreads();
@@ -550,24 +768,66 @@ static GramPlan gram_plan(int64_t n, int d) {
   return p;
 }
 
+struct Gram2Plan {
+  int nt, T, R, xcd;
+  int64_t chunk;
+};
+
+static Gram2Plan gram2_plan(int64_t n, int d) {
+  Gram2Plan p;
+  p.nt = static_cast<int>(ceil_div(d, 16));
+  p.T = p.nt * (p.nt + 1) / 2;
+  int64_t R = n / 512;
+  if (R < 1) R = 1;
+  if (R > 256) R = 256;
+  if (R >= 8) R = R / 8 * 8;
+  p.R = static_cast<int>(R);
+  p.xcd = (p.R % 8 == 0) ? 1 : 0;
+  p.chunk = ceil_div(n, p.R);
+  return p;
+}
+
+static bool gram2_ok(const float* num, int d) {
+  // 16-wave tile kernel: d <= 320 (20 tile rows, <= 8 tiles per wave per half)
+  return d % 4 == 0 && d <= 320 && (reinterpret_cast<uintptr_t>(num) & 15) == 0;
+}
+
 }  // namespace mmb
 
 using namespace mmb;
 
 extern "C" size_t mmb_gram_workspace_bytes(int64_t n, int d) {
   const GramPlan p = gram_plan(n, d);
-  return static_cast<size_t>(p.S) * p.npairs * kGB * kGB * sizeof(double);
+  const size_t v1 = static_cast<size_t>(p.S) * p.npairs * kGB * kGB * sizeof(double);
+  const Gram2Plan q = gram2_plan(n, d);
+  const size_t v2 = static_cast<size_t>(q.R) * q.T * 256 * sizeof(double);
+  return v1 > v2 ? v1 : v2;
 }
 
 extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, double* g,
                         int accumulate, void* ws, hipStream_t stream) {
   MMB_REQUIRE(num && g && ws && n >= 0 && d > 0);
-  const GramPlan p = gram_plan(n, d);
   double* part = static_cast<double*>(ws);
+  const int64_t total = static_cast<int64_t>(d) * d;
+  if (gram2_ok(num, d)) {
+    const Gram2Plan q = gram2_plan(n, d);
+    const size_t lds = sizeof(double) * 2 * kG2Rows * kG2Stride;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_tri_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      attr = true;
+    }
+    gram_tri_kernel<<<2 * q.R, kG2NT, lds, stream>>>(num, cnt, n, d, q.nt, q.R, q.chunk, q.xcd, part);
+    MMB_LAUNCH_CHECK();
+    gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, q.nt, q.R, accumulate, g);
+    MMB_LAUNCH_CHECK();
+    return MMB_OK;
+  }
+  const GramPlan p = gram_plan(n, d);
   gram_partial_kernel<<<p.npairs * p.S, 256, 0, stream>>>(num, cnt, n, d, p.nb, p.npairs, p.S,
                                                          p.chunk, p.xcd, part);
   MMB_LAUNCH_CHECK();
-  const int64_t total = static_cast<int64_t>(d) * d;
   gram_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, p.nb, p.npairs, p.S, accumulate, g);
   MMB_LAUNCH_CHECK();
   return MMB_OK;

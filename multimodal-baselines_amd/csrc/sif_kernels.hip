@@ -10,6 +10,8 @@
 // image per accumulator in a fixed order (deterministic), and only the
 // reductions leave the chip: the [N,L,300] gathered text tensor the reference
 // materialises (simplesif.py:319-340, :871) never exists.
+#include <cstdlib>
+
 #include "mmb_common.h"
 
 namespace mmb {
@@ -46,6 +48,22 @@ __device__ __forceinline__ void ldv(const float* p, float (&v)[VEC]) {
   } else {
     v[0] = *p;
   }
+}
+
+// Power-of-2 scale that brings a row's max |value| into [2^14, 2^15): the
+// projection GEMM splits the sums into fp16 hi/lo pairs (mm2_kernels.hip) and
+// needs them in fp16's full-precision range.  Exact (a power of two).
+__device__ __forceinline__ float row_scale(float m) {
+  if (!(m > 0.f) || !isfinite(m)) return 1.f;
+  int ex;
+  frexpf(m, &ex);  // m = f * 2^ex, f in [0.5, 1)
+  return ldexpf(1.f, 15 - ex);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
 }
 
 // Resolve token t of utterance i: element offset of its text row (or -1) and
@@ -206,6 +224,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       cnt += s_cnt[w];
       sw += s_sw[w];
     }
+    float smax = 0.f;  // max |sum| of this thread's part of the row (MMB2)
     for (int f = tid; f < a.D; f += kNT) {
       float n_ = 0.f;
       for (int r = 0; r < RT; ++r) n_ += s_red[r * a.D + f];
@@ -218,6 +237,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         a.num_out[i * a.D + f] = n_;
         a.s_out[i * a.Kp + f] = x1;
         a.s_out[i * a.Kp + a.D + f] = x2;
+        smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
       } else {
         if (a.num_out) a.num_out[i * a.D + f] = n_;
         if (a.x_out) a.x_out[i * a.D + f] = n_ / cnt;
@@ -225,7 +245,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
     }
     if (tid == 0) {
       if constexpr (MM2) {
-        a.aux_out[i] = cnt;         // planar [2][N]: row 0 doubles as the SIF count
+        a.aux_out[i] = cnt;         // planar [3][N]: row 0 doubles as the SIF count
         a.aux_out[a.N + i] = sw;
       } else {
         if (a.cnt_out) a.cnt_out[i] = cnt;
@@ -260,6 +280,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         }
         srow[f] = x1;
         srow[a.A + f] = x2;
+        smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
       }
       for (int f = tid; f < a.Vd; f += kNT) {
         float x1 = 0.f, x2 = 0.f;
@@ -269,9 +290,18 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         }
         srow[2 * a.A + f] = x1;
         srow[2 * a.A + a.Vd + f] = x2;
+        smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
       }
       const int k = 2 * (a.D + a.A + a.Vd);
       for (int f = k + tid; f < a.Kp; f += kNT) a.s_out[i * a.Kp + f] = 0.f;
+      smax = wave_max(smax);
+      if (lane == 0) s_cnt[wave] = smax;
+      __syncthreads();
+      if (tid == 0) {
+        float m = 0.f;
+        for (int w = 0; w < kNT / kWave; ++w) m = fmaxf(m, s_cnt[w]);
+        a.aux_out[2 * a.N + i] = row_scale(m);
+      }
     }
     __syncthreads();
   }
@@ -287,6 +317,18 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
 // that the compiler keeps in flight across unrolled frames.
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+using nf4 = float __attribute__((ext_vector_type(4)));
+// Frame streams are read exactly once: NT=true marks them non-temporal so they
+// do not evict the (Zipf-hot) word-table rows from L2 / Infinity Cache.
+template <bool NT>
+__device__ __forceinline__ float4 ldnt4(const float* p) {
+  if constexpr (NT) {
+    const nf4 v = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
 __device__ __forceinline__ void fma4(float4& acc, float w, float4 v) {
   acc.x = fmaf(w, v.x, acc.x); acc.y = fmaf(w, v.y, acc.y);
   acc.z = fmaf(w, v.z, acc.z); acc.w = fmaf(w, v.w, acc.w);
@@ -298,11 +340,14 @@ __device__ __forceinline__ void sq4(float4& acc, float4 v) {
   acc.x = fmaf(v.x, v.x, acc.x); acc.y = fmaf(v.y, v.y, acc.y);
   acc.z = fmaf(v.z, v.z, acc.z); acc.w = fmaf(v.w, v.w, acc.w);
 }
+__device__ __forceinline__ float amax4(float4 v) {
+  return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
 __device__ __forceinline__ float4 div4(float4 v, float c) {
   return make_float4(v.x / c, v.y / c, v.z / c, v.w / c);
 }
 
-template <bool MM2, int CT, int CA, int CV>
+template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
@@ -310,7 +355,7 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
   const int UT = a.D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
   const float* tsrc = a.ids ? a.table : a.text_dense;
   const float* esrc = a.ids ? a.table : a.emb_dense;
-  const bool split_emb = MM2 && (esrc != tsrc);
+  constexpr bool split_emb = MM2 && SPLIT;  // weighted sum over a different dense tensor
   const bool gather = a.ids != nullptr;
 
   for (int64_t i = wid; i < a.N; i += nw) {
@@ -337,49 +382,77 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
     const float* vbase = a.visual + i * a.L * a.Vd;
     const int64_t dbase = i * a.L;
 
-#pragma unroll 2
-    for (int t = 0; t < a.L; ++t) {
-      const int r = __builtin_amdgcn_readlane(rid, t);
-      const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
-      if (r >= 0 && (MM2 || wt != 0.f)) {
-        const int64_t o = (gather ? static_cast<int64_t>(r) : dbase + r) * a.D;
+    // Column offsets clamped into the row so every lane loads unconditionally:
+    // lanes past a row's width read a valid duplicate and never store it.  A
+    // group of UNR frames issues ALL its loads before any accumulation — no
+    // branch separates them, so UNR frames x (CT+CA+CV) 16-B loads per lane
+    // are in flight together (a guarded load per lane would be waited on
+    // right after its branch: one load in flight per wave).
+    int ct[CT], ca[CA], cv[CV];
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          const int u = lane + kWave * c;
-          if (u < UT) {
-            const float4 v = ld4(tsrc + o + 4 * u);
-            if (split_emb) {
-              fma4(num[c], wt, ld4(esrc + o + 4 * u));
-            } else {
-              fma4(num[c], wt, v);
-            }
-            if constexpr (MM2) {
-              add4(sx[c], v);
-              sq4(sxx[c], v);
-            }
-          }
+    for (int c = 0; c < CT; ++c) ct[c] = 4 * min(lane + kWave * c, UT - 1);
+#pragma unroll
+    for (int c = 0; c < CA; ++c) ca[c] = 4 * min(lane + kWave * c, MM2 ? UA - 1 : 0);
+#pragma unroll
+    for (int c = 0; c < CV; ++c) cv[c] = 4 * min(lane + kWave * c, MM2 ? UV - 1 : 0);
+    auto frame = [&](int t, float4 (&vt)[CT], float4 (&ve)[CT], float4 (&va)[CA],
+                     float4 (&vv)[CV], float& wt, bool& ok) {
+      const int r = __builtin_amdgcn_readlane(rid, t);
+      wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+      ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
+      const int64_t o = (gather ? static_cast<int64_t>(ok ? r : 0) : dbase + t) * a.D;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        vt[c] = ld4(tsrc + o + ct[c]);
+        if (split_emb) ve[c] = ld4(esrc + o + ct[c]);
+      }
+      if constexpr (MM2) {
+#pragma unroll
+        for (int c = 0; c < CA; ++c) va[c] = ldnt4<NT>(abase + static_cast<int64_t>(t) * a.A + ca[c]);
+#pragma unroll
+        for (int c = 0; c < CV; ++c) vv[c] = ldnt4<NT>(vbase + static_cast<int64_t>(t) * a.Vd + cv[c]);
+      }
+    };
+    auto accum = [&](float4 (&vt)[CT], float4 (&ve)[CT], float4 (&va)[CA], float4 (&vv)[CV],
+                     float wt, bool ok) {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const float4 v = ok ? vt[c] : z4;
+        fma4(num[c], wt, split_emb ? (ok ? ve[c] : z4) : v);
+        if constexpr (MM2) {
+          add4(sx[c], v);
+          sq4(sxx[c], v);
         }
       }
       if constexpr (MM2) {
 #pragma unroll
         for (int c = 0; c < CA; ++c) {
-          const int u = lane + kWave * c;
-          if (u < UA) {
-            const float4 v = ld4(abase + static_cast<int64_t>(t) * a.A + 4 * u);
-            add4(sa[c], v);
-            sq4(saa[c], v);
-          }
+          add4(sa[c], va[c]);
+          sq4(saa[c], va[c]);
         }
 #pragma unroll
         for (int c = 0; c < CV; ++c) {
-          const int u = lane + kWave * c;
-          if (u < UV) {
-            const float4 v = ld4(vbase + static_cast<int64_t>(t) * a.Vd + 4 * u);
-            add4(sv[c], v);
-            sq4(svv[c], v);
-          }
+          add4(sv[c], vv[c]);
+          sq4(svv[c], vv[c]);
         }
       }
+    };
+    int t = 0;
+    for (; t + UNR <= a.L; t += UNR) {
+      float4 vt[UNR][CT], ve[UNR][CT], va[UNR][CA], vv[UNR][CV];
+      float wt[UNR];
+      bool ok[UNR];
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) frame(t + q, vt[q], ve[q], va[q], vv[q], wt[q], ok[q]);
+#pragma unroll
+      for (int q = 0; q < UNR; ++q) accum(vt[q], ve[q], va[q], vv[q], wt[q], ok[q]);
+    }
+    for (; t < a.L; ++t) {
+      float4 vt[CT], ve[CT], va[CA], vv[CV];
+      float wt;
+      bool ok;
+      frame(t, vt, ve, va, vv, wt, ok);
+      accum(vt, ve, va, vv, wt, ok);
     }
 
     if constexpr (MM2) {
@@ -411,9 +484,18 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       }
       const int k = 2 * (a.D + a.A + a.Vd);
       for (int f = k + lane; f < a.Kp; f += kWave) srow[f] = 0.f;
+      float m = 0.f;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
+#pragma unroll
+      for (int c = 0; c < CA; ++c) m = fmaxf(m, fmaxf(amax4(sa[c]), amax4(saa[c])));
+#pragma unroll
+      for (int c = 0; c < CV; ++c) m = fmaxf(m, fmaxf(amax4(sv[c]), amax4(svv[c])));
+      m = wave_max(m);
       if (lane == 0) {
-        a.aux_out[i] = cnt;
+        a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | fp16 row scale
         a.aux_out[a.N + i] = sw;
+        a.aux_out[2 * a.N + i] = row_scale(m);
       }
     } else {
 #pragma unroll
@@ -429,11 +511,126 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
   }
 }
 
-template <bool MM2, int CT, int CA, int CV>
-static int launch_wave(const StreamArgs& a, hipStream_t stream) {
+// MMB2 wave kernel, unified column space: the three rows of a frame (gathered
+// text row, audio frame, visual frame) are (D + A + Vd) / 4 float4 units
+// (225 at 3 x 300) spread over the 64 lanes, UPL units per lane, fixed for the
+// whole utterance.  Every frame is UPL fully-used 16-B load instructions
+// (vs. 6 half-empty ones per frame with a lane map per modality) and the loop
+// body has no branch, so the unrolled frames' loads are all in flight together.
+template <int UPL>
+__global__ __launch_bounds__(256) void utt_wave3_kernel(StreamArgs a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  const int UT = a.D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
+  const int UTOT = UT + UA + UV;
+  const float* tsrc = a.ids ? a.table : a.text_dense;
+  const float* esrc = a.ids ? a.table : a.emb_dense;
+  const bool split_emb = esrc != tsrc;
+  const bool gather = a.ids != nullptr;
+  // per-lane unit descriptors: modality m (0 text, 1 audio, 2 visual), float offset in its row
+  int um[UPL], uo[UPL];
+  bool uok[UPL];
+#pragma unroll
+  for (int j = 0; j < UPL; ++j) {
+    const int u = lane + kWave * j;
+    uok[j] = u < UTOT;
+    um[j] = u < UT ? 0 : (u < UT + UA ? 1 : 2);
+    uo[j] = 4 * (um[j] == 0 ? u : (um[j] == 1 ? u - UT : u - UT - UA));
+    if (!uok[j]) { um[j] = 1; uo[j] = 0; }  // harmless in-bounds reads, never stored
+  }
+  // output offsets in the sums row: Sx_m at seg, Sxx_m at seg + width
+  int sxo[UPL], sqo[UPL];
+#pragma unroll
+  for (int j = 0; j < UPL; ++j) {
+    const int seg = um[j] == 0 ? 0 : (um[j] == 1 ? 2 * a.D : 2 * (a.D + a.A));
+    const int wdt = um[j] == 0 ? a.D : (um[j] == 1 ? a.A : a.Vd);
+    sxo[j] = seg + uo[j];
+    sqo[j] = seg + wdt + uo[j];
+  }
+
+  for (int64_t i = wid; i < a.N; i += nw) {
+    int rid = -1;
+    float w = 0.f;
+    if (lane < a.L) {
+      int64_t off;
+      stage_token(a, i, lane, off, w);
+      rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
+    }
+    const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+    const float sw = wave_sum(w);
+
+    float4 num[UPL], sx[UPL], sxx[UPL];
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < UPL; ++j) num[j] = sx[j] = sxx[j] = z4;
+    const float* abase = a.audio + i * a.L * a.A;
+    const float* vbase = a.visual + i * a.L * a.Vd;
+    const int64_t dbase = i * a.L;
+
+#pragma unroll 4
+    for (int t = 0; t < a.L; ++t) {
+      const int r = __builtin_amdgcn_readlane(rid, t);
+      const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+      const bool ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
+      const int64_t toff = (gather ? static_cast<int64_t>(ok ? r : 0) : dbase + t) * a.D;
+      const float* trow = tsrc + toff;
+      const float* arow = abase + static_cast<int64_t>(t) * a.A;
+      const float* vrow = vbase + static_cast<int64_t>(t) * a.Vd;
+#pragma unroll
+      for (int j = 0; j < UPL; ++j) {
+        const float* p = (um[j] == 0 ? trow : (um[j] == 1 ? arow : vrow)) + uo[j];
+        float4 v = ld4(p);
+        if (um[j] == 0 && !ok) v = z4;
+        add4(sx[j], v);
+        sq4(sxx[j], v);
+        if (um[j] == 0) {
+          if (split_emb) v = ok ? ld4(esrc + toff + uo[j]) : z4;
+          fma4(num[j], wt, v);
+        }
+      }
+    }
+
+    float* srow = a.s_out + i * a.Kp;
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < UPL; ++j) {
+      if (uok[j]) {
+        st4(srow + sxo[j], sx[j]);
+        st4(srow + sqo[j], sxx[j]);
+        if (um[j] == 0) st4(a.num_out + i * a.D + uo[j], num[j]);
+        m = fmaxf(m, fmaxf(amax4(sx[j]), amax4(sxx[j])));
+      }
+    }
+    const int k = 2 * (a.D + a.A + a.Vd);
+    for (int f = k + lane; f < a.Kp; f += kWave) srow[f] = 0.f;
+    m = wave_max(m);
+    if (lane == 0) {
+      a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | fp16 row scale
+      a.aux_out[a.N + i] = sw;
+      a.aux_out[2 * a.N + i] = row_scale(m);
+    }
+  }
+}
+
+template <int UPL>
+static int launch_wave3(const StreamArgs& a, hipStream_t stream) {
   const int64_t blocks = ceil_div(a.N, 4);
   const int grid = static_cast<int>(blocks < 256 * 8 ? blocks : 256 * 8);
-  utt_wave_kernel<MM2, CT, CA, CV><<<grid, 256, 0, stream>>>(a);
+  utt_wave3_kernel<UPL><<<grid, 256, 0, stream>>>(a);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false>
+static int launch_wave(const StreamArgs& a, hipStream_t stream, int grid_cap = 256 * 8) {
+  const int64_t blocks = ceil_div(a.N, 4);
+  const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
+  if (MM2 && a.ids == nullptr && a.emb_dense != a.text_dense) {
+    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, true><<<grid, 256, 0, stream>>>(a);
+  } else {
+    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, false><<<grid, 256, 0, stream>>>(a);
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -556,6 +753,34 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   const bool vt = (d % 4 == 0) && (ids ? aligned16(table) : (aligned16(text_dense) && aligned16(emb_dense)));
   const bool va = (a_ % 4 == 0) && aligned16(audio);
   const bool vv = (vd % 4 == 0) && aligned16(visual);
+  // experiment selector (tools/kernel_bench.py sweeps; unset = default path)
+  static const char* cfg = getenv("MMB_STREAM_CFG");
+  if (cfg && vt && va && vv && t <= kWave && d > 256 && d <= 512 && a_ > 256 && a_ <= 512 &&
+      vd > 256 && vd <= 512 && aligned16(num_out) && aligned16(s_out)) {
+    const int c = atoi(cfg);
+    switch (c) {
+      case 1: return launch_wave<true, 2, 2, 2, 1, false>(s, stream);
+      case 2: return launch_wave<true, 2, 2, 2, 2, false>(s, stream);
+      case 3: return launch_wave<true, 2, 2, 2, 4, false>(s, stream);
+      case 4: return launch_wave<true, 2, 2, 2, 1, true>(s, stream);
+      case 5: return launch_wave<true, 2, 2, 2, 2, true>(s, stream);
+      case 6: return launch_wave<true, 2, 2, 2, 4, true>(s, stream);
+      case 7: return launch_wave<true, 2, 2, 2, 2, true>(s, stream, 256 * 4);
+      case 8: return launch_wave<true, 2, 2, 2, 2, true>(s, stream, 256 * 16);
+      case 9: return launch_wave3<4>(s, stream);
+      default: break;
+    }
+  }
+  if (!cfg && vt && va && vv && t <= kWave && aligned16(num_out) && aligned16(s_out) &&
+      (d + a_ + vd) / 4 <= 4 * kWave && false) {
+    const int upl = static_cast<int>(ceil_div((d + a_ + vd) / 4, kWave));
+    switch (upl) {
+      case 1: return launch_wave3<1>(s, stream);
+      case 2: return launch_wave3<2>(s, stream);
+      case 3: return launch_wave3<3>(s, stream);
+      default: return launch_wave3<4>(s, stream);
+    }
+  }
   if (vt && va && vv && t <= kWave && d <= 512 && a_ <= 512 && vd <= 512 && aligned16(num_out) &&
       aligned16(s_out)) {
     const int sel = (d > 256 ? 4 : 0) | (a_ > 256 ? 2 : 0) | (vd > 256 ? 1 : 0);

@@ -44,8 +44,10 @@ SIGNATURES = {
     "mmb_mm2_ldw": (_I, [_I]),
     "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P,
                             _P, _P]),
-    "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
+    "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
+    "mmb_mm2_split_bytes": (_S, [_I, _I, _I]),
     "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
+    "mmb_mm2_project_x3": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
     "mmb_mlp_forward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_eval": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_workspace_bytes": (_S, [_I, _I]),

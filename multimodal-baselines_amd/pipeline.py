@@ -225,6 +225,8 @@ class MMB2Projection:
         self.kp, self.ldw = mm2_dims(d, a, vd)
         self.wm = torch.empty((self.kp, self.ldw), dtype=torch.float32, device=device)
         self.c0 = torch.empty((self.ldw,), dtype=torch.float32, device=device)
+        nbytes = L.query("mmb_mm2_split_bytes", d, a, vd)
+        self.wsplit = torch.empty((nbytes + 15) // 16 * 16, dtype=torch.uint8, device=device)
         self.params = []
         for k in MMB2_KEYS:  # KeyError for a missing combination, like sif2.py:182
             mu, ls = networks[k]
@@ -235,7 +237,7 @@ class MMB2Projection:
     def refresh(self):
         arr = lambda i: (ctypes_ptr_array([p[i].data_ptr() for p in self.params]))
         L.call("mmb_mm2_prepare", arr(0), arr(1), arr(2), arr(3), self.d, self.a, self.vd, self.t,
-               L.ptr(self.wm), self.ldw, L.ptr(self.c0), L.stream_ptr())
+               L.ptr(self.wm), self.ldw, L.ptr(self.c0), L.ptr(self.wsplit), L.stream_ptr())
 
 
 def ctypes_ptr_array(ptrs):
@@ -251,7 +253,7 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
     if out is None:
         out = (torch.empty((n, d), dtype=torch.float32, device=dev),
                torch.empty((n, kp), dtype=torch.float32, device=dev),
-               torch.empty((2, n), dtype=torch.float32, device=dev))
+               torch.empty((3, n), dtype=torch.float32, device=dev))
     num, s, aux = out
     V = table.shape[0] if table is not None else 0
     L.call("mmb_mm2_stream", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32), L.ptr(text_dense),
@@ -260,12 +262,18 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
     return num, s, aux
 
 
-def mm2_project(s, num, aux, proj: MMB2Projection, out=None):
+def mm2_project(s, num, aux, proj: MMB2Projection, out=None, fp32_mfma: bool = False):
+    """Default: fp16 hi/lo split MFMA GEMM (mmb_mm2_project_x3); fp32_mfma=True
+    selects the plain fp32-MFMA kernel (same epilogue)."""
     n = num.shape[0]
     if out is None:
         out = torch.empty((n, proj.d), dtype=torch.float32, device=num.device)
-    L.call("mmb_mm2_project", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wm), proj.ldw,
-           L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
+    if fp32_mfma:
+        L.call("mmb_mm2_project", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wm), proj.ldw,
+               L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
+    else:
+        L.call("mmb_mm2_project_x3", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wsplit),
+               proj.ldw, L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
     return out
 
 
@@ -296,7 +304,7 @@ class FusedStep:
         kp = self.proj.kp
         self.num = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.s = torch.empty((self.n, kp), dtype=torch.float32, device=dev)
-        self.aux = torch.empty((2, self.n), dtype=torch.float32, device=dev)
+        self.aux = torch.empty((3, self.n), dtype=torch.float32, device=dev)
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
         self.gws = GramWorkspace(self.n, self.d, dev)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)

@@ -131,6 +131,36 @@ def test_fused_step_vs_oracle(gpu, N, T, A, Vd):
     assert M.row_rel_err(mm2_out.cpu().numpy(), ref_mm2) < TOL
 
 
+@pytest.mark.parametrize("scale,pad", [(1.0, 0.0), (100.0, 0.3), (1e-3, 0.0)])
+def test_fp16_split_projection_vs_fp32_and_oracle(gpu, scale, pad):
+    """The fp16 hi/lo split GEMM (bench path) and the fp32-MFMA GEMM both meet
+    the 1e-5 bar, also for frames of very large / very small magnitude (the
+    per-row and per-column power-of-2 scaling keeps fp16 in range)."""
+    N, T, A, Vd, V = 700, 40, 300, 300, 5000
+    torch.manual_seed(3)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None)
+    E = synth.word_table(V, 300, seed=4) * np.float32(scale)
+    wt = synth.sif_weights(V)
+    ids = synth.token_ids(N, T, V, seed=5, ragged=True)
+    audio = synth.frames(N, T, A, seed=6, pad_frac=pad) * np.float32(scale)
+    visual = synth.frames(N, T, Vd, seed=7, pad_frac=pad) * np.float32(scale)
+    ids32 = torch.as_tensor(ids, dtype=torch.int32, device=gpu)
+    au, vi = torch.tensor(audio, device=gpu), torch.tensor(visual, device=gpu)
+    proj = P.MMB2Projection(gen.to(gpu).networks(), 300, A, Vd, T, gpu)
+    num, s, aux = P.mm2_stream(N, T, 300, A, Vd, au, vi, ids32=ids32,
+                               table=torch.tensor(E, device=gpu),
+                               wtab32=torch.tensor(wt, device=gpu, dtype=torch.float32))
+    x3 = P.mm2_project(s, num, aux, proj).cpu().numpy()
+    f32 = P.mm2_project(s, num, aux, proj, fp32_mfma=True).cpu().numpy()
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    text = E[ids]
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                            M.params_from_module(gen.cpu()), sw, text)
+    assert M.row_rel_err(x3, ref) < TOL
+    assert M.row_rel_err(f32, ref) < TOL
+    assert M.row_rel_err(x3, f32) < TOL
+
+
 def test_fused_step_large_properties(gpu):
     """At 100k utterances x 40 frames x 3 x 300: unit rows, finite, deterministic."""
     N, T, V = 100_000, 40, 200_000
