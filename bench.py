@@ -89,6 +89,9 @@ def main():
     ap.add_argument("--utts-per-gpu", type=int, default=1_000_000)
     ap.add_argument("--tokens", type=int, default=40)
     ap.add_argument("--vocab", type=int, default=400_000)
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="row chunks per step (stream of chunk c+1 overlaps projection of c); "
+                         "default 1")
     ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -123,42 +126,25 @@ def main():
             dist.all_reduce(t)
 
     step = P.FusedStep(inp, gen.networks(), allreduce=allreduce if world > 1 else None,
-                       n_total=U * world, row0=rank * U)
+                       n_total=U * world, row0=rank * U, chunks=args.chunks)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step.run()
     torch.cuda.synchronize()
 
-    # timed region: K steps, barrier + sync on both sides; HIP events on the
-    # launch stream around the dominant kernel (mm2_stream) of every step
+    # timed region: K steps, barrier + sync on both sides.  HIP events are
+    # recorded on the stream each phase is launched on (FusedStep.run trace):
+    # the stream kernel's chunks on the caller's stream, projection + Gram of
+    # each chunk on the side stream they overlap on.
     assert U * world >= D  # sklearn's direct (non-transposed) randomized-SVD branch
-    z0 = P.omega(D, 1 + P.N_OVERSAMPLES, dev)
-    E = lambda: torch.cuda.Event(enable_timing=True)
-    ev = [[E() for _ in range(7)] for _ in range(args.steps)]
+    traces = [dict() for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        e = ev[k]
-        e[0].record()
-        P.mm2_stream(step.n, step.t, step.d, step.a, step.vd, inp["audio"], inp["visual"],
-                     ids32=inp["ids"], table=inp["table"], wtab32=inp["wtab"], flag=step.flag,
-                     out=(step.num, step.s, step.aux))
-        e[1].record()
-        cnt = step.aux[0]
-        P.gram(step.num, cnt, step.G, ws=step.gws)
-        e[2].record()
-        allreduce(step.G)
-        e[3].record()
-        pc = P.pc_solve(step.G, z0, 1, False)
-        e[4].record()
-        P.remove_pc(step.num, cnt, pc, out=step.sif)
-        e[5].record()
-        step.proj.refresh()
-        P.mm2_project(step.s, step.num, step.aux, step.proj, out=step.mmb2)
-        e[6].record()
+        step.run(trace=traces[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -170,28 +156,30 @@ def main():
     if int(step.flag.item()) != 0:
         raise RuntimeError("id range flag set")
 
-    names = ["mm2_stream", "gram", "allreduce", "pc_solve", "pc_remove", "mm2_prepare+project"]
-    phase_ms = {n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps
-                for i, n in enumerate(names)}
+    names = sorted({n for tr in traces for n in tr})
+    phase_ms = {n: sum(a.elapsed_time(b) for tr in traces for a, b in tr.get(n, ()))
+                / args.steps for n in names}
+    n_launch = sum(len(tr["mm2_stream"]) for tr in traces)
+    stream_launch_ms = phase_ms["mm2_stream"] * args.steps / n_launch
     ms_per_step = elapsed * 1e3 / args.steps
     total_utts = U * world * args.steps
     value = total_utts / elapsed
 
     if rank == 0:
         kb = stream_kernel_bytes(T, D, 300, 300)
-        stream_s = phase_ms["mm2_stream"] / 1e3
-        achieved = kb * U / stream_s / 1e9
+        utts_per_launch = U / len(step.bounds)
+        achieved = kb * utts_per_launch / (stream_launch_ms / 1e3) / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("utts_per_launch") == U and tj.get("tokens") == T:
+            if tj.get("utts_per_launch") == utts_per_launch and tj.get("tokens") == T:
                 traffic = tj.get("mm2_stream_hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "utt_stream_kernel (mmb_mm2_stream)",
-                "algorithmic_bytes_per_utt": kb, "utts_per_launch": U,
-                "avg_launch_ms": round(phase_ms["mm2_stream"], 4)}
+                "algorithmic_bytes_per_utt": kb, "utts_per_launch": utts_per_launch,
+                "avg_launch_ms": round(stream_launch_ms, 4)}
         pb = path_bytes(T, D, 300, 300)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -221,6 +209,7 @@ def main():
             "path_roofline": {"bytes_per_utt": pb, "achieved": round(pb * U * world / (ms_per_step / 1e3) / world / 1e9, 1),
                               "unit": "GB/s per GPU", "peak": HBM_PEAK_GBS},
             "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
+            "chunks": len(step.bounds),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -241,6 +241,9 @@ __global__ __launch_bounds__(256) void mm2_project_kernel(const float* __restric
 // 5.3x fewer MFMA cycles than fp32 MFMA at fp32-class accuracy.
 // f16 32x32x16: lane l holds A[l&31][8(l>>5)+j] and B[8(l>>5)+j][l&31], j<8.
 using half8 = __attribute__((ext_vector_type(8))) _Float16;
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using half4 = __attribute__((ext_vector_type(4))) _Float16;
 
 constexpr int kXM = 128;  // rows per workgroup (8 waves: 4 row tiles x 2 column halves)
 constexpr int kXK = 32;   // K chunk (2 MFMA k-steps)
@@ -275,20 +278,41 @@ __global__ void mm2_split_wm_kernel(const float* __restrict__ wm, int Kp, int ld
   if (tid == 0) col_inv[j] = 1.f / sc;
 }
 
+// LDS image of one K chunk: A hi, A lo [kXM][kXS], B hi, B lo [LDW][kXS]
+// halves; each lo plane sits 32 halves past its hi plane's end so the hi and
+// lo 16-byte stores of one 8-lane group land on disjoint banks
+constexpr int kXPad = 32;
 template <int CT>
-__global__ __launch_bounds__(512) void mm2_project_x3_kernel(
+constexpr int x3_buf_halves() { return 2 * (kXM * kXS + kXPad) + 2 * (64 * CT * kXS + kXPad); }
+template <int CT>
+constexpr size_t x3_lds_bytes() {
+  return 2 * x3_buf_halves<CT>() * sizeof(_Float16) + 4 * kXM * sizeof(float);
+}
+// MR = 32-row MFMA tiles per wave: the 128 x LDW block is split over
+// (4 / MR) x 2 waves, each owning MR x CT tiles of 32 x 32
+template <int MR>
+constexpr int x3_threads() { return 64 * 2 * (4 / MR); }
+
+template <int CT, int MR>
+__global__ __launch_bounds__(x3_threads<MR>()) void mm2_project_x3_kernel(
     const float* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
     const _Float16* __restrict__ wth, const _Float16* __restrict__ wtl,
     const float* __restrict__ col_inv, const float* __restrict__ c0, int64_t N, int Kp, int D,
     float* __restrict__ out) {
   constexpr int LDW = 64 * CT;
-  __shared__ __attribute__((aligned(16))) _Float16 sAh[kXM * kXS], sAl[kXM * kXS];
-  __shared__ __attribute__((aligned(16))) _Float16 sBh[LDW * kXS], sBl[LDW * kXS];
-  __shared__ float s_rs[kXM];
-  __shared__ float s_tot[kXM];
-  __shared__ float s_ss[2][kXM];
+  constexpr int BUF = x3_buf_halves<CT>();
+  constexpr int kXT = x3_threads<MR>();
+  constexpr int AQ = kXM * 8 / kXT;   // float4 A pieces per thread per chunk
+  constexpr int BQ = LDW * 8 / kXT;   // 16-byte B pieces per thread per chunk
+  constexpr int OA = 0, OAL = kXM * kXS + kXPad;
+  constexpr int OB = 2 * OAL, OBL = OB + LDW * kXS + kXPad;
+  // one dynamic LDS array: two chunk buffers, then the per-row scalars
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  float* s_rs = reinterpret_cast<float*>(lds + 2 * BUF);
+  float* s_tot = s_rs + kXM;
+  float(*s_ss)[kXM] = reinterpret_cast<float(*)[kXM]>(s_tot + kXM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave >> 1, wc = wave & 1;  // rows wr*32*MR + [0,32*MR), tiles wc*CT + [0,CT)
   const int hl = lane >> 5, cl = lane & 31;
   const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
   const float* rscale = aux + 2 * N;
@@ -296,78 +320,134 @@ __global__ __launch_bounds__(512) void mm2_project_x3_kernel(
   if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? rscale[n0 + tid] : 1.f;
   __syncthreads();
 
-  f32x16 acc[CT];
+  f32x16 acc[MR][CT];
 #pragma unroll
-  for (int t = 0; t < CT; ++t)
+  for (int i = 0; i < MR; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
 
-  // register double buffer: the next K chunk's global loads are issued before
-  // the current chunk's MFMAs and land in LDS after them (latency hidden)
-  float4 pa[2];
-  uint4 pb[CT];  // LDW*8 16-byte pieces / 512 threads == CT per thread
-  auto load_chunk = [&](int k0) {
+  // Software pipeline over K chunks of kXK, two LDS buffers, one barrier per
+  // chunk.  Iteration c: the fragments of both k-steps of chunk c are read
+  // from buffer c&1 up front, the first k-step's MFMAs run while the
+  // registers holding chunk c+1 are converted and stored into the other
+  // buffer and the global loads of B(c+2) and A(c+3) are issued, then the
+  // second k-step's MFMAs.  A (the s rows, streamed once from HBM) is
+  // prefetched through a ring of two register sets, B (the split weights,
+  // L2-resident) through one.  Loads are unconditional (rows clamped to N-1,
+  // chunks past the end re-read the last) so no load is branched around; A
+  // loads are non-temporal to spare L2 for B.
+  f32x4 pa0[AQ], pa1[AQ];
+  u32x4 pb[BQ];
+  const float* arow[AQ];
+  const _Float16* bcol[BQ];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int idx = tid + 512 * q;
-      const int row = idx >> 3, c4 = idx & 7;
-      pa[q] = (n0 + row < N) ? *reinterpret_cast<const float4*>(S + (n0 + row) * Kp + k0 + c4 * 4)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  for (int q = 0; q < AQ; ++q) {
+    const int idx = tid + kXT * q;
+    const int64_t row = min(n0 + (idx >> 3), N - 1);
+    arow[q] = S + row * Kp + (idx & 7) * 4;
+  }
 #pragma unroll
-    for (int q = 0; q < CT; ++q) {
-      const int idx = tid + 512 * q;
-      const int col = idx >> 3, part = idx & 7;
-      const int plane = part >> 2, qq = part & 3;
-      pb[q] = *reinterpret_cast<const uint4*>((plane ? wtl : wth) + static_cast<int64_t>(col) * Kp +
-                                              k0 + qq * 8);
-    }
+  for (int q = 0; q < BQ; ++q) {
+    const int idx = tid + kXT * q;
+    const int col = idx >> 3, part = idx & 7;
+    bcol[q] = ((part >> 2) ? wtl : wth) + static_cast<int64_t>(col) * Kp + (part & 3) * 8;
+  }
+  const int nch = Kp / kXK;
+  auto load_a = [&](f32x4(&pa)[AQ], int c) {
+    const int k = min(c, nch - 1) * kXK;
+#pragma unroll
+    for (int q = 0; q < AQ; ++q)
+      pa[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(arow[q] + k));
   };
-  load_chunk(0);
-  for (int k0 = 0; k0 < Kp; k0 += kXK) {
-    // A: 128 rows x 32 fp32 -> scaled fp16 hi/lo
+  auto load_b = [&](int c) {
+    const int k = min(c, nch - 1) * kXK;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int idx = tid + 512 * q;
+    for (int q = 0; q < BQ; ++q) pb[q] = *reinterpret_cast<const u32x4*>(bcol[q] + k);
+  };
+  auto stage = [&](const f32x4(&pa)[AQ], _Float16* buf) {
+    // A: 128 rows x 32 fp32 -> row-scaled fp16 hi/lo
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) {
+      const int idx = tid + kXT * q;
       const int row = idx >> 3, c4 = idx & 7;
       const float sc = s_rs[row];
-      const float x[4] = {pa[q].x * sc, pa[q].y * sc, pa[q].z * sc, pa[q].w * sc};
-      _Float16* ph = sAh + row * kXS + c4 * 4;
-      _Float16* pl = sAl + row * kXS + c4 * 4;
+      half4 h, l;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const _Float16 h = static_cast<_Float16>(x[e]);
-        ph[e] = h;
-        pl[e] = static_cast<_Float16>(x[e] - static_cast<float>(h));
+        const float x = pa[q][e] * sc;
+        h[e] = static_cast<_Float16>(x);
+        l[e] = static_cast<_Float16>(x - static_cast<float>(h[e]));
       }
+      *reinterpret_cast<half4*>(buf + OA + row * kXS + c4 * 4) = h;
+      *reinterpret_cast<half4*>(buf + OAL + row * kXS + c4 * 4) = l;
     }
     // B: LDW columns x 32 halves per plane = 4 x 16 B per column per plane
 #pragma unroll
-    for (int q = 0; q < CT; ++q) {
-      const int idx = tid + 512 * q;
+    for (int q = 0; q < BQ; ++q) {
+      const int idx = tid + kXT * q;
       const int col = idx >> 3, part = idx & 7;
-      const int plane = part >> 2, qq = part & 3;
-      *reinterpret_cast<uint4*>((plane ? sBl : sBh) + col * kXS + qq * 8) = pb[q];
+      *reinterpret_cast<u32x4*>(buf + ((part >> 2) ? OBL : OB) + col * kXS + (part & 3) * 8) =
+          pb[q];
     }
-    __syncthreads();
-    if (k0 + kXK < Kp) load_chunk(k0 + kXK);
+  };
+  struct Frag {
+    half8 ah[MR], al[MR], bh[CT], bl[CT];
+  };
+  auto read_frag = [&](const _Float16* buf, int s, Frag& f) {
+    const int ko = 16 * s + 8 * hl;
 #pragma unroll
-    for (int s = 0; s < kXK / 16; ++s) {
-      const int ko = 16 * s + 8 * hl;
-      const half8 ah = *reinterpret_cast<const half8*>(sAh + (wr * 32 + cl) * kXS + ko);
-      const half8 al = *reinterpret_cast<const half8*>(sAl + (wr * 32 + cl) * kXS + ko);
+    for (int i = 0; i < MR; ++i) {
+      const int row = (wr * MR + i) * 32 + cl;
+      f.ah[i] = *reinterpret_cast<const half8*>(buf + OA + row * kXS + ko);
+      f.al[i] = *reinterpret_cast<const half8*>(buf + OAL + row * kXS + ko);
+    }
 #pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int col = (wc * CT + t) * 32 + cl;
-        const half8 bh = *reinterpret_cast<const half8*>(sBh + col * kXS + ko);
-        const half8 bl = *reinterpret_cast<const half8*>(sBl + col * kXS + ko);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[t], 0, 0, 0);
+    for (int t = 0; t < CT; ++t) {
+      const int col = (wc * CT + t) * 32 + cl;
+      f.bh[t] = *reinterpret_cast<const half8*>(buf + OB + col * kXS + ko);
+      f.bl[t] = *reinterpret_cast<const half8*>(buf + OBL + col * kXS + ko);
+    }
+  };
+  auto mfma = [&](const Frag& f) {
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[t], acc[i][t], 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[t], acc[i][t], 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[t], acc[i][t], 0, 0, 0);
       }
-    }
+  };
+  // iteration c: buffer `cur` holds chunk c, `nxt` holds A(c+1) (pb holds
+  // B(c+1)), the other ring set holds A(c+2) in flight
+  auto iter = [&](int c, f32x4(&nxt)[AQ], const _Float16* cur, _Float16* oth) {
+    Frag f0, f1;
+    read_frag(cur, 0, f0);
+    read_frag(cur, 1, f1);
+    mfma(f0);
+    stage(nxt, oth);
+    load_b(c + 2);
+    load_a(nxt, c + 3);
+    mfma(f1);
     __syncthreads();
+  };
+  _Float16* buf0 = lds;
+  _Float16* buf1 = lds + BUF;
+  load_a(pa0, 0);
+  load_b(0);
+  load_a(pa1, 1);
+  stage(pa0, buf0);
+  load_b(1);
+  load_a(pa0, 2);
+  __syncthreads();
+  int c = 0;
+  for (; c + 1 < nch; c += 2) {
+    iter(c, pa1, buf0, buf1);
+    iter(c + 1, pa0, buf1, buf0);
   }
+  if (c < nch) iter(c, pa1, buf0, buf1);
 
   // epilogue (as mm2_project_kernel): unscale, add weighted text sum + c0,
   // divide by the total weight (column D), L2-normalise the row
@@ -376,61 +456,77 @@ __global__ __launch_bounds__(512) void mm2_project_x3_kernel(
     const int col = (wc * CT + t) * 32 + cl;
     const float ci = col_inv[col];
 #pragma unroll
+    for (int i = 0; i < MR; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int64_t row = n0 + rl;
+        float y = acc[i][t][r] * (ci / s_rs[rl]);
+        if (row < N) {
+          if (col < D) y += num[row * D + col] + c0[col];
+          else if (col == D) y += aux[N + row] + c0[D];
+        }
+        acc[i][t][r] = y;
+        if (col == D) s_tot[rl] = y;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MR; ++i) {
+    float ss[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ss[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int col = (wc * CT + t) * 32 + cl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const float cs = acc[i][t][r] / s_tot[rl];
+        acc[i][t][r] = cs;
+        if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
+      }
+    }
+#pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float sum = half_sum(ss[r]);
+      if (cl == 0) s_ss[wc][(wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = sum;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = (wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
       const int64_t row = n0 + rl;
-      float y = acc[t][r] * (ci / s_rs[rl]);
+      const float inv = 1.f / sqrtf(s_ss[0][rl] + s_ss[1][rl]);
       if (row < N) {
-        if (col < D) y += num[row * D + col] + c0[col];
-        else if (col == D) y += aux[N + row] + c0[D];
-      }
-      acc[t][r] = y;
-      if (col == D) s_tot[rl] = y;
-    }
-  }
-  __syncthreads();
-  float ss[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) ss[r] = 0.f;
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int col = (wc * CT + t) * 32 + cl;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const float cs = acc[t][r] / s_tot[rl];
-      acc[t][r] = cs;
-      if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float s = half_sum(ss[r]);
-    if (cl == 0) s_ss[wc][wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = s;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    const int64_t row = n0 + rl;
-    const float nrm = sqrtf(s_ss[0][rl] + s_ss[1][rl]);
-    if (row < N) {
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int col = (wc * CT + t) * 32 + cl;
-        if (col < D) out[row * D + col] = acc[t][r] / nrm;
+        for (int t = 0; t < CT; ++t) {
+          const int col = (wc * CT + t) * 32 + cl;
+          if (col < D) out[row * D + col] = acc[i][t][r] * inv;
+        }
       }
     }
-  }
 }
 
-template <int CT>
+template <int CT, int MR = 1>
 static int launch_project_x3(const float* s, const float* num, const float* aux,
                              const _Float16* wth, const _Float16* wtl, const float* ci,
                              const float* c0, int64_t n, int kp, int d, float* out,
                              hipStream_t stream) {
   const int grid = static_cast<int>(ceil_div(n, kXM));
-  mm2_project_x3_kernel<CT><<<grid, 512, 0, stream>>>(s, num, aux, wth, wtl, ci, c0, n, kp, d, out);
+  constexpr size_t lds = x3_lds_bytes<CT>();
+  static_assert(lds <= 160 * 1024, "x3 chunk buffers exceed LDS");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3_kernel<CT, MR>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr = true;
+  }
+  mm2_project_x3_kernel<CT, MR><<<grid, x3_threads<MR>(), lds, stream>>>(s, num, aux, wth, wtl, ci,
+                                                                        c0, n, kp, d, out);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -503,8 +599,7 @@ extern "C" int mmb_mm2_project_x3(const float* s, const float* num, const float*
     case 3: return launch_project_x3<3>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
     case 4: return launch_project_x3<4>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
     case 5: return launch_project_x3<5>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    case 6: return launch_project_x3<6>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    default: return MMB_EINVAL;
+    default: return MMB_EINVAL;  // d >= 320: two chunk buffers exceed the 160 KB LDS
   }
 }
 

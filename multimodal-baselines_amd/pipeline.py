@@ -268,13 +268,39 @@ def mm2_project(s, num, aux, proj: MMB2Projection, out=None, fp32_mfma: bool = F
     n = num.shape[0]
     if out is None:
         out = torch.empty((n, proj.d), dtype=torch.float32, device=num.device)
-    if fp32_mfma:
+    if fp32_mfma or proj.ldw > 320:  # x3 kernel's LDS buffers fit d < 320 (D=300 configs)
         L.call("mmb_mm2_project", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wm), proj.ldw,
                L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
     else:
         L.call("mmb_mm2_project_x3", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wsplit),
                proj.ldw, L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
     return out
+
+
+class _NullSpan:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+class _EventSpan:
+    """Records a timing event pair on the current stream around a block."""
+
+    def __init__(self, sink: list):
+        self.sink = sink
+
+    def __enter__(self):
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.a.record()
+        return self
+
+    def __exit__(self, *exc):
+        b = torch.cuda.Event(enable_timing=True)
+        b.record()
+        self.sink.append((self.a, b))
+        return False
 
 
 class FusedStep:
@@ -286,12 +312,21 @@ class FusedStep:
       gram         num/cnt -> G (fp64 MFMA)            [+ RCCL all-reduce of G]
       pc_solve     G -> pc (1 workgroup)
       pc_remove    num/cnt, pc -> sif                    (HBM-bound)
-      mm2_prepare  generator weights -> Wm, c0
-      mm2_project  s, num, aux, Wm -> mmb2 (fp32 MFMA + fused normalisation)
+      mm2_prepare  generator weights -> Wm, c0, fp16 hi/lo split
+      mm2_project  s, num, aux, Wm -> mmb2 (fp16-split MFMA + fused normalisation)
+
+    With `chunks` > 1 the utterances are cut into row chunks: the HBM-bound
+    stream kernel runs chunk c+1 on the caller's stream while the MFMA-bound
+    projection and the Gram accumulation of chunk c run on a second HIP stream
+    (they read only chunk c's num/s/aux).  The PC solve needs the Gram of every
+    row, so it and the removal run after the last chunk.  Measured on MI355X
+    (1M utterances) the overlap does not pay: the stream kernel occupies every
+    CU and the projection only runs in its gaps (chunks 1/4/8/16: 31.3 / 30.8
+    / 32.3 / 32.0 ms), so the default is one chunk.
     """
 
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
-                 n_total: int | None = None, row0: int = 0):
+                 n_total: int | None = None, row0: int = 0, chunks: int | None = None):
         self.inp = inputs
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
@@ -304,9 +339,7 @@ class FusedStep:
         kp = self.proj.kp
         self.num = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.s = torch.empty((self.n, kp), dtype=torch.float32, device=dev)
-        self.aux = torch.empty((3, self.n), dtype=torch.float32, device=dev)
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
-        self.gws = GramWorkspace(self.n, self.d, dev)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.npc = npc
@@ -314,16 +347,87 @@ class FusedStep:
         self.n_total = self.n if n_total is None else n_total
         self.row0 = row0
         self.flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        if chunks is None:
+            chunks = 1
+        if self.n_total < self.d:  # sklearn's transposed branch needs X^T Omega of all rows
+            chunks = 1
+        chunks = max(1, min(chunks, self.n))
+        step = -(-self.n // chunks)
+        self.bounds = [(r, min(r + step, self.n)) for r in range(0, self.n, step)] or [(0, 0)]
+        # aux is planar per chunk: chunk [r0, r1) owns flat[3 r0 : 3 r1] as [3][r1 - r0]
+        self.aux_flat = torch.empty((3 * self.n,), dtype=torch.float32, device=dev)
+        self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
+        self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
 
-    def run(self):
-        mm2_stream(self.n, self.t, self.d, self.a, self.vd, self.inp["audio"], self.inp["visual"],
-                   ids32=self.ids, table=self.table, wtab32=self.inp["wtab"], flag=self.flag,
-                   out=(self.num, self.s, self.aux))
-        cnt = self.aux[0]
-        pc = global_pc(self.num, cnt, self.npc, self.n_total, self.row0, self.allreduce,
-                       G=self.G, ws=self.gws)
-        remove_pc(self.num, cnt, pc, out=self.sif)
-        self.proj.refresh()
-        mm2_project(self.s, self.num, self.aux, self.proj, out=self.mmb2)
+    def aux_of(self, c: int) -> torch.Tensor:
+        r0, r1 = self.bounds[c]
+        return self.aux_flat[3 * r0:3 * r1].view(3, r1 - r0)
+
+    @property
+    def aux(self) -> torch.Tensor:
+        """[3, N] planar aux (count, total weight, row scale) of a one-chunk step."""
+        if len(self.bounds) != 1:
+            raise ValueError("aux is planar per chunk when chunks > 1; use aux_of(c)")
+        return self.aux_of(0)
+
+    def _stream_chunk(self, c: int):
+        r0, r1 = self.bounds[c]
+        inp = self.inp
+        mm2_stream(r1 - r0, self.t, self.d, self.a, self.vd, inp["audio"][r0:r1],
+                   inp["visual"][r0:r1], ids32=self.ids[r0:r1], table=self.table,
+                   wtab32=inp["wtab"], flag=self.flag,
+                   out=(self.num[r0:r1], self.s[r0:r1], self.aux_of(c)))
+
+    def _consume_chunk(self, c: int):
+        r0, r1 = self.bounds[c]
+        aux = self.aux_of(c)
+        mm2_project(self.s[r0:r1], self.num[r0:r1], aux, self.proj, out=self.mmb2[r0:r1])
+        gram(self.num[r0:r1], aux[0], self.G, accumulate=c > 0, ws=self.gws)
+
+    def run(self, trace: dict | None = None):
+        """One step.  With `trace` (a dict), HIP events are recorded on the
+        stream each phase runs on: trace[phase] gets (start, end) pairs."""
+        def mark(name):
+            if trace is None:
+                return _NullSpan()
+            return _EventSpan(trace.setdefault(name, []))
+
+        d, k = self.d, self.npc + N_OVERSAMPLES
+        if self.side is None:
+            with mark("mm2_prepare"):
+                self.proj.refresh()
+            with mark("mm2_stream"):
+                self._stream_chunk(0)
+            with mark("mm2_project+gram"):
+                self._consume_chunk(0)
+        else:
+            main = torch.cuda.current_stream(self.table.device)
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side), mark("mm2_prepare"):
+                self.proj.refresh()
+            for c in range(len(self.bounds)):
+                with mark("mm2_stream"):
+                    self._stream_chunk(c)
+                self.side.wait_stream(main)
+                with torch.cuda.stream(self.side), mark("mm2_project+gram"):
+                    self._consume_chunk(c)
+            with mark("join"):
+                main.wait_stream(self.side)
+        with mark("pc_start"):
+            if self.n_total >= d:
+                z0, transposed = omega(d, k, self.table.device), False
+            else:
+                om = omega(self.n_total, k, self.table.device)[self.row0:self.row0 + self.n]
+                z0, transposed = xt_omega(self.num, self.aux_of(0)[0], om.contiguous()), True
+        if self.allreduce is not None:
+            with mark("allreduce"):
+                self.allreduce(self.G)
+                if transposed:
+                    self.allreduce(z0)
+        with mark("pc_solve"):
+            pc = pc_solve(self.G, z0, self.npc, transposed)
+        with mark("pc_remove"):
+            for c, (r0, r1) in enumerate(self.bounds):
+                remove_pc(self.num[r0:r1], self.aux_of(c)[0], pc, out=self.sif[r0:r1])
         self.pc = pc
         return self.sif, self.mmb2

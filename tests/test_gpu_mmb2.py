@@ -174,3 +174,26 @@ def test_fused_step_large_properties(gpu):
     assert torch.isfinite(m1).all() and torch.isfinite(s1).all()
     norms = torch.linalg.norm(m1.double(), dim=1)
     assert (norms - 1).abs().max().item() < 1e-5
+
+
+def test_chunked_overlapped_step_matches_single_chunk(gpu):
+    """FusedStep(chunks=3): the stream kernel of chunk c+1 overlaps the projection
+    and Gram of chunk c on a second HIP stream.  MMB2 rows are independent of the
+    chunking (bit-identical); the SIF Gram is summed per chunk, so the PC-removed
+    rows agree to fp64 summation order."""
+    N, T, V = 5000, 24, 20_000
+    inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=11, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    one = P.FusedStep(inp, gen.networks(), chunks=1)
+    s1, m1 = [t.clone() for t in one.run()]
+    three = P.FusedStep(inp, gen.networks(), chunks=3)
+    assert len(three.bounds) == 3
+    trace = {}
+    s3, m3 = three.run(trace=trace)
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m3)
+    assert M.row_rel_err(s3.cpu().numpy(), s1.cpu().numpy()) < 1e-6
+    assert len(trace["mm2_stream"]) == 3 and len(trace["mm2_project+gram"]) == 3
+    with pytest.raises(ValueError):
+        three.aux
