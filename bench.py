@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--chunks", type=int, default=None,
                     help="row chunks per step (stream of chunk c+1 overlaps projection of c); "
                          "default 1")
+    ap.add_argument("--side-cus", type=int, default=0,
+                    help="with --chunks > 1: CUs reserved for the projection + Gram stream")
+    ap.add_argument("--side-layout", default="strided", choices=["strided", "high"])
     ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -126,7 +129,8 @@ def main():
             dist.all_reduce(t)
 
     step = P.FusedStep(inp, gen.networks(), allreduce=allreduce if world > 1 else None,
-                       n_total=U * world, row0=rank * U, chunks=args.chunks)
+                       n_total=U * world, row0=rank * U, chunks=args.chunks,
+                       side_cus=args.side_cus, side_layout=args.side_layout)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):

@@ -93,6 +93,15 @@ int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n
 int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int d, const double* pc,
                   int npc, float* out32, double* out64, hipStream_t stream);
 
+/* Streams restricted to a subset of the CUs (hipExtStreamCreateWithCUMask):
+ * bit i of cu_mask[i / 32] enables CU i.  Used to run the HBM-bound stream
+ * kernel and the MFMA-bound projection side by side on disjoint CUs.
+ * mmb_cu_count writes the device's CU count.  No reference counterpart
+ * (scheduling only).                                                         */
+int mmb_cu_count(int device, int* out);
+int mmb_stream_create_cu_mask(const uint32_t* cu_mask, int mask_words, hipStream_t* out);
+int mmb_stream_destroy(hipStream_t stream);
+
 /* Host helper: numpy RandomState(seed).normal(size=count) (MT19937 +
  * legacy polar Box-Muller), written to host memory.  Used for the
  * randomized-SVD start block Omega.                                          */
@@ -112,7 +121,10 @@ int mmb_calc_weights(const float* x, int64_t rows, int f, const float* b_mean,
  * Writes, per utterance i:
  *   num[i,:d]  = sum_t w_t E_t                      (weighted text sum)
  *   s[i,:]     = [Sx_e | Sxx_e | Sx_a | Sxx_a | Sx_v | Sxx_v | 0-pad]  (sum
- *                over t of x and x^2 per feature; row stride mmb_mm2_k())
+ *                over t of x and x^2 per feature; row stride mmb_mm2_k());
+ *                s_half = 0: fp32 [n][k]; s_half = 1: fp16 [n][2][k], the hi
+ *                and lo (residual) planes of s[i,:] * aux[2][i] -- the A
+ *                operand of mmb_mm2_project_x3 (same bytes per row)
  *   aux[0][i]  = count_nonzero(w), aux[1][i] = sum_t w_t, aux[2][i] = the
  *                power-of-2 scale putting max|s[i,:]| in [2^14, 2^15) (planar
  *                [3][n]; aux[0] is the SIF count the Gram / removal kernels take)
@@ -121,8 +133,8 @@ int mmb_calc_weights(const float* x, int64_t rows, int f, const float* b_mean,
 int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const float* wtab32,
                    const float* text_dense, const float* emb_dense, const float* w_dense,
                    const float* audio, const float* visual, int64_t n, int t, int d, int a,
-                   int vd, float* num_out, float* s_out, float* aux_out, int32_t* flag,
-                   hipStream_t stream);
+                   int vd, float* num_out, void* s_out, int s_half, float* aux_out,
+                   int32_t* flag, hipStream_t stream);
 
 /* Padded width (row stride) of the per-utterance sums: roundup(2(d+a+vd), 32). */
 int mmb_mm2_k(int d, int a, int vd);
@@ -140,7 +152,9 @@ int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_mu,
                     int t, float* wm, int ldw, float* c0, void* wsplit, hipStream_t stream);
 
 /* Bytes of the fp16 hi/lo split of wm written by mmb_mm2_prepare when wsplit
- * is non-null (transposed [ldw][k] hi and lo planes + per-column 1/scale). */
+ * is non-null: per 32-deep K chunk, the hi and lo planes [ldw][32] of the
+ * column-scaled wm (16-byte slots swizzled as mmb_mm2_project_x3 stages
+ * them), then the per-column 1/scale [ldw] f32.                             */
 size_t mmb_mm2_split_bytes(int d, int a, int vd);
 
 /* cs = (num + s @ wm[:, :d] + c0) / (aux[1] + s @ wm[:, d] + c0[d]);
@@ -152,9 +166,10 @@ int mmb_mm2_project(const float* s, const float* num, const float* aux, const fl
 
 /* The same projection on the fp16 MFMA pipe: s (scaled per row by aux[2]) and
  * wm (scaled per column) split into fp16 hi + lo, a*b ~ ah*bh + ah*bl + al*bh
- * (3 f16 MFMAs, ~22-bit operands, fp32 accumulation).  wsplit from
- * mmb_mm2_prepare.  The bench path.                                          */
-int mmb_mm2_project_x3(const float* s, const float* num, const float* aux, const void* wsplit,
+ * (3 f16 MFMAs, ~22-bit operands, fp32 accumulation).  s_split is the
+ * s_half = 1 output of mmb_mm2_stream, wsplit from mmb_mm2_prepare; d < 320.
+ * The bench path.                                                            */
+int mmb_mm2_project_x3(const void* s_split, const float* num, const float* aux, const void* wsplit,
                        int ldw, const float* c0, int64_t n, int k, int d, float* out,
                        hipStream_t stream);
 

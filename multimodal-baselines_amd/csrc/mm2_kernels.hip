@@ -247,13 +247,21 @@ using half4 = __attribute__((ext_vector_type(4))) _Float16;
 
 constexpr int kXM = 128;  // rows per workgroup (8 waves: 4 row tiles x 2 column halves)
 constexpr int kXK = 32;   // K chunk (2 MFMA k-steps)
-constexpr int kXS = kXK + 8;  // padded LDS row (halves)
+constexpr int kXT = 512;  // threads
+constexpr int kXAbuf = 4; // A chunk ring (3 chunks in flight from HBM)
+constexpr int kXBbuf = 2; // B chunk ring (1 chunk in flight from L2)
 
+// 16-byte slot swizzle of a 64-byte LDS row (4 slots of 8 halves): row r
+// keeps data slot j at position j ^ swz(r), which spreads the 16 rows one
+// ds_read_b128 lane group touches over all 64 banks
+__host__ __device__ constexpr int x3_swz(int r) { return (r >> 2) & 3; }
+
+// Weight split, written in the projection kernel's B chunk image order so the
+// kernel stages B with straight 16-byte global->LDS copies:
+//   img[c][plane][col][slot position q] = plane(Wm[32c + 8 (q ^ swz(col)) + e][col] * scale_col)
+// plane 0 = fp16 hi, 1 = fp16 lo (residual); col_inv[col] = 1 / scale_col.
 __global__ void mm2_split_wm_kernel(const float* __restrict__ wm, int Kp, int ldw,
-                                    _Float16* __restrict__ wth, _Float16* __restrict__ wtl,
-                                    float* __restrict__ col_inv) {
-  // one workgroup per column j: max |Wm[:, j]| -> scale, then the transposed
-  // hi/lo planes Wt[j][k] (K contiguous, the B-fragment order)
+                                    _Float16* __restrict__ img, float* __restrict__ col_inv) {
   __shared__ float s_m[4];
   const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float m = 0.f;
@@ -272,261 +280,245 @@ __global__ void mm2_split_wm_kernel(const float* __restrict__ wm, int Kp, int ld
   for (int k = tid; k < Kp; k += blockDim.x) {
     const float v = wm[static_cast<int64_t>(k) * ldw + j] * sc;
     const _Float16 h = static_cast<_Float16>(v);
-    wth[static_cast<int64_t>(j) * Kp + k] = h;
-    wtl[static_cast<int64_t>(j) * Kp + k] = static_cast<_Float16>(v - static_cast<float>(h));
+    const int c = k / kXK, kk = k % kXK;
+    const int64_t at = static_cast<int64_t>(c) * 2 * ldw * kXK + static_cast<int64_t>(j) * kXK +
+                       ((kk >> 3) ^ x3_swz(j)) * 8 + (kk & 7);
+    img[at] = h;
+    img[at + static_cast<int64_t>(ldw) * kXK] = static_cast<_Float16>(v - static_cast<float>(h));
   }
   if (tid == 0) col_inv[j] = 1.f / sc;
 }
 
-// LDS image of one K chunk: A hi, A lo [kXM][kXS], B hi, B lo [LDW][kXS]
-// halves; each lo plane sits 32 halves past its hi plane's end so the hi and
-// lo 16-byte stores of one 8-lane group land on disjoint banks
-constexpr int kXPad = 32;
 template <int CT>
-constexpr int x3_buf_halves() { return 2 * (kXM * kXS + kXPad) + 2 * (64 * CT * kXS + kXPad); }
+constexpr int x3_bbuf_halves() { return 2 * 64 * CT * kXK; }  // hi + lo planes of a chunk
+constexpr int kXAbufHalves = 2 * kXM * kXK;
 template <int CT>
 constexpr size_t x3_lds_bytes() {
-  return 2 * x3_buf_halves<CT>() * sizeof(_Float16) + 4 * kXM * sizeof(float);
+  return (kXBbuf * x3_bbuf_halves<CT>() + kXAbuf * kXAbufHalves) * sizeof(_Float16) +
+         4 * kXM * sizeof(float);
 }
-// MR = 32-row MFMA tiles per wave: the 128 x LDW block is split over
-// (4 / MR) x 2 waves, each owning MR x CT tiles of 32 x 32
-template <int MR>
-constexpr int x3_threads() { return 64 * 2 * (4 / MR); }
 
-template <int CT, int MR>
-__global__ __launch_bounds__(x3_threads<MR>()) void mm2_project_x3_kernel(
-    const float* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
-    const _Float16* __restrict__ wth, const _Float16* __restrict__ wtl,
-    const float* __restrict__ col_inv, const float* __restrict__ c0, int64_t N, int Kp, int D,
-    float* __restrict__ out) {
+using gptr_t = const __attribute__((address_space(1))) void*;
+using lptr_t = __attribute__((address_space(3))) void*;
+
+// 16 bytes per lane global -> LDS; the LDS destination is the wave-uniform
+// `lds` plus 16 * lane (M0 = readfirstlane(lds))
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds, 16, 0, 0);
+}
+
+// out = L2-normalised (num + s @ Wm[:, :D] + c0) / (total), the fp16 hi/lo
+// split GEMM on the f16 MFMA pipe (sif2.py:186-207).
+//   S_split [N][2][Kp] fp16: hi | lo of the row-scaled sums (mmb_mm2_stream)
+//   img     B chunk images (mm2_split_wm_kernel)
+// Both operands are staged by direct global->LDS copies (no VGPR staging, no
+// ds_write): B two chunks deep (L2-resident), A four chunks deep (streamed
+// once from HBM, three chunks in flight).  One barrier per chunk, behind a
+// counted vmcnt that leaves the newest A chunk in flight.
+template <int CT>
+__global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
+    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
+    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
+    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out) {
   constexpr int LDW = 64 * CT;
-  constexpr int BUF = x3_buf_halves<CT>();
-  constexpr int kXT = x3_threads<MR>();
-  constexpr int AQ = kXM * 8 / kXT;   // float4 A pieces per thread per chunk
-  constexpr int BQ = LDW * 8 / kXT;   // 16-byte B pieces per thread per chunk
-  constexpr int OA = 0, OAL = kXM * kXS + kXPad;
-  constexpr int OB = 2 * OAL, OBL = OB + LDW * kXS + kXPad;
-  // one dynamic LDS array: two chunk buffers, then the per-row scalars
+  constexpr int BBUF = x3_bbuf_halves<CT>();
+  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 16-byte pieces per thread per B chunk (= CT)
+  constexpr int AQ = kXAbufHalves * 2 / 16 / kXT;  // = 2
+  static_assert(BQ * kXT * 16 == BBUF * 2 && AQ * kXT * 16 == kXAbufHalves * 2, "staging split");
+  // one dynamic LDS array: B ring, A ring, per-row scalars
   extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-  float* s_rs = reinterpret_cast<float*>(lds + 2 * BUF);
+  _Float16* bring = lds;
+  _Float16* aring = lds + kXBbuf * BBUF;
+  float* s_rs = reinterpret_cast<float*>(aring + kXAbuf * kXAbufHalves);
   float* s_tot = s_rs + kXM;
   float(*s_ss)[kXM] = reinterpret_cast<float(*)[kXM]>(s_tot + kXM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;  // rows wr*32*MR + [0,32*MR), tiles wc*CT + [0,CT)
+  const int wr = wave >> 1, wc = wave & 1;  // rows wr*32 + [0,32), column tiles wc*CT + [0,CT)
   const int hl = lane >> 5, cl = lane & 31;
   const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
-  const float* rscale = aux + 2 * N;
+  const int nch = Kp / kXK;
 
-  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? rscale[n0 + tid] : 1.f;
-  __syncthreads();
-
-  f32x16 acc[MR][CT];
-#pragma unroll
-  for (int i = 0; i < MR; ++i)
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
-
-  // Software pipeline over K chunks of kXK, two LDS buffers, one barrier per
-  // chunk.  Iteration c: the fragments of both k-steps of chunk c are read
-  // from buffer c&1 up front, the first k-step's MFMAs run while the
-  // registers holding chunk c+1 are converted and stored into the other
-  // buffer and the global loads of B(c+2) and A(c+3) are issued, then the
-  // second k-step's MFMAs.  A (the s rows, streamed once from HBM) is
-  // prefetched through a ring of two register sets, B (the split weights,
-  // L2-resident) through one.  Loads are unconditional (rows clamped to N-1,
-  // chunks past the end re-read the last) so no load is branched around; A
-  // loads are non-temporal to spare L2 for B.
-  f32x4 pa0[AQ], pa1[AQ];
-  u32x4 pb[BQ];
-  const float* arow[AQ];
-  const _Float16* bcol[BQ];
+  // A piece g = q * kXT + tid of a chunk: plane g >> 9, row (g >> 2) & 127,
+  // LDS slot position g & 3 <- data slot (g & 3) ^ swz(row); rows past N
+  // re-read row N-1 (never stored)
+  const _Float16* asrc[AQ];
 #pragma unroll
   for (int q = 0; q < AQ; ++q) {
-    const int idx = tid + kXT * q;
-    const int64_t row = min(n0 + (idx >> 3), N - 1);
-    arow[q] = S + row * Kp + (idx & 7) * 4;
+    const int g = q * kXT + tid;
+    const int plane = g >> 9, row = (g >> 2) & (kXM - 1);
+    const int64_t r = min(n0 + row, N - 1);
+    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
   }
-#pragma unroll
-  for (int q = 0; q < BQ; ++q) {
-    const int idx = tid + kXT * q;
-    const int col = idx >> 3, part = idx & 7;
-    bcol[q] = ((part >> 2) ? wtl : wth) + static_cast<int64_t>(col) * Kp + (part & 3) * 8;
-  }
-  const int nch = Kp / kXK;
-  auto load_a = [&](f32x4(&pa)[AQ], int c) {
-    const int k = min(c, nch - 1) * kXK;
+  auto stage_a = [&](int c) {
+    const int cc = min(c, nch - 1);
+    _Float16* dst = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
 #pragma unroll
     for (int q = 0; q < AQ; ++q)
-      pa[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(arow[q] + k));
+      glds16(asrc[q] + cc * kXK, dst + (q * kXT + wave * 64) * 8);
   };
-  auto load_b = [&](int c) {
-    const int k = min(c, nch - 1) * kXK;
+  auto stage_b = [&](int c) {
+    const int cc = min(c, nch - 1);
+    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
+    _Float16* dst = bring + (c & (kXBbuf - 1)) * BBUF;
 #pragma unroll
-    for (int q = 0; q < BQ; ++q) pb[q] = *reinterpret_cast<const u32x4*>(bcol[q] + k);
+    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, dst + (q * kXT + wave * 64) * 8);
   };
-  auto stage = [&](const f32x4(&pa)[AQ], _Float16* buf) {
-    // A: 128 rows x 32 fp32 -> row-scaled fp16 hi/lo
+
+  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? aux[2 * N + n0 + tid] : 1.f;
+  stage_b(0);
+  stage_a(0);
+  stage_a(1);
+  stage_a(2);
+
+  f32x16 acc[CT];
 #pragma unroll
-    for (int q = 0; q < AQ; ++q) {
-      const int idx = tid + kXT * q;
-      const int row = idx >> 3, c4 = idx & 7;
-      const float sc = s_rs[row];
-      half4 h, l;
+  for (int t = 0; t < CT; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float x = pa[q][e] * sc;
-        h[e] = static_cast<_Float16>(x);
-        l[e] = static_cast<_Float16>(x - static_cast<float>(h[e]));
-      }
-      *reinterpret_cast<half4*>(buf + OA + row * kXS + c4 * 4) = h;
-      *reinterpret_cast<half4*>(buf + OAL + row * kXS + c4 * 4) = l;
-    }
-    // B: LDW columns x 32 halves per plane = 4 x 16 B per column per plane
-#pragma unroll
-    for (int q = 0; q < BQ; ++q) {
-      const int idx = tid + kXT * q;
-      const int col = idx >> 3, part = idx & 7;
-      *reinterpret_cast<u32x4*>(buf + ((part >> 2) ? OBL : OB) + col * kXS + (part & 3) * 8) =
-          pb[q];
-    }
-  };
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
   struct Frag {
-    half8 ah[MR], al[MR], bh[CT], bl[CT];
+    half8 ah, al, bh[CT], bl[CT];
   };
-  auto read_frag = [&](const _Float16* buf, int s, Frag& f) {
-    const int ko = 16 * s + 8 * hl;
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      const int row = (wr * MR + i) * 32 + cl;
-      f.ah[i] = *reinterpret_cast<const half8*>(buf + OA + row * kXS + ko);
-      f.al[i] = *reinterpret_cast<const half8*>(buf + OAL + row * kXS + ko);
-    }
+  auto read_frag = [&](const _Float16* a, const _Float16* b, int s, Frag& f) {
+    const int js = 2 * s + hl;  // 16-byte data slot of this lane's 8 k values
+    const int row = wr * 32 + cl;
+    const int ao = row * kXK + ((js ^ x3_swz(row)) * 8);
+    f.ah = *reinterpret_cast<const half8*>(a + ao);
+    f.al = *reinterpret_cast<const half8*>(a + kXM * kXK + ao);
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
       const int col = (wc * CT + t) * 32 + cl;
-      f.bh[t] = *reinterpret_cast<const half8*>(buf + OB + col * kXS + ko);
-      f.bl[t] = *reinterpret_cast<const half8*>(buf + OBL + col * kXS + ko);
+      const int bo = col * kXK + ((js ^ x3_swz(col)) * 8);
+      f.bh[t] = *reinterpret_cast<const half8*>(b + bo);
+      f.bl[t] = *reinterpret_cast<const half8*>(b + LDW * kXK + bo);
     }
   };
   auto mfma = [&](const Frag& f) {
 #pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[t], acc[i][t], 0, 0, 0);
-        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[t], acc[i][t], 0, 0, 0);
-        acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[t], acc[i][t], 0, 0, 0);
-      }
+    for (int t = 0; t < CT; ++t) {
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah, f.bh[t], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah, f.bl[t], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al, f.bh[t], acc[t], 0, 0, 0);
+    }
   };
-  // iteration c: buffer `cur` holds chunk c, `nxt` holds A(c+1) (pb holds
-  // B(c+1)), the other ring set holds A(c+2) in flight
-  auto iter = [&](int c, f32x4(&nxt)[AQ], const _Float16* cur, _Float16* oth) {
+
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed: this wave's copies of B(c) and A(c) retired (only the
+    // newest A chunk, AQ copies, may still be in flight; in the first
+    // iteration A(1) and A(2) too), then every wave's, by the barrier; the
+    // barrier also retires all reads of the buffers restaged below
+    if (c == 0) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage_b(c + 1);
+    stage_a(c + 3);
+    const _Float16* a = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
+    const _Float16* b = bring + (c & (kXBbuf - 1)) * BBUF;
     Frag f0, f1;
-    read_frag(cur, 0, f0);
-    read_frag(cur, 1, f1);
+    read_frag(a, b, 0, f0);
+    read_frag(a, b, 1, f1);
     mfma(f0);
-    stage(nxt, oth);
-    load_b(c + 2);
-    load_a(nxt, c + 3);
     mfma(f1);
-    __syncthreads();
-  };
-  _Float16* buf0 = lds;
-  _Float16* buf1 = lds + BUF;
-  load_a(pa0, 0);
-  load_b(0);
-  load_a(pa1, 1);
-  stage(pa0, buf0);
-  load_b(1);
-  load_a(pa0, 2);
-  __syncthreads();
-  int c = 0;
-  for (; c + 1 < nch; c += 2) {
-    iter(c, pa1, buf0, buf1);
-    iter(c + 1, pa0, buf1, buf0);
   }
-  if (c < nch) iter(c, pa1, buf0, buf1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // epilogue (as mm2_project_kernel): unscale, add weighted text sum + c0,
-  // divide by the total weight (column D), L2-normalise the row
+  // divide by the total weight (column D), L2-normalise the row.  Every load
+  // is unconditional (row and column clamped in range, results selected
+  // afterwards): a load behind a per-lane branch is waited for right after
+  // it, which serialises the whole epilogue on memory latency.
+  {
+    // all 16 x (CT + 1) loads of this lane first, then the arithmetic: one
+    // memory latency for the whole epilogue instead of one per row group
+    // (the fragment registers are dead here, so the loads fit)
+    float nv[16][CT], tv[16];
 #pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int col = (wc * CT + t) * 32 + cl;
-    const float ci = col_inv[col];
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const int64_t rowc = min(n0 + rl, N - 1);
+      tv[r] = aux[N + rowc];
 #pragma unroll
-    for (int i = 0; i < MR; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = (wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const int64_t row = n0 + rl;
-        float y = acc[i][t][r] * (ci / s_rs[rl]);
-        if (row < N) {
-          if (col < D) y += num[row * D + col] + c0[col];
-          else if (col == D) y += aux[N + row] + c0[D];
-        }
-        acc[i][t][r] = y;
-        if (col == D) s_tot[rl] = y;
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 32 + cl;
+        nv[r][t] = num[rowc * D + min(col, D - 1)];
       }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < MR; ++i) {
-    float ss[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ss[r] = 0.f;
+    }
+    float cadd[CT], cinv[CT];
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
       const int col = (wc * CT + t) * 32 + cl;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = (wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const float cs = acc[i][t][r] / s_tot[rl];
-        acc[i][t][r] = cs;
-        if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
-      }
+      cinv[t] = col_inv[col];
+      cadd[t] = c0[col];
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float sum = half_sum(ss[r]);
-      if (cl == 0) s_ss[wc][(wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = sum;
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float inv_rs = 1.f / s_rs[rl];
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 32 + cl;
+        const float add = col < D ? nv[r][t] : (col == D ? tv[r] : 0.f);
+        const float y = acc[t][r] * (cinv[t] * inv_rs) + add + cadd[t];
+        acc[t][r] = y;
+        if (col == D) s_tot[rl] = y;
+      }
     }
   }
   __syncthreads();
+  float ss[16];
 #pragma unroll
-  for (int i = 0; i < MR; ++i)
+  for (int r = 0; r < 16; ++r) ss[r] = 0.f;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int col = (wc * CT + t) * 32 + cl;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int rl = (wr * MR + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const int64_t row = n0 + rl;
-      const float inv = 1.f / sqrtf(s_ss[0][rl] + s_ss[1][rl]);
-      if (row < N) {
+      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+      const float cs = acc[t][r] / s_tot[rl];
+      acc[t][r] = cs;
+      if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
+    }
+  }
 #pragma unroll
-        for (int t = 0; t < CT; ++t) {
-          const int col = (wc * CT + t) * 32 + cl;
-          if (col < D) out[row * D + col] = acc[i][t][r] * inv;
-        }
+  for (int r = 0; r < 16; ++r) {
+    const float sum = half_sum(ss[r]);
+    if (cl == 0) s_ss[wc][wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = sum;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    const int64_t row = n0 + rl;
+    const float inv = 1.f / sqrtf(s_ss[0][rl] + s_ss[1][rl]);
+    if (row < N) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 32 + cl;
+        if (col < D) out[row * D + col] = acc[t][r] * inv;
       }
     }
+  }
 }
 
-template <int CT, int MR = 1>
-static int launch_project_x3(const float* s, const float* num, const float* aux,
-                             const _Float16* wth, const _Float16* wtl, const float* ci,
-                             const float* c0, int64_t n, int kp, int d, float* out,
-                             hipStream_t stream) {
+template <int CT>
+static int launch_project_x3(const _Float16* s, const float* num, const float* aux,
+                             const _Float16* img, const float* ci, const float* c0, int64_t n,
+                             int kp, int d, float* out, hipStream_t stream) {
   const int grid = static_cast<int>(ceil_div(n, kXM));
   constexpr size_t lds = x3_lds_bytes<CT>();
-  static_assert(lds <= 160 * 1024, "x3 chunk buffers exceed LDS");
+  static_assert(lds <= 160 * 1024, "x3 chunk rings exceed LDS");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3_kernel<CT, MR>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3_kernel<CT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
-  mm2_project_x3_kernel<CT, MR><<<grid, x3_threads<MR>(), lds, stream>>>(s, num, aux, wth, wtl, ci,
-                                                                        c0, n, kp, d, out);
+  mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -574,32 +566,32 @@ extern "C" int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_m
   mm2_prepare_c0_kernel<<<ldw / 64, 1024, 0, stream>>>(p);
   MMB_LAUNCH_CHECK();
   if (wsplit) {
-    _Float16* wth = static_cast<_Float16*>(wsplit);
-    _Float16* wtl = wth + static_cast<size_t>(ldw) * p.Kp;
-    float* ci = reinterpret_cast<float*>(wtl + static_cast<size_t>(ldw) * p.Kp);
-    mm2_split_wm_kernel<<<ldw, 256, 0, stream>>>(wm, p.Kp, ldw, wth, wtl, ci);
+    _Float16* img = static_cast<_Float16*>(wsplit);
+    float* ci = reinterpret_cast<float*>(img + 2 * static_cast<size_t>(ldw) * p.Kp);
+    mm2_split_wm_kernel<<<ldw, 256, 0, stream>>>(wm, p.Kp, ldw, img, ci);
     MMB_LAUNCH_CHECK();
   }
   return MMB_OK;
 }
 
-extern "C" int mmb_mm2_project_x3(const float* s, const float* num, const float* aux,
+extern "C" int mmb_mm2_project_x3(const void* s_split, const float* num, const float* aux,
                                   const void* wsplit, int ldw, const float* c0, int64_t n, int k,
                                   int d, float* out, hipStream_t stream) {
-  MMB_REQUIRE(s && num && aux && wsplit && c0 && out && n >= 0 && d > 0);
-  MMB_REQUIRE(ldw == mmb_mm2_ldw(d) && k % 32 == 0);
-  MMB_REQUIRE((reinterpret_cast<uintptr_t>(s) & 15) == 0 && (reinterpret_cast<uintptr_t>(wsplit) & 15) == 0);
+  MMB_REQUIRE(s_split && num && aux && wsplit && c0 && out && n >= 0 && d > 0);
+  MMB_REQUIRE(ldw == mmb_mm2_ldw(d) && k % 32 == 0 && k >= 32);
+  MMB_REQUIRE((reinterpret_cast<uintptr_t>(s_split) & 15) == 0 &&
+              (reinterpret_cast<uintptr_t>(wsplit) & 15) == 0);
   if (n == 0) return MMB_OK;
-  const _Float16* wth = static_cast<const _Float16*>(wsplit);
-  const _Float16* wtl = wth + static_cast<size_t>(ldw) * k;
-  const float* ci = reinterpret_cast<const float*>(wtl + static_cast<size_t>(ldw) * k);
+  const _Float16* s = static_cast<const _Float16*>(s_split);
+  const _Float16* img = static_cast<const _Float16*>(wsplit);
+  const float* ci = reinterpret_cast<const float*>(img + 2 * static_cast<size_t>(ldw) * k);
   switch (ldw / 64) {
-    case 1: return launch_project_x3<1>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    case 2: return launch_project_x3<2>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    case 3: return launch_project_x3<3>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    case 4: return launch_project_x3<4>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    case 5: return launch_project_x3<5>(s, num, aux, wth, wtl, ci, c0, n, k, d, out, stream);
-    default: return MMB_EINVAL;  // d >= 320: two chunk buffers exceed the 160 KB LDS
+    case 1: return launch_project_x3<1>(s, num, aux, img, ci, c0, n, k, d, out, stream);
+    case 2: return launch_project_x3<2>(s, num, aux, img, ci, c0, n, k, d, out, stream);
+    case 3: return launch_project_x3<3>(s, num, aux, img, ci, c0, n, k, d, out, stream);
+    case 4: return launch_project_x3<4>(s, num, aux, img, ci, c0, n, k, d, out, stream);
+    case 5: return launch_project_x3<5>(s, num, aux, img, ci, c0, n, k, d, out, stream);
+    default: return MMB_EINVAL;  // d >= 320: the chunk rings exceed the 160 KB LDS
   }
 }
 

@@ -35,9 +35,10 @@ struct StreamArgs {
   float* x_out;
   float* num_out;
   float* cnt_out;
-  float* s_out;
+  float* s_out;     // [N][Kp] fp32, or with s_half [N][2][Kp] fp16 (hi | lo, row-scaled)
   float* aux_out;
   int32_t* flag;
+  int s_half;
 };
 
 template <int VEC>
@@ -346,6 +347,19 @@ __device__ __forceinline__ float amax4(float4 v) {
 __device__ __forceinline__ float4 div4(float4 v, float c) {
   return make_float4(v.x / c, v.y / c, v.z / c, v.w / c);
 }
+using h4 = _Float16 __attribute__((ext_vector_type(4)));
+// x * rs (rs a power of two: exact) as fp16 hi + fp16 lo = the residual
+__device__ __forceinline__ void split_store4(_Float16* hi, _Float16* lo, float4 v, float rs) {
+  const float x[4] = {v.x * rs, v.y * rs, v.z * rs, v.w * rs};
+  h4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = static_cast<_Float16>(x[e]);
+    l[e] = static_cast<_Float16>(x[e] - static_cast<float>(h[e]));
+  }
+  *reinterpret_cast<h4*>(hi) = h;
+  *reinterpret_cast<h4*>(lo) = l;
+}
 
 template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
@@ -456,34 +470,6 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
     }
 
     if constexpr (MM2) {
-      float* srow = a.s_out + i * a.Kp;
-#pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        const int u = lane + kWave * c;
-        if (u < UT) {
-          st4(a.num_out + i * a.D + 4 * u, num[c]);
-          st4(srow + 4 * u, sx[c]);
-          st4(srow + a.D + 4 * u, sxx[c]);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < CA; ++c) {
-        const int u = lane + kWave * c;
-        if (u < UA) {
-          st4(srow + 2 * a.D + 4 * u, sa[c]);
-          st4(srow + 2 * a.D + a.A + 4 * u, saa[c]);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < CV; ++c) {
-        const int u = lane + kWave * c;
-        if (u < UV) {
-          st4(srow + 2 * (a.D + a.A) + 4 * u, sv[c]);
-          st4(srow + 2 * (a.D + a.A) + a.Vd + 4 * u, svv[c]);
-        }
-      }
-      const int k = 2 * (a.D + a.A + a.Vd);
-      for (int f = k + lane; f < a.Kp; f += kWave) srow[f] = 0.f;
       float m = 0.f;
 #pragma unroll
       for (int c = 0; c < CT; ++c) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
@@ -491,11 +477,55 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       for (int c = 0; c < CA; ++c) m = fmaxf(m, fmaxf(amax4(sa[c]), amax4(saa[c])));
 #pragma unroll
       for (int c = 0; c < CV; ++c) m = fmaxf(m, fmaxf(amax4(sv[c]), amax4(svv[c])));
-      m = wave_max(m);
+      const float rs = row_scale(wave_max(m));
+      // one sums row: fp32, or fp16 hi | lo planes of the row-scaled sums (the
+      // projection GEMM's A operand, ready for direct global->LDS staging)
+      float* srow = a.s_out + i * a.Kp;
+      _Float16* hrow = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * a.Kp;
+      auto put = [&](int f, float4 v) {
+        if (a.s_half) {
+          split_store4(hrow + f, hrow + a.Kp + f, v, rs);
+        } else {
+          st4(srow + f, v);
+        }
+      };
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UT) {
+          st4(a.num_out + i * a.D + 4 * u, num[c]);
+          put(4 * u, sx[c]);
+          put(a.D + 4 * u, sxx[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UA) {
+          put(2 * a.D + 4 * u, sa[c]);
+          put(2 * a.D + a.A + 4 * u, saa[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CV; ++c) {
+        const int u = lane + kWave * c;
+        if (u < UV) {
+          put(2 * (a.D + a.A) + 4 * u, sv[c]);
+          put(2 * (a.D + a.A) + a.Vd + 4 * u, svv[c]);
+        }
+      }
+      const int k = 2 * (a.D + a.A + a.Vd);
+      for (int f = k + lane; f < a.Kp; f += kWave) {
+        if (a.s_half) {
+          hrow[f] = hrow[a.Kp + f] = static_cast<_Float16>(0.f);
+        } else {
+          srow[f] = 0.f;
+        }
+      }
       if (lane == 0) {
         a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | fp16 row scale
         a.aux_out[a.N + i] = sw;
-        a.aux_out[2 * a.N + i] = row_scale(m);
+        a.aux_out[2 * a.N + i] = rs;
       }
     } else {
 #pragma unroll
@@ -509,117 +539,6 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       if (lane == 0 && a.cnt_out) a.cnt_out[i] = cnt;
     }
   }
-}
-
-// MMB2 wave kernel, unified column space: the three rows of a frame (gathered
-// text row, audio frame, visual frame) are (D + A + Vd) / 4 float4 units
-// (225 at 3 x 300) spread over the 64 lanes, UPL units per lane, fixed for the
-// whole utterance.  Every frame is UPL fully-used 16-B load instructions
-// (vs. 6 half-empty ones per frame with a lane map per modality) and the loop
-// body has no branch, so the unrolled frames' loads are all in flight together.
-template <int UPL>
-__global__ __launch_bounds__(256) void utt_wave3_kernel(StreamArgs a) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
-  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
-  const int UT = a.D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
-  const int UTOT = UT + UA + UV;
-  const float* tsrc = a.ids ? a.table : a.text_dense;
-  const float* esrc = a.ids ? a.table : a.emb_dense;
-  const bool split_emb = esrc != tsrc;
-  const bool gather = a.ids != nullptr;
-  // per-lane unit descriptors: modality m (0 text, 1 audio, 2 visual), float offset in its row
-  int um[UPL], uo[UPL];
-  bool uok[UPL];
-#pragma unroll
-  for (int j = 0; j < UPL; ++j) {
-    const int u = lane + kWave * j;
-    uok[j] = u < UTOT;
-    um[j] = u < UT ? 0 : (u < UT + UA ? 1 : 2);
-    uo[j] = 4 * (um[j] == 0 ? u : (um[j] == 1 ? u - UT : u - UT - UA));
-    if (!uok[j]) { um[j] = 1; uo[j] = 0; }  // harmless in-bounds reads, never stored
-  }
-  // output offsets in the sums row: Sx_m at seg, Sxx_m at seg + width
-  int sxo[UPL], sqo[UPL];
-#pragma unroll
-  for (int j = 0; j < UPL; ++j) {
-    const int seg = um[j] == 0 ? 0 : (um[j] == 1 ? 2 * a.D : 2 * (a.D + a.A));
-    const int wdt = um[j] == 0 ? a.D : (um[j] == 1 ? a.A : a.Vd);
-    sxo[j] = seg + uo[j];
-    sqo[j] = seg + wdt + uo[j];
-  }
-
-  for (int64_t i = wid; i < a.N; i += nw) {
-    int rid = -1;
-    float w = 0.f;
-    if (lane < a.L) {
-      int64_t off;
-      stage_token(a, i, lane, off, w);
-      rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
-    }
-    const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
-    const float sw = wave_sum(w);
-
-    float4 num[UPL], sx[UPL], sxx[UPL];
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < UPL; ++j) num[j] = sx[j] = sxx[j] = z4;
-    const float* abase = a.audio + i * a.L * a.A;
-    const float* vbase = a.visual + i * a.L * a.Vd;
-    const int64_t dbase = i * a.L;
-
-#pragma unroll 4
-    for (int t = 0; t < a.L; ++t) {
-      const int r = __builtin_amdgcn_readlane(rid, t);
-      const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
-      const bool ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
-      const int64_t toff = (gather ? static_cast<int64_t>(ok ? r : 0) : dbase + t) * a.D;
-      const float* trow = tsrc + toff;
-      const float* arow = abase + static_cast<int64_t>(t) * a.A;
-      const float* vrow = vbase + static_cast<int64_t>(t) * a.Vd;
-#pragma unroll
-      for (int j = 0; j < UPL; ++j) {
-        const float* p = (um[j] == 0 ? trow : (um[j] == 1 ? arow : vrow)) + uo[j];
-        float4 v = ld4(p);
-        if (um[j] == 0 && !ok) v = z4;
-        add4(sx[j], v);
-        sq4(sxx[j], v);
-        if (um[j] == 0) {
-          if (split_emb) v = ok ? ld4(esrc + toff + uo[j]) : z4;
-          fma4(num[j], wt, v);
-        }
-      }
-    }
-
-    float* srow = a.s_out + i * a.Kp;
-    float m = 0.f;
-#pragma unroll
-    for (int j = 0; j < UPL; ++j) {
-      if (uok[j]) {
-        st4(srow + sxo[j], sx[j]);
-        st4(srow + sqo[j], sxx[j]);
-        if (um[j] == 0) st4(a.num_out + i * a.D + uo[j], num[j]);
-        m = fmaxf(m, fmaxf(amax4(sx[j]), amax4(sxx[j])));
-      }
-    }
-    const int k = 2 * (a.D + a.A + a.Vd);
-    for (int f = k + lane; f < a.Kp; f += kWave) srow[f] = 0.f;
-    m = wave_max(m);
-    if (lane == 0) {
-      a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | fp16 row scale
-      a.aux_out[a.N + i] = sw;
-      a.aux_out[2 * a.N + i] = row_scale(m);
-    }
-  }
-}
-
-template <int UPL>
-static int launch_wave3(const StreamArgs& a, hipStream_t stream) {
-  const int64_t blocks = ceil_div(a.N, 4);
-  const int grid = static_cast<int>(blocks < 256 * 8 ? blocks : 256 * 8);
-  utt_wave3_kernel<UPL><<<grid, 256, 0, stream>>>(a);
-  MMB_LAUNCH_CHECK();
-  return MMB_OK;
 }
 
 template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false>
@@ -682,6 +601,26 @@ using namespace mmb;
 
 extern "C" int mmb_version(void) { return 100; }
 
+extern "C" int mmb_cu_count(int device, int* out) {
+  MMB_REQUIRE(out);
+  const hipError_t e = hipDeviceGetAttribute(out, hipDeviceAttributeMultiprocessorCount, device);
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+
+extern "C" int mmb_stream_create_cu_mask(const uint32_t* cu_mask, int mask_words,
+                                         hipStream_t* out) {
+  MMB_REQUIRE(cu_mask && mask_words > 0 && out);
+  const hipError_t e =
+      hipExtStreamCreateWithCUMask(out, static_cast<uint32_t>(mask_words), cu_mask);
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+
+extern "C" int mmb_stream_destroy(hipStream_t stream) {
+  MMB_REQUIRE(stream);
+  const hipError_t e = hipStreamDestroy(stream);
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+
 extern "C" int mmb_seq2weight(const int32_t* seq, const uint8_t* sel, int64_t n, int64_t l,
                               const double* wtab64, int64_t v, float* w_out, int32_t* flag,
                               hipStream_t stream) {
@@ -731,14 +670,35 @@ extern "C" int mmb_mm2_k(int d, int a, int vd) {
   return (k + 31) / 32 * 32;
 }
 
+// The workgroup stream kernel writes fp32 sums; for the fp16 hi/lo format a
+// second pass splits each row in place (one workgroup per row, the row staged
+// in LDS).  Only the fallback shapes (tokens > 64, widths not % 4) take it.
+__global__ __launch_bounds__(256) void split_rows_kernel(float* __restrict__ s,
+                                                         const float* __restrict__ rscale,
+                                                         int Kp) {
+  extern __shared__ float srow[];
+  const int64_t i = blockIdx.x;
+  float* row = s + i * Kp;
+  for (int f = threadIdx.x; f < Kp; f += blockDim.x) srow[f] = row[f];
+  __syncthreads();
+  const float rs = rscale[i];
+  _Float16* hi = reinterpret_cast<_Float16*>(row);
+  for (int f = threadIdx.x; f < Kp; f += blockDim.x) {
+    const float x = srow[f] * rs;
+    const _Float16 h = static_cast<_Float16>(x);
+    hi[f] = h;
+    hi[Kp + f] = static_cast<_Float16>(x - static_cast<float>(h));
+  }
+}
+
 extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
                               const float* wtab32, const float* text_dense,
                               const float* emb_dense, const float* w_dense, const float* audio,
                               const float* visual, int64_t n, int t, int d, int a_, int vd,
-                              float* num_out, float* s_out, float* aux_out, int32_t* flag,
-                              hipStream_t stream) {
+                              float* num_out, void* s_out, int s_half, float* aux_out,
+                              int32_t* flag, hipStream_t stream) {
   MMB_REQUIRE(n >= 0 && t > 0 && d > 0 && a_ > 0 && vd > 0);
-  MMB_REQUIRE(audio && visual && num_out && s_out && aux_out);
+  MMB_REQUIRE(audio && visual && num_out && s_out && aux_out && (s_half == 0 || s_half == 1));
   if (ids) {
     MMB_REQUIRE(table && v > 0 && (wtab32 || w_dense));
   } else {
@@ -749,38 +709,11 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.w_dense = w_dense;
   s.text_dense = text_dense; s.emb_dense = emb_dense; s.audio = audio; s.visual = visual;
   s.N = n; s.L = t; s.D = d; s.A = a_; s.Vd = vd; s.Kp = mmb_mm2_k(d, a_, vd);
-  s.num_out = num_out; s.s_out = s_out; s.aux_out = aux_out; s.flag = flag;
+  s.num_out = num_out; s.s_out = static_cast<float*>(s_out); s.aux_out = aux_out; s.flag = flag;
+  s.s_half = s_half;
   const bool vt = (d % 4 == 0) && (ids ? aligned16(table) : (aligned16(text_dense) && aligned16(emb_dense)));
   const bool va = (a_ % 4 == 0) && aligned16(audio);
   const bool vv = (vd % 4 == 0) && aligned16(visual);
-  // experiment selector (tools/kernel_bench.py sweeps; unset = default path)
-  static const char* cfg = getenv("MMB_STREAM_CFG");
-  if (cfg && vt && va && vv && t <= kWave && d > 256 && d <= 512 && a_ > 256 && a_ <= 512 &&
-      vd > 256 && vd <= 512 && aligned16(num_out) && aligned16(s_out)) {
-    const int c = atoi(cfg);
-    switch (c) {
-      case 1: return launch_wave<true, 2, 2, 2, 1, false>(s, stream);
-      case 2: return launch_wave<true, 2, 2, 2, 2, false>(s, stream);
-      case 3: return launch_wave<true, 2, 2, 2, 4, false>(s, stream);
-      case 4: return launch_wave<true, 2, 2, 2, 1, true>(s, stream);
-      case 5: return launch_wave<true, 2, 2, 2, 2, true>(s, stream);
-      case 6: return launch_wave<true, 2, 2, 2, 4, true>(s, stream);
-      case 7: return launch_wave<true, 2, 2, 2, 2, true>(s, stream, 256 * 4);
-      case 8: return launch_wave<true, 2, 2, 2, 2, true>(s, stream, 256 * 16);
-      case 9: return launch_wave3<4>(s, stream);
-      default: break;
-    }
-  }
-  if (!cfg && vt && va && vv && t <= kWave && aligned16(num_out) && aligned16(s_out) &&
-      (d + a_ + vd) / 4 <= 4 * kWave && false) {
-    const int upl = static_cast<int>(ceil_div((d + a_ + vd) / 4, kWave));
-    switch (upl) {
-      case 1: return launch_wave3<1>(s, stream);
-      case 2: return launch_wave3<2>(s, stream);
-      case 3: return launch_wave3<3>(s, stream);
-      default: return launch_wave3<4>(s, stream);
-    }
-  }
   if (vt && va && vv && t <= kWave && d <= 512 && a_ <= 512 && vd <= 512 && aligned16(num_out) &&
       aligned16(s_out)) {
     const int sel = (d > 256 ? 4 : 0) | (a_ > 256 ? 2 : 0) | (vd > 256 ? 1 : 0);
@@ -796,15 +729,22 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
     }
   }
   MMB_REQUIRE(d / (vt ? 4 : 1) <= kNT && a_ / (va ? 4 : 1) <= kNT && vd / (vv ? 4 : 1) <= kNT);
+  s.s_half = 0;
   const int sel = (vt ? 4 : 0) | (va ? 2 : 0) | (vv ? 1 : 0);
+  int rc;
   switch (sel) {
-    case 7: return launch_stream<true, 4, 4, 4>(s, stream);
-    case 6: return launch_stream<true, 4, 4, 1>(s, stream);
-    case 5: return launch_stream<true, 4, 1, 4>(s, stream);
-    case 4: return launch_stream<true, 4, 1, 1>(s, stream);
-    case 3: return launch_stream<true, 1, 4, 4>(s, stream);
-    case 2: return launch_stream<true, 1, 4, 1>(s, stream);
-    case 1: return launch_stream<true, 1, 1, 4>(s, stream);
-    default: return launch_stream<true, 1, 1, 1>(s, stream);
+    case 7: rc = launch_stream<true, 4, 4, 4>(s, stream); break;
+    case 6: rc = launch_stream<true, 4, 4, 1>(s, stream); break;
+    case 5: rc = launch_stream<true, 4, 1, 4>(s, stream); break;
+    case 4: rc = launch_stream<true, 4, 1, 1>(s, stream); break;
+    case 3: rc = launch_stream<true, 1, 4, 4>(s, stream); break;
+    case 2: rc = launch_stream<true, 1, 4, 1>(s, stream); break;
+    case 1: rc = launch_stream<true, 1, 1, 4>(s, stream); break;
+    default: rc = launch_stream<true, 1, 1, 1>(s, stream); break;
   }
+  if (rc != MMB_OK || !s_half) return rc;
+  split_rows_kernel<<<static_cast<unsigned>(n), 256, s.Kp * sizeof(float), stream>>>(
+      s.s_out, aux_out + 2 * n, s.Kp);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
 }

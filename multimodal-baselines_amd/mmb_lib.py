@@ -39,11 +39,14 @@ SIGNATURES = {
     "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "mmb_pc_remove": (_I, [_P, _P, _L, _I, _P, _I, _P, _P, _P]),
     "mmb_host_randn": (_I, [ctypes.c_uint32, _L, _P]),
+    "mmb_cu_count": (_I, [_I, _P]),
+    "mmb_stream_create_cu_mask": (_I, [_P, _I, _P]),
+    "mmb_stream_destroy": (_I, [_P]),
     "mmb_calc_weights": (_I, [_P, _L, _I, _P, _P, _P, _P, _P]),
     "mmb_mm2_k": (_I, [_I, _I, _I]),
     "mmb_mm2_ldw": (_I, [_I]),
-    "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P,
-                            _P, _P]),
+    "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _I,
+                            _P, _P, _P]),
     "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "mmb_mm2_split_bytes": (_S, [_I, _I, _I]),
     "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
@@ -119,3 +122,40 @@ def host_randn(seed: int, count: int):
     out = np.empty(count, dtype=np.float64)
     call("mmb_host_randn", seed, count, out.ctypes.data if count else None)
     return out
+
+
+def cu_count(device=None) -> int:
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    out = ctypes.c_int(0)
+    call("mmb_cu_count", dev.index or 0, ctypes.addressof(out))
+    return out.value
+
+
+class CUStream:
+    """A HIP stream restricted to the CUs in `cus` (libmmb
+    mmb_stream_create_cu_mask), usable as a torch stream via `.torch`."""
+
+    def __init__(self, cus, device):
+        n = max(cus) + 1
+        words = (ctypes.c_uint32 * ((n + 31) // 32))()
+        for c in cus:
+            words[c // 32] |= 1 << (c % 32)
+        handle = ctypes.c_void_p(0)
+        with torch.cuda.device(device):
+            call("mmb_stream_create_cu_mask", ctypes.addressof(words), len(words),
+                 ctypes.addressof(handle))
+        self.handle = handle.value
+        self.cus = list(cus)
+        self.torch = torch.cuda.ExternalStream(self.handle, device=device)
+
+    def close(self):
+        if self.handle:
+            torch.cuda.synchronize()
+            call("mmb_stream_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

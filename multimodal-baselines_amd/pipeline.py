@@ -247,33 +247,52 @@ def ctypes_ptr_array(ptrs):
 
 
 def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=None,
-               text_dense=None, emb_dense=None, w_dense=None, flag=None, out=None):
+               text_dense=None, emb_dense=None, w_dense=None, flag=None, out=None,
+               s_half: bool = True):
+    """a6-a8 frame sums.  s_half=True (default) writes s as fp16 [n, 2*kp]
+    (hi | lo planes of the row-scaled sums, the x3 projection's A operand);
+    s_half=False writes fp32 [n, kp] for the fp32-MFMA projection."""
     kp, _ = mm2_dims(d, a, vd)
     dev = audio.device
     if out is None:
         out = (torch.empty((n, d), dtype=torch.float32, device=dev),
-               torch.empty((n, kp), dtype=torch.float32, device=dev),
+               s_buffer(n, kp, s_half, dev),
                torch.empty((3, n), dtype=torch.float32, device=dev))
     num, s, aux = out
+    if s.dtype != (torch.float16 if s_half else torch.float32):
+        raise L.MMBError("s buffer dtype does not match s_half")
     V = table.shape[0] if table is not None else 0
     L.call("mmb_mm2_stream", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32), L.ptr(text_dense),
            L.ptr(emb_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
-           L.ptr(num), L.ptr(s), L.ptr(aux), L.ptr(flag), L.stream_ptr())
+           L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag), L.stream_ptr())
     return num, s, aux
 
 
-def mm2_project(s, num, aux, proj: MMB2Projection, out=None, fp32_mfma: bool = False):
-    """Default: fp16 hi/lo split MFMA GEMM (mmb_mm2_project_x3); fp32_mfma=True
-    selects the plain fp32-MFMA kernel (same epilogue)."""
+def s_buffer(n: int, kp: int, s_half: bool, device) -> torch.Tensor:
+    if s_half:
+        return torch.empty((n, 2 * kp), dtype=torch.float16, device=device)
+    return torch.empty((n, kp), dtype=torch.float32, device=device)
+
+
+def x3_supported(proj: "MMB2Projection") -> bool:
+    """The x3 kernel's LDS chunk rings fit d < 320 (the D=300 configs)."""
+    return proj.ldw <= 320
+
+
+def mm2_project(s, num, aux, proj: MMB2Projection, out=None):
+    """fp16 s (s_half stream output): the fp16 hi/lo split MFMA GEMM
+    (mmb_mm2_project_x3); fp32 s: the fp32-MFMA GEMM.  Same epilogue."""
     n = num.shape[0]
     if out is None:
         out = torch.empty((n, proj.d), dtype=torch.float32, device=num.device)
-    if fp32_mfma or proj.ldw > 320:  # x3 kernel's LDS buffers fit d < 320 (D=300 configs)
+    if s.dtype == torch.float32:
         L.call("mmb_mm2_project", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wm), proj.ldw,
                L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
-    else:
+    elif s.dtype == torch.float16:
         L.call("mmb_mm2_project_x3", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wsplit),
                proj.ldw, L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
+    else:
+        raise L.MMBError(f"unsupported s dtype {s.dtype}")
     return out
 
 
@@ -326,7 +345,8 @@ class FusedStep:
     """
 
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
-                 n_total: int | None = None, row0: int = 0, chunks: int | None = None):
+                 n_total: int | None = None, row0: int = 0, chunks: int | None = None,
+                 side_cus: int = 0, side_layout: str = "strided"):
         self.inp = inputs
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
@@ -338,7 +358,8 @@ class FusedStep:
         self.proj = MMB2Projection(networks, self.d, self.a, self.vd, self.t, dev)
         kp = self.proj.kp
         self.num = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
-        self.s = torch.empty((self.n, kp), dtype=torch.float32, device=dev)
+        self.s_half = x3_supported(self.proj)
+        self.s = s_buffer(self.n, kp, self.s_half, dev)
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
@@ -358,6 +379,20 @@ class FusedStep:
         self.aux_flat = torch.empty((3 * self.n,), dtype=torch.float32, device=dev)
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
+        self.main = None
+        self._cu_streams = []
+        if side_cus and self.side is not None:
+            # disjoint CU sets: the stream kernel on `main`, the projection +
+            # Gram of the previous chunk on `side`
+            n_cu = L.cu_count(dev)
+            if side_layout == "strided":
+                step_cu = n_cu / side_cus
+                side_set = sorted({int(i * step_cu) for i in range(side_cus)})
+            else:
+                side_set = list(range(n_cu - side_cus, n_cu))
+            main_set = [c for c in range(n_cu) if c not in set(side_set)]
+            self._cu_streams = [L.CUStream(main_set, dev), L.CUStream(side_set, dev)]
+            self.main, self.side = self._cu_streams[0].torch, self._cu_streams[1].torch
 
     def aux_of(self, c: int) -> torch.Tensor:
         r0, r1 = self.bounds[c]
@@ -375,7 +410,7 @@ class FusedStep:
         inp = self.inp
         mm2_stream(r1 - r0, self.t, self.d, self.a, self.vd, inp["audio"][r0:r1],
                    inp["visual"][r0:r1], ids32=self.ids[r0:r1], table=self.table,
-                   wtab32=inp["wtab"], flag=self.flag,
+                   wtab32=inp["wtab"], flag=self.flag, s_half=self.s_half,
                    out=(self.num[r0:r1], self.s[r0:r1], self.aux_of(c)))
 
     def _consume_chunk(self, c: int):
@@ -401,18 +436,24 @@ class FusedStep:
             with mark("mm2_project+gram"):
                 self._consume_chunk(0)
         else:
-            main = torch.cuda.current_stream(self.table.device)
-            self.side.wait_stream(main)
+            caller = torch.cuda.current_stream(self.table.device)
+            main = self.main if self.main is not None else caller
+            if main is not caller:
+                main.wait_stream(caller)
+            self.side.wait_stream(caller)
             with torch.cuda.stream(self.side), mark("mm2_prepare"):
                 self.proj.refresh()
-            for c in range(len(self.bounds)):
-                with mark("mm2_stream"):
-                    self._stream_chunk(c)
-                self.side.wait_stream(main)
-                with torch.cuda.stream(self.side), mark("mm2_project+gram"):
-                    self._consume_chunk(c)
+            with torch.cuda.stream(main):
+                for c in range(len(self.bounds)):
+                    with mark("mm2_stream"):
+                        self._stream_chunk(c)
+                    self.side.wait_stream(main)
+                    with torch.cuda.stream(self.side), mark("mm2_project+gram"):
+                        self._consume_chunk(c)
             with mark("join"):
-                main.wait_stream(self.side)
+                caller.wait_stream(self.side)
+                if main is not caller:
+                    caller.wait_stream(main)
         with mark("pc_start"):
             if self.n_total >= d:
                 z0, transposed = omega(d, k, self.table.device), False

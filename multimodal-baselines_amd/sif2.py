@@ -55,7 +55,7 @@ def estimate_embedding_overall_gpu2(data, masks, networks, sentence_weights, emb
                            "simplesif.py:825-830)")
     proj = P.MMB2Projection(networks, d, a, vd, t, dev)
     num, s, aux = P.mm2_stream(n, t, d, a, vd, audio, visual, text_dense=text, emb_dense=emb,
-                               w_dense=sw)
+                               w_dense=sw, s_half=P.x3_supported(proj))
     if n == 1:
         # the reference squeezes the batch dim away (sif2.py:200-201) and then
         # fails in cs.norm(dim=1) (:207); keep that error behaviour

@@ -135,7 +135,8 @@ def test_fused_step_vs_oracle(gpu, N, T, A, Vd):
 def test_fp16_split_projection_vs_fp32_and_oracle(gpu, scale, pad):
     """The fp16 hi/lo split GEMM (bench path) and the fp32-MFMA GEMM both meet
     the 1e-5 bar, also for frames of very large / very small magnitude (the
-    per-row and per-column power-of-2 scaling keeps fp16 in range)."""
+    per-row and per-column power-of-2 scaling keeps fp16 in range).  N=700 is
+    not a multiple of the 128-row tile (clamped tail rows)."""
     N, T, A, Vd, V = 700, 40, 300, 300, 5000
     torch.manual_seed(3)
     gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None)
@@ -147,11 +148,21 @@ def test_fp16_split_projection_vs_fp32_and_oracle(gpu, scale, pad):
     ids32 = torch.as_tensor(ids, dtype=torch.int32, device=gpu)
     au, vi = torch.tensor(audio, device=gpu), torch.tensor(visual, device=gpu)
     proj = P.MMB2Projection(gen.to(gpu).networks(), 300, A, Vd, T, gpu)
-    num, s, aux = P.mm2_stream(N, T, 300, A, Vd, au, vi, ids32=ids32,
-                               table=torch.tensor(E, device=gpu),
-                               wtab32=torch.tensor(wt, device=gpu, dtype=torch.float32))
+    table = torch.tensor(E, device=gpu)
+    wtab = torch.tensor(wt, device=gpu, dtype=torch.float32)
+    num, s, aux = P.mm2_stream(N, T, 300, A, Vd, au, vi, ids32=ids32, table=table, wtab32=wtab)
+    assert s.dtype == torch.float16 and s.shape == (N, 2 * proj.kp)
     x3 = P.mm2_project(s, num, aux, proj).cpu().numpy()
-    f32 = P.mm2_project(s, num, aux, proj, fp32_mfma=True).cpu().numpy()
+    num32, s32, aux32 = P.mm2_stream(N, T, 300, A, Vd, au, vi, ids32=ids32, table=table,
+                                     wtab32=wtab, s_half=False)
+    assert torch.equal(num32, num) and torch.equal(aux32, aux)
+    f32 = P.mm2_project(s32, num32, aux32, proj).cpu().numpy()
+    # the split is exact to fp16 hi + lo of the row-scaled fp32 sums
+    sc = aux32[2][:, None]
+    xs = s32 * sc
+    hi = xs.half()
+    assert torch.equal(s[:, :proj.kp], hi)
+    assert torch.equal(s[:, proj.kp:], (xs - hi.float()).half())
     sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
     text = E[ids]
     ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),

@@ -75,8 +75,12 @@ def main():
         res["project"] = timed(lambda: P.mm2_project(step.s, step.num, step.aux, step.proj,
                                                      out=step.mmb2), args.reps)
     if "project32" in which:
-        res["project32"] = timed(lambda: P.mm2_project(step.s, step.num, step.aux, step.proj,
-                                                       out=step.mmb2, fp32_mfma=True), args.reps)
+        s32 = P.s_buffer(step.n, step.proj.kp, False, dev)
+        P.mm2_stream(step.n, step.t, 300, 300, 300, inp["audio"], inp["visual"], ids32=inp["ids"],
+                     table=inp["table"], wtab32=inp["wtab"], s_half=False,
+                     out=(step.num, s32, step.aux))
+        res["project32"] = timed(lambda: P.mm2_project(s32, step.num, step.aux, step.proj,
+                                                       out=step.mmb2), args.reps)
     for k, v in res.items():
         print(f"{k}: {v:.4f} ms")
 
