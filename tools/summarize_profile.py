@@ -16,11 +16,35 @@ import csv
 import json
 import os
 import re
+import subprocess
 import sys
 
 
+def demangle(name):
+    if name.startswith("_Z"):
+        try:
+            out = subprocess.run(["c++filt", name], capture_output=True, text=True,
+                                 check=True).stdout.strip()
+            if out != name:
+                return out
+        except (OSError, subprocess.CalledProcessError):
+            pass
+    if name.startswith("_ZN"):  # binutils c++filt lacks _Float16 (DF16_): keep the nested name
+        parts, i = [], 3
+        while i < len(name) and name[i].isdigit():
+            j = i
+            while name[j].isdigit():
+                j += 1
+            n = int(name[i:j])
+            parts.append(name[j:j + n])
+            i = j + n
+        if parts:
+            return "::".join(parts)
+    return name
+
+
 def short(name):
-    name = re.sub(r"\(.*", "", name)
+    name = re.sub(r"\(.*", "", demangle(name))
     name = name.replace("void ", "").replace("mmb::", "")
     return name[:70]
 
@@ -45,7 +69,7 @@ def main(src, tag):
         out = {}
         for r in csv.DictReader(open(path)):
             k = short(r["Kernel_Name"])
-            if "mmb" not in r["Kernel_Name"]:
+            if "mmb" not in demangle(r["Kernel_Name"]):
                 continue
             out.setdefault(k, []).append(float(r["Counter_Value"]))
         return out
@@ -63,7 +87,7 @@ def main(src, tag):
         traffic[k] = b
         lines.append(f"| `{k}` | {len(fetch[k])} | {f:.0f} | {w:.0f} | {b:.4g} |")
     lines.append("")
-    stream = [v for k, v in traffic.items() if "utt_stream_kernel" in k]
+    stream = [v for k, v in traffic.items() if "utt_stream_kernel" in k or "utt_wave_kernel" in k]
     cfg = bench["config"]
     tj = {"tag": tag, "utts_per_launch": cfg["utts_per_gpu"], "tokens": cfg["tokens"],
           "mm2_stream_hbm_bytes_per_launch": stream[0] if stream else None,
