@@ -115,6 +115,55 @@ __global__ __launch_bounds__(1024) void mm2_prepare_c0_kernel(PrepArgs p) {
   }
 }
 
+// The same c0 with the features of all six combinations cut into S splits:
+// block (column group, split) reduces its split into part[split][ldw] (f64),
+// mm2_c0_reduce_kernel sums the splits in a fixed order (deterministic).
+constexpr int kC0Splits = 64;
+__global__ __launch_bounds__(1024) void mm2_prepare_c0_part_kernel(PrepArgs p, double* part) {
+  __shared__ double s_part[16][64];
+  const int jl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + jl, split = blockIdx.y;
+  int Ftot = 0;
+  for (int k = 0; k < 6; ++k) Ftot += combo_width(k, p.D, p.A, p.Vd);
+  const int per = (Ftot + kC0Splits - 1) / kC0Splits;
+  const int e0 = split * per, e1 = min(Ftot, e0 + per);
+  double acc = 0.0;
+  if (j <= p.D) {
+    for (int e = e0 + g; e < e1; e += 16) {
+      int k = 0, f = e;
+      while (f >= combo_width(k, p.D, p.A, p.Vd)) {
+        f -= combo_width(k, p.D, p.A, p.Vd);
+        ++k;
+      }
+      const double b = p.bmu[k][f];
+      const double al = 1.0 / exp(2.0 * static_cast<double>(p.bls[k][f]));
+      if (j < p.D) {
+        const double wmu = p.wmu[k][static_cast<int64_t>(f) * p.D + j];
+        const double wls = p.wls[k][static_cast<int64_t>(f) * p.D + j];
+        acc += -al * b * wmu + al * b * b * wls - wls;
+      } else {
+        acc += -al * b + al * b * b - 1.0;
+      }
+    }
+  }
+  s_part[g][jl] = acc;
+  __syncthreads();
+  if (g == 0 && j < p.ldw) {
+    double s = 0.0;
+    for (int q = 0; q < 16; ++q) s += s_part[q][jl];
+    part[static_cast<int64_t>(split) * p.ldw + j] = s;
+  }
+}
+
+__global__ void mm2_c0_reduce_kernel(const double* __restrict__ part, int D, int ldw, int T,
+                                     float* __restrict__ c0) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ldw) return;
+  double s = 0.0;
+  for (int q = 0; q < kC0Splits; ++q) s += part[static_cast<int64_t>(q) * ldw + j];
+  c0[j] = (j <= D) ? static_cast<float>(s * T) : 0.f;
+}
+
 // ------------------------------------------------------------------ projection
 // fp32 MFMA 32x32x2: lane l holds A[l&31][l>>5] and B[l>>5][l&31];
 // C/D: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
@@ -563,8 +612,18 @@ extern "C" int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_m
   const int64_t total = static_cast<int64_t>(p.Kp) * ldw;
   mm2_prepare_wm_kernel<<<static_cast<int>(std::min<int64_t>(ceil_div(total, 256), 4096)), 256, 0, stream>>>(p);
   MMB_LAUNCH_CHECK();
-  mm2_prepare_c0_kernel<<<ldw / 64, 1024, 0, stream>>>(p);
-  MMB_LAUNCH_CHECK();
+  if (wsplit && p.Kp >= 128) {
+    // the split image is written last: its memory is the c0 partials' scratch
+    // (kC0Splits x ldw doubles <= 2 x ldw x Kp halves for every Kp >= 128)
+    double* part = static_cast<double*>(wsplit);
+    mm2_prepare_c0_part_kernel<<<dim3(ldw / 64, kC0Splits), 1024, 0, stream>>>(p, part);
+    MMB_LAUNCH_CHECK();
+    mm2_c0_reduce_kernel<<<static_cast<int>(ceil_div(ldw, 256)), 256, 0, stream>>>(part, d, ldw, t, c0);
+    MMB_LAUNCH_CHECK();
+  } else {
+    mm2_prepare_c0_kernel<<<ldw / 64, 1024, 0, stream>>>(p);
+    MMB_LAUNCH_CHECK();
+  }
   if (wsplit) {
     _Float16* img = static_cast<_Float16*>(wsplit);
     float* ci = reinterpret_cast<float*>(img + 2 * static_cast<size_t>(ldw) * p.Kp);

@@ -277,6 +277,18 @@ __global__ void xt_omega_kernel(const float* __restrict__ num, const float* __re
 }
 
 // ------------------------------------------------------------------ pc_solve
+#ifdef MMB_PC_PROBE  // phase timestamps for tools/pc_probe.hip (never in libmmb)
+__device__ unsigned long long g_pc_probe[64];
+#define PC_MARK(i)                                      \
+  do {                                                  \
+    __syncthreads();                                    \
+    if (threadIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
+  } while (0)
+#else
+#define PC_MARK(i) \
+  do {             \
+  } while (0)
+#endif
 constexpr int kMaxD = 512;
 constexpr int kMaxK = 16;
 constexpr int kSolveNT = 1024;
@@ -365,15 +377,18 @@ __device__ void jacobi_wave(double* A, double* V, int k, int lane) {
     }
     off = wave_sum(off);
     dia = wave_sum(dia);
-    // converged when the off-diagonal mass is at fp64 rounding level
-    // (|a_pq| ~ 1e-15 |lambda|); a tighter bar is unreachable and only spins
-    if (off <= 1e-30 * dia) break;
+    // converged when the off-diagonal mass is ~1e-14 of the diagonal's: the
+    // rotations' own rounding (~1e-16 |lambda_max|) keeps regenerating
+    // off-diagonal entries, so a bar at the rounding level itself is never met
+    if (off <= 1e-28 * dia) break;
+    bool rotated = false;
     for (int p = 0; p < k - 1; ++p) {
       for (int q = p + 1; q < k; ++q) {
         const double apq = A[p * k + q];
         const double app = A[p * k + p], aqq = A[q * k + q];
-        // negligible next to both diagonal entries: rotating would change nothing
-        if (fabs(apq) <= 1e-18 * (fabs(app) + fabs(aqq))) continue;
+        // at rounding level next to both diagonal entries: rotating changes nothing
+        if (fabs(apq) <= 2e-16 * (fabs(app) + fabs(aqq))) continue;
+        rotated = true;
         const double theta = (aqq - app) / (2.0 * apq);
         double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
         if (theta < 0.0) t = -t;
@@ -406,6 +421,7 @@ __device__ void jacobi_wave(double* A, double* V, int k, int lane) {
         wave_lds_sync();
       }
     }
+    if (!rotated) break;
   }
 }
 
@@ -504,18 +520,23 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __rest
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
 
   __shared__ int s_fail;
+  PC_MARK(0);
   for (int e = tid; e < D * k; e += kSolveNT) sZ[e] = z0[e];
   __syncthreads();
   orth_block(sZ, D, k, sW, sL, sLi, &s_fail);
+  PC_MARK(1);
   for (int it = 0; it < n_iter; ++it) {
     gz_product(G, sZ, sGZ, D, k);
     __syncthreads();
+    PC_MARK(2 + 2 * it);
     for (int e = tid; e < D * k; e += kSolveNT) sZ[e] = sGZ[e];
     __syncthreads();
     orth_block(sZ, D, k, sW, sL, sLi, &s_fail);
+    PC_MARK(3 + 2 * it);
   }
   gz_product(G, sZ, sGZ, D, k);
   __syncthreads();
+  PC_MARK(40);
 
   if (transposed) {
     small_gram(sZ, sGZ, sA, D, k);  // Q^T G Q
@@ -585,6 +606,7 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __rest
     __syncthreads();
   }
 
+  PC_MARK(41);
   if (wave == 0) {
     jacobi_wave(sA, sV, k, lane);
     if (lane == 0) {  // eigenvalues descending (selection; first max wins ties)
@@ -600,6 +622,7 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __rest
     }
   }
   __syncthreads();
+  PC_MARK(42);
 
   for (int c = 0; c < npc; ++c) {
     const int col = s_order[c];
@@ -652,6 +675,409 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __rest
     if (tid < D) pc_out[c * D + tid] = v * scale;
     __syncthreads();
   }
+  PC_MARK(43);
+}
+
+// ------------------------------------------------------------------ pc_solve (D <= 320)
+// The same solve with every D-long contraction on the fp64 matrix pipe
+// (MFMA 16x16x4): the block is kept 16 columns wide in LDS (columns >= k and
+// rows >= D zero), so
+//   G Z      = 16-row tiles of G (A operand, read straight from L2: G is
+//              symmetric, so a fragment is 16 consecutive doubles of 4 rows)
+//              times Z (B operand from LDS);
+//   X^T Y    = one 16x16 MFMA accumulator per wave over a quarter-strided
+//              share of the rows, the 16 partials summed in a fixed order.
+// Everything k x k (Cholesky, triangular inverse, Jacobi) stays on one wave.
+constexpr int kP16MaxD = 320;
+constexpr int kP16W = 16;  // block width (k <= 16)
+
+struct P16Lds {
+  double* Z;     // [Dp][16]
+  double* GZ;    // [Dp][16]
+  double* part;  // [16 waves][256]
+};
+
+// M (k x k, compact) = X^T Y over the Dp rows of two [Dp][16] blocks.
+__device__ void p16_gram(const double* X, const double* Y, int Dp, int k, double* part, double* M) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  f64x4 acc = {0, 0, 0, 0};
+  for (int p = 4 * wave; p < Dp; p += 4 * (kSolveNT / kWave)) {
+    const int o = (p + (lane >> 4)) * kP16W + (lane & 15);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[o], Y[o], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+  __syncthreads();
+  if (tid < 256) {
+    const int i = tid >> 4, j = tid & 15;
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < kSolveNT / kWave; ++w) s += part[w * 256 + tid];
+    if (i < k && j < k) M[i * k + j] = s;
+  }
+  __syncthreads();
+}
+
+// GZ = G Z (G symmetric [D][D] in global memory / L2).  16 k-steps of loads
+// are issued before their MFMAs (one L2 latency per batch, not per step);
+// two accumulators alternate so consecutive MFMAs are independent.
+__device__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double* Z, double* GZ) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int mt = Dp / 16;
+  for (int t = wave; t < mt; t += kSolveNT / kWave) {
+    const int p = t * 16 + (lane & 15);
+    const int pc = min(p, D - 1);
+    f64x4 acc0 = {0, 0, 0, 0}, acc1 = acc0;
+    for (int q0 = 0; q0 < Dp; q0 += 64) {
+      double g[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int q = q0 + 4 * s + (lane >> 4);
+        // clamped address, unconditional load, selected after (keeps loads in flight)
+        g[s] = G[static_cast<int64_t>(min(q, D - 1)) * D + pc];
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int q = q0 + 4 * s + (lane >> 4);
+        const double a = (p < D && q < D) ? g[s] : 0.0;
+        const double b = Z[min(q, Dp - 1) * kP16W + (lane & 15)];
+        if (s & 1) {
+          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc1, 0, 0, 0);
+        } else {
+          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc0, 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+      GZ[(t * 16 + (lane >> 4) + 4 * reg) * kP16W + (lane & 15)] = acc0[reg] + acc1[reg];
+  }
+}
+
+// Cholesky W = L L^T (k x k, compact) and Linv = L^{-1} by one wave: lane i
+// keeps row i of the trailing matrix in registers (right-looking, column j's
+// multipliers broadcast by shuffles); lane c then solves L x = e_c.  *fail is
+// set if a pivot is not positive (the pivot is then replaced by 1).
+__device__ void p16_chol(const double* sW, double* sL, double* sLi, int k, int lane, int* fail) {
+  double w[kMaxK], l[kMaxK];
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m) {
+    w[m] = (lane < k && m < k) ? sW[lane * k + m] : 0.0;
+    l[m] = 0.0;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < kMaxK; ++j) {
+    if (j < k) {
+      const double djj = __shfl(w[j], j, kWave);
+      bad = bad || !(djj > 0.0);
+      const double s = sqrt(djj > 0.0 ? djj : 1.0);
+      const double lij = (lane == j) ? s : (lane > j ? w[j] / s : 0.0);
+      l[j] = lij;
+#pragma unroll
+      for (int m = j + 1; m < kMaxK; ++m) w[m] -= lij * __shfl(lij, m, kWave);
+    }
+  }
+  if (bad && lane == 0) *fail = 1;
+  if (lane < k) {
+#pragma unroll
+    for (int m = 0; m < kMaxK; ++m)
+      if (m < k) sL[lane * k + m] = l[m];
+  }
+  wave_lds_sync();
+  // column c = lane of Linv: forward substitution, L entries read as broadcasts
+  double x[kMaxK];
+#pragma unroll
+  for (int i = 0; i < kMaxK; ++i) {
+    x[i] = 0.0;
+    if (i < k) {
+      double s = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < i; ++m) s -= sL[i * k + m] * x[m];
+      x[i] = s / sL[i * k + i];
+    }
+  }
+  if (lane < k) {
+#pragma unroll
+    for (int i = 0; i < kMaxK; ++i)
+      if (i < k) sLi[i * k + lane] = (i < lane) ? 0.0 : x[i];
+  }
+  wave_lds_sync();
+}
+
+// Top eigenvector of the symmetric positive semi-definite A (k x k, compact,
+// LDS) by one wave: B = A (16 x 16, zero padded) is squared 32 times on the
+// fp64 matrix pipe, B <- B B / trace(B B), so B -> v v^T along the top
+// eigenvector (any ratio lambda_2 / lambda_1 < 1 - 1e-9 is resolved); the
+// f64 16x16 accumulator layout (row (l>>4) + 4 r, column l&15) IS the operand
+// layout of the next squaring (B symmetric), so B never leaves the
+// registers.  v = the column of B with the largest diagonal, normalised, then
+// two Rayleigh steps on A.  Returns lambda = v^T A v; u[0..k) = v.
+__device__ double p16_top_eig(const double* A, int k, int lane, double* u) {
+  const int c = lane & 15, r0 = lane >> 4;
+  f64x4 b;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = r0 + 4 * r;
+    b[r] = (row < k && c < k) ? A[row * k + c] : 0.0;
+  }
+  for (int it = 0; it < 32; ++it) {
+    f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(b[s], b[s], acc, 0, 0, 0);
+    double tr = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r0 + 4 * r == c) tr += acc[r];
+    tr = wave_sum(tr);
+    const double inv = tr > 0.0 ? 1.0 / tr : 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[r] = acc[r] * inv;
+  }
+  // column with the largest diagonal entry (first index on ties)
+  double dg = -1.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (r0 + 4 * r == c && c < k) dg = b[r];
+  int jb = c;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double od = __shfl_xor(dg, o, kWave);
+    const int oj = __shfl_xor(jb, o, kWave);
+    if (od > dg || (od == dg && oj < jb)) {
+      dg = od;
+      jb = oj;
+    }
+  }
+  if (c == jb) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r0 + 4 * r < k) u[r0 + 4 * r] = b[r];
+  }
+  wave_lds_sync();
+  double lam = 0.0;
+  for (int step = 0; step < 3; ++step) {
+    // lane i < k: y_i = (A u)_i; normalise
+    double y = 0.0;
+    if (lane < k) {
+      for (int m = 0; m < k; ++m) y += A[lane * k + m] * u[m];
+    }
+    const double ui = lane < k ? u[lane] : 0.0;
+    const double nrm2 = wave_sum(lane < k ? ui * ui : 0.0);
+    lam = wave_sum(ui * y) / nrm2;  // Rayleigh quotient of the current u
+    if (step == 2) {
+      if (lane < k) u[lane] = ui / sqrt(nrm2);
+    } else {
+      const double yn = sqrt(wave_sum(y * y));
+      wave_lds_sync();
+      if (lane < k) u[lane] = yn > 0.0 ? y / yn : ui;
+    }
+    wave_lds_sync();
+  }
+  return lam;
+}
+
+// Orthonormalise the k columns of Z [Dp][16]: equilibration, CholeskyQR twice;
+// wave-0 MGS^2 on a compact copy if a pivot fails (extreme ill-conditioning).
+__device__ void p16_orth(double* Z, int D, int Dp, int k, double* part, double* sW, double* sL,
+                         double* sLi, int* s_fail) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  for (int pass = 0; pass < 3; ++pass) {
+    p16_gram(Z, Z, Dp, k, part, sW);
+    if (pass == 0) {
+      if (tid < D) {
+        for (int j = 0; j < k; ++j) Z[tid * kP16W + j] *= 1.0 / sqrt(sW[j * k + j]);
+      }
+      __syncthreads();
+      continue;
+    }
+    if (wave == 0) {
+      if (lane == 0) *s_fail = 0;
+      wave_lds_sync();
+      p16_chol(sW, sL, sLi, k, lane, s_fail);
+    }
+    __syncthreads();
+    if (*s_fail) {
+      if (wave == 0) {
+        // compact [D][k] copy through the partial buffer (D*k <= 16*256 doubles)
+        for (int e = lane; e < D * k; e += kWave) part[e] = Z[(e / k) * kP16W + e % k];
+        wave_lds_sync();
+        orth_wave(part, D, k, lane);
+        for (int e = lane; e < D * k; e += kWave) Z[(e / k) * kP16W + e % k] = part[e];
+      }
+      __syncthreads();
+      return;
+    }
+    if (tid < D) {  // row p: z <- z L^{-T}
+      double z[kP16W];
+#pragma unroll
+      for (int m = 0; m < kP16W; ++m) z[m] = Z[tid * kP16W + m];
+      for (int j = 0; j < k; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < kP16W; ++m)
+          if (m <= j) s += z[m] * sLi[j * k + m];
+        Z[tid * kP16W + j] = s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kSolveNT) void pc_solve16_kernel(const double* __restrict__ G, int D,
+                                                              const double* __restrict__ z0, int k,
+                                                              int npc, int n_iter, int transposed,
+                                                              double* __restrict__ pc_out) {
+  extern __shared__ __attribute__((aligned(16))) double p16_lds[];
+  const int Dp = (D + 15) / 16 * 16;
+  double* sZ = p16_lds;
+  double* sGZ = sZ + Dp * kP16W;
+  double* part = sGZ + Dp * kP16W;  // max(16 x 256, Dp x 16): partials / fallback copy
+  __shared__ double sA[kMaxK * kMaxK], sV[kMaxK * kMaxK], sW[kMaxK * kMaxK];
+  __shared__ double sL[kMaxK * kMaxK], sLi[kMaxK * kMaxK], sT[kMaxK * kMaxK];
+  __shared__ double sy[kMaxK];
+  __shared__ double s_rd[kSolveNT / kWave];
+  __shared__ double s_rv[kSolveNT / kWave];
+  __shared__ int s_ri[kSolveNT / kWave];
+  __shared__ double sU[kMaxK * kMaxK];  // eigenvectors of A, largest first
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+
+  PC_MARK(0);
+  for (int e = tid; e < Dp * kP16W; e += kSolveNT) {
+    const int p = e / kP16W, j = e % kP16W;
+    sZ[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
+    sGZ[e] = 0.0;
+  }
+  __syncthreads();
+  p16_orth(sZ, D, Dp, k, part, sW, sL, sLi, &s_fail);
+  PC_MARK(1);
+  double* Z = sZ;
+  double* GZ = sGZ;
+  for (int it = 0; it < n_iter; ++it) {
+    p16_gz(G, D, Dp, Z, GZ);
+    __syncthreads();
+    PC_MARK(2 + 2 * it);
+    double* t = Z; Z = GZ; GZ = t;  // the product becomes the block
+    p16_orth(Z, D, Dp, k, part, sW, sL, sLi, &s_fail);
+    PC_MARK(3 + 2 * it);
+  }
+  p16_gz(G, D, Dp, Z, GZ);
+  __syncthreads();
+  PC_MARK(40);
+
+  if (transposed) {
+    p16_gram(Z, GZ, Dp, k, part, sA);  // Q^T G Q
+    symmetrize(sA, k);
+    __syncthreads();
+  } else {
+    p16_gram(Z, GZ, Dp, k, part, sW);   // W = Z^T G Z
+    p16_gram(GZ, GZ, Dp, k, part, sT);  // H = (GZ)^T (GZ)
+    symmetrize(sW, k);
+    symmetrize(sT, k);
+    __syncthreads();
+    if (wave == 0) {
+      p16_chol(sW, sL, sLi, k, lane, &s_fail);  // a failed pivot is clamped (W is SPD here)
+      for (int e = lane; e < k * k; e += kWave) {  // Linv H
+        const int i = e / k, j = e % k;
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sLi[i * k + m] * sT[m * k + j];
+        sV[e] = s;
+      }
+      wave_lds_sync();
+      for (int e = lane; e < k * k; e += kWave) {  // (Linv H) Linv^T
+        const int i = e / k, j = e % k;
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sV[i * k + m] * sLi[j * k + m];
+        sA[e] = s;
+      }
+      wave_lds_sync();
+      for (int e = lane; e < k * k; e += kWave) {
+        const int i = e / k, j = e % k;
+        if (i < j) {
+          const double m = 0.5 * (sA[i * k + j] + sA[j * k + i]);
+          sA[i * k + j] = m;
+          sA[j * k + i] = m;
+        }
+      }
+      wave_lds_sync();
+    }
+    __syncthreads();
+  }
+  PC_MARK(41);
+  if (wave == 0) {  // top npc eigenvectors of A, largest first (deflation)
+    for (int c = 0; c < npc; ++c) {
+      double* u = sU + c * kMaxK;
+      const double lam = p16_top_eig(sA, k, lane, u);
+      if (c + 1 < npc) {
+        for (int e = lane; e < k * k; e += kWave) sA[e] -= lam * u[e / k] * u[e % k];
+        wave_lds_sync();
+      }
+    }
+  }
+  __syncthreads();
+  PC_MARK(42);
+
+  for (int c = 0; c < npc; ++c) {
+    const double* u = sU + c * kMaxK;
+    if (!transposed) {
+      if (tid < k) {  // y = Linv^T u
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sLi[m * k + tid] * u[m];
+        sy[tid] = s;
+      }
+      __syncthreads();
+    }
+    double v = 0.0;
+    if (tid < D) {
+      if (transposed) {
+        for (int j = 0; j < k; ++j) v += Z[tid * kP16W + j] * u[j];
+      } else {
+        for (int j = 0; j < k; ++j) v += GZ[tid * kP16W + j] * sy[j];
+      }
+    }
+    // norm and first argmax |v|
+    double nn = wave_sum(v * v);
+    double best = (tid < D) ? fabs(v) : -1.0;
+    int bidx = (tid < D) ? tid : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best, o, kWave);
+      const int oi = __shfl_xor(bidx, o, kWave);
+      if (ob > best || (ob == best && oi < bidx)) {
+        best = ob;
+        bidx = oi;
+      }
+    }
+    if (lane == 0) {
+      s_rd[wave] = nn;
+      s_rv[wave] = best;
+      s_ri[wave] = bidx;
+    }
+    __syncthreads();
+    double tot = 0.0, bb = -1.0;
+    int bi = 0x7fffffff;
+    double vbest = 0.0;
+    for (int w = 0; w < kSolveNT / kWave; ++w) {
+      tot += s_rd[w];
+      if (s_rv[w] > bb || (s_rv[w] == bb && s_ri[w] < bi)) {
+        bb = s_rv[w];
+        bi = s_ri[w];
+      }
+    }
+    if (tid == bi) part[0] = v;  // sign of the largest-|.| entry (svd_flip)
+    __syncthreads();
+    vbest = part[0];
+    const double scale = (vbest < 0.0 ? -1.0 : 1.0) / sqrt(tot);
+    if (tid < D) pc_out[c * D + tid] = v * scale;
+    __syncthreads();
+  }
+  PC_MARK(43);
+}
+
+inline size_t p16_lds_bytes(int d) {
+  const size_t dp = (d + 15) / 16 * 16;
+  return (2 * dp * kP16W + (dp * kP16W > 16 * 256 ? dp * kP16W : 16 * 256)) * sizeof(double);
 }
 
 // ------------------------------------------------------------------ pc_remove
@@ -845,7 +1271,19 @@ extern "C" int mmb_pc_solve(const double* g, int d, const double* z0, int k, int
                             int transposed, double* pc_out, hipStream_t stream) {
   MMB_REQUIRE(g && z0 && pc_out && d > 1 && d <= kMaxD && k >= 1 && k <= kMaxK);
   MMB_REQUIRE(npc >= 1 && npc <= k && n_iter >= 0);
-  pc_solve_kernel<<<1, kSolveNT, 0, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
+  if (d <= kP16MaxD) {
+    const size_t lds = p16_lds_bytes(d);
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve16_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                static_cast<int>(p16_lds_bytes(kP16MaxD)));
+      attr = true;
+    }
+    pc_solve16_kernel<<<1, kSolveNT, lds, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
+  } else {
+    pc_solve_kernel<<<1, kSolveNT, 0, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
