@@ -203,6 +203,58 @@ int mmb_mlp_train(const float* latents, const float* labels, const int64_t* perm
                   float* w1, float* b1, float* w2, float* b2, float* step_loss, void* ws,
                   hipStream_t stream);
 
+/* ---------------------------------------------------------------- §8f row 1
+ * Latent-optimisation likelihoods (the objective simplesif.py:49-162,708-806
+ * minimises).  Word term = get_word_log_prob_angular2, losses.py:68-95;
+ * Gaussian term = get_normal_log_prob, losses.py:13-33, summed per modality
+ * combination by get_log_prob_matrix, losses.py:216-274.
+ *
+ * mmb_word_normalize: wn [v, mmb_word_pad(d)] = table / max(|row|, 1e-8),
+ * zero padded (torch cosine_similarity's x2 / |x2|; done once per table).   */
+int mmb_word_pad(int d);
+int mmb_word_normalize(const float* table, int64_t v, int d, float* wn, hipStream_t stream);
+
+/* lp[b] = sum_t mask[b,t] log(alpha_b w[b,t] + (1-alpha_b) score_bt / Z_b),
+ * Z_b = sum_{v<V} (1 - acos(cos(l_b, table_v))/pi), alpha_b = 1/(a Z_b + 1),
+ * score_bt = 1 - acos(cos(l_b, e_bt))/pi, e_bt = table[ids[b,t]] (ids non-null)
+ * or sent_dense[b,t,:].  d <= 320 for the MFMA Z kernel.  ws: scratch of
+ * mmb_word_workspace_bytes(b, d, v).  With want_grad, state [b,4], gsum
+ * [b, pad(d)] and cos_out [b, l] are written for mmb_word_logprob_backward.
+ * replaces: losses.get_word_log_prob_angular2 /root/reference/losses.py:68-95
+ *           (and get_word_log_prob_angular :36-66 with w = weights[data])  */
+size_t mmb_word_workspace_bytes(int64_t b, int d, int64_t v);
+int mmb_word_logprob_forward(const float* latents, int64_t b, int d, const float* wn, int64_t v,
+                             const int32_t* ids, const float* table, const float* sent_dense,
+                             int l, const float* w, const float* mask, float a, int want_grad,
+                             void* ws, float* lp, float* state, float* gsum, float* cos_out,
+                             hipStream_t stream);
+/* dlat[b,:] = dlp[b] * d lp_b / d latents[b,:] (autograd of losses.py:68-95). */
+int mmb_word_logprob_backward(const float* latents, int64_t b, int d, int64_t v,
+                              const int32_t* ids, const float* table, const float* sent_dense,
+                              int l, const float* w, const float* mask, float a,
+                              const float* state, const float* gsum, const float* cosv,
+                              const float* dlp, float* dlat, hipStream_t stream);
+
+/* stats [n][3][f] f64 = per-utterance masked frame sums (sum_t m, sum_t m x,
+ * sum_t m x^2) of x [n,t,f] (mask nullable = ones); streamed once per split. */
+int mmb_gauss_stats(const float* x, const float* mask, int64_t n, int t, int f, double* stats,
+                    hipStream_t stream);
+/* lp[k][b] = get_normal_log_prob(mu_k[b], sigma_k[b], x, mask) for combination
+ * k of modalities mods[k] (bit 0 text, 1 audio, 2 visual; features in that
+ * torch.cat order), from the stats of rows idx[b] (idx nullable = b).
+ * stats[3] / fm[3] / mods / mu / sigma are HOST arrays (of device pointers).
+ * replaces: losses.get_normal_log_prob /root/reference/losses.py:13-33 and the
+ *           per-modality loop of get_log_prob_matrix :249-256               */
+int mmb_gauss_loglik(const double* const* stats, const int* fm, const int64_t* idx, int64_t b,
+                     int nkeys, const int* mods, const float* const* mu,
+                     const float* const* sigma, float* lp, hipStream_t stream);
+/* dmu_k = dlp_k (M1 - mu M0)/s^2,  dsigma_k = dlp_k (Q/s^3 - M0/s)  (dmu/dsigma
+ * entries nullable). */
+int mmb_gauss_backward(const double* const* stats, const int* fm, const int64_t* idx, int64_t b,
+                       int nkeys, const int* mods, const float* const* mu,
+                       const float* const* sigma, const float* dlp, float* const* dmu,
+                       float* const* dsigma, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,194 @@
+"""Device side of the latent-optimisation objective.
+
+The reference (`losses.py:13-95, 216-274`) scores latent sentence embeddings
+with torch eager ops that materialise a [B, V, 300] cosine tensor for the word
+model and a [B, T, F] tensor per modality combination for the Gaussians, every
+step.  Here both terms are libmmb kernels (csrc/latent_kernels.hip) wrapped as
+torch autograd Functions with hand-written backward passes:
+
+  _WordLogProb   Z / G / h over the vocabulary (fused fp32-MFMA kernel) +
+                 per-token terms;  backward: closed-form d lp / d latents
+  _GaussLogProb  the Gaussian log-likelihood of every combination from
+                 per-utterance masked frame sums (streamed once per split);
+                 backward: closed-form d lp / d mu, d lp / d sigma
+
+Gradients flow to the latents and, through torch's own autograd, to the
+generator (norm + linears) and the regressor, exactly as in the reference
+training loops.  Nothing here falls back to CPU: without libmmb / a GPU the
+calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+import mmb_lib as L
+
+MOD_BITS = {"text": 1, "audio": 2, "visual": 4}
+
+
+def key_mods(key: str) -> int:
+    """Modality bits of a combination key (features in text, audio, visual order)."""
+    m = 0
+    if key.startswith("text"):
+        m |= 1
+    if "audio" in key:
+        m |= 2
+    if "visual" in key:
+        m |= 4
+    if m == 0:
+        raise KeyError(key)
+    return m
+
+
+# ------------------------------------------------------------------ word table
+class WordTable:
+    """A word-embedding table on device plus its row-normalised, 16-padded copy
+    (torch cosine_similarity's x / max(|x|, 1e-8)), computed once."""
+
+    def __init__(self, table: torch.Tensor):
+        dev = L.require_gpu()
+        self.table = table.detach().to(device=dev, dtype=torch.float32).contiguous()
+        self.V, self.D = self.table.shape
+        self.Dp = L.query("mmb_word_pad", self.D)
+        self.wn = torch.empty((self.V, self.Dp), dtype=torch.float32, device=dev)
+        L.call("mmb_word_normalize", L.ptr(self.table), self.V, self.D, L.ptr(self.wn),
+               L.stream_ptr())
+
+
+_table_cache: dict = {}
+
+
+def word_table(word_embeddings: torch.Tensor) -> WordTable:
+    """Cached WordTable for a (device) table tensor — keyed by storage and version,
+    so an in-place edit of the table is noticed."""
+    key = (word_embeddings.data_ptr(), tuple(word_embeddings.shape), word_embeddings._version,
+           str(word_embeddings.device), word_embeddings.dtype)
+    wt = _table_cache.get(key)
+    if wt is None:
+        if len(_table_cache) > 8:
+            _table_cache.clear()
+        wt = WordTable(word_embeddings)
+        _table_cache[key] = wt
+    return wt
+
+
+class _WordLogProb(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, latents, table: WordTable, ids, sent_dense, w, mask, a):
+        lat = latents.detach().float().contiguous()
+        B, D = lat.shape
+        if D != table.D:
+            raise ValueError(f"latent width {D} != word-table width {table.D}")
+        Lt = w.shape[1]
+        dev = lat.device
+        want = bool(ctx.needs_input_grad[0])
+        ws = torch.empty(max(L.query("mmb_word_workspace_bytes", B, D, table.V), 16),
+                         dtype=torch.uint8, device=dev)
+        lp = torch.empty((B,), dtype=torch.float32, device=dev)
+        state = torch.empty((B, 4), dtype=torch.float32, device=dev) if want else None
+        gsum = torch.empty((B, table.Dp), dtype=torch.float32, device=dev) if want else None
+        cosv = torch.empty((B, Lt), dtype=torch.float32, device=dev) if want else None
+        L.call("mmb_word_logprob_forward", L.ptr(lat), B, D, L.ptr(table.wn), table.V, L.ptr(ids),
+               L.ptr(table.table) if ids is not None else None, L.ptr(sent_dense), Lt, L.ptr(w),
+               L.ptr(mask), float(a), int(want), L.ptr(ws), L.ptr(lp), L.ptr(state), L.ptr(gsum),
+               L.ptr(cosv), L.stream_ptr())
+        if want:
+            ctx.save_for_backward(lat, ids, sent_dense, w, mask, state, gsum, cosv)
+            ctx.table, ctx.a = table, a
+        return lp
+
+    @staticmethod
+    def backward(ctx, dlp):
+        lat, ids, sent_dense, w, mask, state, gsum, cosv = ctx.saved_tensors
+        table = ctx.table
+        B, D = lat.shape
+        dlat = torch.empty_like(lat)
+        L.call("mmb_word_logprob_backward", L.ptr(lat), B, D, table.V, L.ptr(ids),
+               L.ptr(table.table) if ids is not None else None, L.ptr(sent_dense), w.shape[1],
+               L.ptr(w), L.ptr(mask), float(ctx.a), L.ptr(state), L.ptr(gsum), L.ptr(cosv),
+               L.ptr(dlp.float().contiguous()), L.ptr(dlat), L.stream_ptr())
+        return dlat, None, None, None, None, None, None
+
+
+def word_log_prob(latents, table: WordTable, w, mask, a, ids=None, sent_dense=None):
+    """lp [B] of the angular word model (losses.py:68-95) for tokens given by
+    `ids` [B, L] (rows of table) or `sent_dense` [B, L, D]; w, mask [B, L]."""
+    dev = latents.device
+    w = w.to(device=dev, dtype=torch.float32).contiguous()
+    mask = mask.to(device=dev, dtype=torch.float32).contiguous()
+    if ids is not None:
+        ids = ids.to(device=dev, dtype=torch.int32).contiguous()
+    if sent_dense is not None:
+        sent_dense = sent_dense.detach().to(device=dev, dtype=torch.float32).contiguous()
+    return _WordLogProb.apply(latents, table, ids, sent_dense, w, mask, a)
+
+
+# ------------------------------------------------------------------ Gaussians
+def gauss_stats(x: torch.Tensor, mask: torch.Tensor | None = None) -> torch.Tensor:
+    """[N, 3, F] f64 masked frame sums of x [N, T, F] (mask [N, T, F] or None)."""
+    x = x.detach().to(dtype=torch.float32).contiguous()
+    N, T, F = x.shape
+    st = torch.empty((N, 3, F), dtype=torch.float64, device=x.device)
+    m = None
+    if mask is not None:
+        m = mask.detach().to(device=x.device, dtype=torch.float32).expand(N, T, F).contiguous()
+    L.call("mmb_gauss_stats", L.ptr(x), L.ptr(m), N, T, F, L.ptr(st), L.stream_ptr())
+    return st
+
+
+def _ptr_array(ts, ctype=ctypes.c_void_p):
+    return (ctype * len(ts))(*[0 if t is None else t.data_ptr() for t in ts])
+
+
+class GaussStats:
+    """Per-modality frame sums of one data split: text / audio / visual."""
+
+    def __init__(self, text=None, audio=None, visual=None):
+        self.stats = [text, audio, visual]
+        self.fm = [0 if s is None else s.shape[2] for s in self.stats]
+
+
+class _GaussLogProb(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gs: GaussStats, idx, mods, *musig):
+        K = len(mods)
+        mus = [m.detach().float().contiguous() for m in musig[:K]]
+        sigs = [s.detach().float().contiguous() for s in musig[K:]]
+        B = mus[0].shape[0]
+        lp = torch.empty((K, B), dtype=torch.float32, device=mus[0].device)
+        st = _ptr_array(gs.stats)
+        fm = (ctypes.c_int * 3)(*gs.fm)
+        md = (ctypes.c_int * K)(*mods)
+        L.call("mmb_gauss_loglik", st, fm, L.ptr(idx), B, K, md, _ptr_array(mus), _ptr_array(sigs),
+               L.ptr(lp), L.stream_ptr())
+        ctx.gs, ctx.mods = gs, mods
+        ctx.save_for_backward(idx, *mus, *sigs)
+        return lp
+
+    @staticmethod
+    def backward(ctx, dlp):
+        saved = ctx.saved_tensors
+        idx = saved[0]
+        K = len(ctx.mods)
+        mus, sigs = saved[1:1 + K], saved[1 + K:]
+        B = mus[0].shape[0]
+        need_mu = ctx.needs_input_grad[3:3 + K]
+        need_s = ctx.needs_input_grad[3 + K:]
+        dmu = [torch.empty_like(m) if n else None for m, n in zip(mus, need_mu)]
+        dsg = [torch.empty_like(s) if n else None for s, n in zip(sigs, need_s)]
+        gs = ctx.gs
+        L.call("mmb_gauss_backward", _ptr_array(gs.stats), (ctypes.c_int * 3)(*gs.fm), L.ptr(idx),
+               B, K, (ctypes.c_int * K)(*ctx.mods), _ptr_array(mus), _ptr_array(sigs),
+               L.ptr(dlp.float().contiguous()), _ptr_array(dmu), _ptr_array(dsg), L.stream_ptr())
+        return (None, None, None, *dmu, *dsg)
+
+
+def gauss_log_prob(gs: GaussStats, keys, mus, sigmas, idx=None):
+    """lp [K, B]: get_normal_log_prob (losses.py:13-33) of every combination in
+    `keys`, mus/sigmas [B, F_k], from the frame sums of rows idx [B] (or 0..B)."""
+    mods = [key_mods(k) for k in keys]
+    if idx is not None:
+        idx = idx.to(device=mus[0].device, dtype=torch.int64).contiguous()
+    return _GaussLogProb.apply(gs, idx, mods, *mus, *sigmas)

@@ -55,6 +55,16 @@ SIGNATURES = {
     "mmb_mlp_eval": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_workspace_bytes": (_S, [_I, _I]),
     "mmb_mlp_train": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_word_pad": (_I, [_I]),
+    "mmb_word_normalize": (_I, [_P, _L, _I, _P, _P]),
+    "mmb_word_workspace_bytes": (_S, [_L, _I, _L]),
+    "mmb_word_logprob_forward": (_I, [_P, _L, _I, _P, _L, _P, _P, _P, _I, _P, _P, _F, _I, _P, _P,
+                                      _P, _P, _P, _P]),
+    "mmb_word_logprob_backward": (_I, [_P, _L, _I, _L, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P,
+                                       _P, _P]),
+    "mmb_gauss_stats": (_I, [_P, _P, _L, _I, _I, _P, _P]),
+    "mmb_gauss_loglik": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P]),
+    "mmb_gauss_backward": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

@@ -3,7 +3,8 @@
 Same classes and functions, same arguments, same printed/saved artefacts.
 The arithmetic runs on the GPU through libmmb:
 
-* SentimentModel.forward          -> mmb_mlp_forward
+* SentimentModel.forward          -> mmb_mlp_forward (no-grad calls; while autograd
+  records — the e2e joint objective — torch's device GEMMs carry the graph)
 * predict_sentiment / validation  -> mmb_mlp_eval (per-batch L1 means + predictions)
 * train_sentiment inner loop      -> mmb_mlp_train: every mini-batch step of a
   block of epochs (forward, L1 backward, SGD) in ONE single-workgroup launch,
@@ -26,6 +27,7 @@ import json
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 import torch.optim as optim
 from torch.utils.data import DataLoader, Dataset
 
@@ -76,6 +78,13 @@ class SentimentModel(nn.Module):
         dev = self.hidden1.weight.device
         if dev.type != "cuda":
             raise L.MMBError("SentimentModel runs on the GPU (libmmb); move it with .to('cuda')")
+        if torch.is_grad_enabled() and (inputs.requires_grad or
+                                        any(p.requires_grad for p in self.parameters())):
+            # differentiable forward (the e2e joint objective, simplesif.py:776-790):
+            # torch's GEMMs on the device carry the autograd graph
+            w1, b1, w2, b2 = _params(self)
+            x = F.linear(F.relu(F.linear(inputs.to(dev, torch.float32), w1, b1)), w2, b2)
+            return x.squeeze()
         home = inputs.device
         x = inputs.detach().to(dev, torch.float32)
         lead = x.shape[:-1]

@@ -109,3 +109,50 @@ def device_workload(N: int, T: int, V: int, D: int = 300, A: int = 300, Vd: int 
     audio.uniform_(-1.0, 1.0, generator=gen)
     visual.uniform_(-1.0, 1.0, generator=gen)
     return {"table": table, "wtab": wtab, "ids": ids, "audio": audio, "visual": visual}
+
+
+# ---------------------------------------------------------------- CLI datasets
+def mm_splits(seed: int = 0, sizes=(96, 32, 32), T: int = 12, V: int = 300, A_raw: int = 20,
+              Vd_raw: int = 14, dataset: str = "mosi", n_labels: int = 1):
+    """Seeded splits in the layout `utils.load_data` returns (utils.py:20-90):
+    (word2ix, word_embeddings [V, 300] f32, (train, valid, test)), each split a
+    dict of numpy arrays.
+
+    mosi: facet [N,T,Vd_raw], covarep [N,T,A_raw], text [N,T] aligned ids
+          (left-padded with 0), lengths, label [N], id.
+    pom:  facet, covarep, text [N,T,300] aligned text embeddings (0 rows at
+          pads), label [N, n_labels], text_id [N, L_text] unaligned ids.
+    Raw frames are 0 at padded time steps (what normalize_data turns into the
+    -10 pads, utils.py:171-189); covarep feature 1 is constant 0 in every split
+    (dropped by normalize_data, utils.py:163-169).
+    """
+    rng = np.random.default_rng(seed)
+    E = word_table(V, 300, seed=seed + 1)
+    word2ix = {f"w{i}": i for i in range(V)}
+    splits = []
+    for N in sizes:
+        lens = rng.integers(max(1, T // 3), T + 1, size=N)
+        pad = np.arange(T)[None, :] < (T - lens)[:, None]          # left padding
+        ids = rng.integers(1, V, size=(N, T)).astype(np.int64)
+        ids[pad] = 0
+        cov = rng.normal(0.0, 1.0, size=(N, T, A_raw)).astype(np.float32)
+        fac = rng.normal(0.5, 1.0, size=(N, T, Vd_raw)).astype(np.float32)
+        cov[pad] = 0.0
+        fac[pad] = 0.0
+        cov[:, :, 1] = 0.0
+        if n_labels == 1 and dataset == "mosi":
+            label = rng.uniform(-3.0, 3.0, size=N).astype(np.float32)
+        else:
+            label = rng.uniform(1.0, 7.0, size=(N, n_labels)).astype(np.float32)
+        d = {"facet": fac, "covarep": cov, "label": label}
+        if dataset == "mosi":
+            d.update(text=ids, lengths=lens.astype(np.int64), id=np.arange(N).astype(np.int64))
+        else:
+            d["text"] = np.where(pad[:, :, None], 0.0, E[ids]).astype(np.float32)
+            Lt = T + 3
+            tid = rng.integers(1, V, size=(N, Lt)).astype(np.int64)
+            tl = rng.integers(2, Lt + 1, size=N)
+            tid[np.arange(Lt)[None, :] >= tl[:, None]] = 0
+            d["text_id"] = tid
+        splits.append(d)
+    return word2ix, E, tuple(splits)

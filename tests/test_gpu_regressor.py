@@ -54,9 +54,14 @@ def test_forward(gpu, golden):
         m.hidden1.bias.copy_(torch.tensor(z["b1"]))
         m.out.weight.copy_(torch.tensor(z["w2"]))
         m.out.bias.copy_(torch.tensor(z["b2"]))
-    y = m(torch.tensor(z["x"], device=gpu))
-    assert y.shape == (32,)
+    x = torch.tensor(z["x"], device=gpu)
+    with torch.no_grad():
+        y = m(x)  # mmb_mlp_forward
+    assert y.shape == (32,) and not y.requires_grad
     np.testing.assert_allclose(y.cpu().numpy(), z["pred"], rtol=1e-5, atol=1e-6)
+    y = m(x)  # autograd recording (the e2e objective): differentiable device path
+    assert y.shape == (32,) and y.requires_grad
+    np.testing.assert_allclose(y.detach().cpu().numpy(), z["pred"], rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("h,o,n", [(150, 1, 77), (100, 7, 64), (60, 3, 33)])
