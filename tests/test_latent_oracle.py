@@ -100,3 +100,23 @@ def test_cli_golden_files_listed():
         j = json.load(open(os.path.join(GOLDEN, f"g9_cli_{v}.json")))
         assert {"config.json", "pre/embed.bin", "post/embed.bin", "embed_loss.txt",
                 "post/senti.bin"} <= set(j["files"])
+
+
+def test_config_grid_seeded(tmp_path):
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("mk", os.path.join(root, "configs", "make_configs.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    a = mk.main(["--seed", "0", "--out", str(tmp_path / "g1")])
+    b = mk.main(["--seed", "0", "--out", str(tmp_path / "g2")])
+    assert len(a) == 512 and a == b  # 2^9 points (make_configs.py:16-31), seeded order
+    assert len({json.dumps(c, sort_keys=True) for c in a}) == 512
+    pinned = json.load(open(os.path.join(root, "configs", "multimodal_search", "config_0.json")))
+    assert pinned == a[0]
+    import simplesif
+
+    args = simplesif.parse_arguments([os.path.join(root, "configs", "multimodal_search",
+                                                    "config_0.json"), "mosi"])
+    assert args["config_num"] == 0 and args["e2e"] is True
