@@ -86,9 +86,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--utts-per-gpu", type=int, default=1_000_000)
-    ap.add_argument("--tokens", type=int, default=40)
-    ap.add_argument("--vocab", type=int, default=400_000)
+    ap.add_argument("--workload", default="synthetic", choices=["synthetic", "pom"],
+                    help="synthetic: BASELINE configs[3] (the metric's workload); pom: "
+                         "configs[2] shape (V=7763, transcripts padded to 1357, ~370 tokens)")
+    ap.add_argument("--utts-per-gpu", type=int, default=None)
+    ap.add_argument("--tokens", type=int, default=None)
+    ap.add_argument("--vocab", type=int, default=None)
     ap.add_argument("--chunks", type=int, default=None,
                     help="row chunks per step (stream of chunk c+1 overlaps projection of c); "
                          "default 1")
@@ -119,8 +122,14 @@ def main():
     import synth
 
     mmb_lib.require_gpu()
-    U, T, V, D = args.utts_per_gpu, args.tokens, args.vocab, 300
-    inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev)
+    pom = args.workload == "pom"
+    dflt = (10_000, 1357, 7763) if pom else (1_000_000, 40, 400_000)
+    U = args.utts_per_gpu or dflt[0]
+    T = args.tokens or dflt[1]
+    V = args.vocab or dflt[2]
+    D = 300
+    inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev,
+                                mean_len=370.0 if pom else None)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
 
@@ -181,14 +190,16 @@ def main():
                 traffic = tj.get("mm2_stream_hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "utt_stream_kernel (mmb_mm2_stream)",
+                "kernel": ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
+                           else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)"),
                 "algorithmic_bytes_per_utt": kb, "utts_per_launch": utts_per_launch,
                 "avg_launch_ms": round(stream_launch_ms, 4)}
         pb = path_bytes(T, D, 300, 300)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(inp, gen.cpu(), args.cpu_sample)
+                n_cpu = args.cpu_sample if not pom else max(1, args.cpu_sample * 40 // T)
+                cpu = cpu_baseline(inp, gen.cpu(), n_cpu)
             except Exception as exc:  # keep the GPU line even if the host leg fails
                 log(f"cpu baseline failed: {exc!r}")
         out = {
@@ -204,8 +215,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded, generated in HBM; no dataset or checkpoint)",
-            "config": {"workload": "configs[3]: synthetic utterances x 40 tokens/frames x 3 "
-                                   "modalities x 300d, SIF(+PC removal) + closed-form MMB2",
+            "config": {"workload": ("configs[2]: POM-shaped (V=7763, w0=1.0, transcripts padded "
+                                    "to 1357, ~370 tokens, aligned frames) x 3 modalities x 300d, "
+                                    "SIF(+PC removal) + closed-form MMB2" if pom else
+                                    "configs[3]: synthetic utterances x 40 tokens/frames x 3 "
+                                    "modalities x 300d, SIF(+PC removal) + closed-form MMB2"),
                        "utts_per_gpu": U, "tokens": T, "vocab": V, "dims": [D, 300, 300],
                        "parallelism": f"dp{world} (utterance shards) + RCCL all-reduce of the "
                                       f"300x300 fp64 Gram"},
