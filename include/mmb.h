@@ -68,6 +68,18 @@ size_t mmb_gram_workspace_bytes(int64_t n, int d);
 int mmb_gram(const float* num, const float* cnt, int64_t n, int d, double* g, int accumulate,
              void* ws, hipStream_t stream);
 
+/* The same Gram in two phases, for a split streamed in row chunks (the
+ * overlapped bench step): mmb_gram_part reduces one chunk of n <= n_plan rows
+ * into per-range partials in ws (accumulate = 0 for the first chunk, 1 to add
+ * the next ones; every chunk must use the same n_plan, and consecutive calls
+ * must be stream-ordered); mmb_gram_finish sums the partials in a fixed order
+ * into g (accumulate: add to g).  ws as for mmb_gram(n_plan, d); d % 4 == 0,
+ * d <= 320, num 16-byte aligned.                                             */
+int mmb_gram_part(const float* num, const float* cnt, int64_t n, int64_t n_plan, int d,
+                  int accumulate, void* ws, hipStream_t stream);
+int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate, const void* ws,
+                    hipStream_t stream);
+
 /* z0[d,k] = X^T omega  (omega [n,k] float64) — start block of the transposed
  * randomized-SVD branch (n < d).                                             */
 int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d, const double* omega,

@@ -48,10 +48,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Grid size for streaming kernels: enough workgroups to fill 256 CUs several
-// times over, capped so per-workgroup setup is amortised by a grid-stride loop.
-inline int stream_grid(int64_t units, int per_cu) {
-  int64_t cap = 256LL * per_cu;
+// CUs a launch on `stream` can use: the device's, or the subset a stream made
+// by hipExtStreamCreateWithCUMask is restricted to (sif_kernels.hip).
+int stream_cu_count(hipStream_t stream);
+
+// Grid size for streaming kernels: enough workgroups to fill the stream's CUs
+// several times over, capped so per-workgroup setup is amortised by a
+// grid-stride loop.  Sized from the stream's CUs: a grid made for 256 CUs on
+// a 160-CU stream queues a partial round of late workgroups (a tail).
+inline int stream_grid(int64_t units, int per_cu, hipStream_t stream) {
+  int64_t cap = static_cast<int64_t>(stream_cu_count(stream)) * per_cu;
   return static_cast<int>(units < cap ? (units > 0 ? units : 1) : cap);
 }
 

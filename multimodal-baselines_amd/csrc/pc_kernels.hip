@@ -121,7 +121,8 @@ __device__ __forceinline__ void tri_tile(int tau, int nt, int& ti, int& tj) {
 __global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict__ num,
                                                          const float* __restrict__ cnt, int64_t N,
                                                          int D, int nt, int R, int64_t chunk,
-                                                         int xcd_map, double* __restrict__ part) {
+                                                         int xcd_map, int acc_part,
+                                                         double* __restrict__ part) {
   extern __shared__ double s_x[];  // [2][kG2Rows][kG2Stride]
   const int T = nt * (nt + 1) / 2;
   int half, range;
@@ -221,8 +222,12 @@ __global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict
     if (q < ntl) {
       const int tau = t0 + wave + (kG2NT / kWave) * q;
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
-        pr[static_cast<int64_t>(tau) * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[q][reg];
+      for (int reg = 0; reg < 4; ++reg) {
+        // acc_part: add to this range's partial of the previous row chunk (each
+        // element has one owner wave: no race; chunks run in stream order)
+        double* dst = pr + static_cast<int64_t>(tau) * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15);
+        *dst = acc_part ? *dst + acc[q][reg] : acc[q][reg];
+      }
     }
   }
 }
@@ -1213,6 +1218,17 @@ static Gram2Plan gram2_plan(int64_t n, int d) {
   return p;
 }
 
+static size_t gram2_lds() {
+  const size_t lds = sizeof(double) * 2 * kG2Rows * kG2Stride;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_tri_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr = true;
+  }
+  return lds;
+}
+
 static bool gram2_ok(const float* num, int d) {
   // 16-wave tile kernel: d <= 320 (20 tile rows, <= 8 tiles per wave per half)
   return d % 4 == 0 && d <= 320 && (reinterpret_cast<uintptr_t>(num) & 15) == 0;
@@ -1237,14 +1253,8 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
   const int64_t total = static_cast<int64_t>(d) * d;
   if (gram2_ok(num, d)) {
     const Gram2Plan q = gram2_plan(n, d);
-    const size_t lds = sizeof(double) * 2 * kG2Rows * kG2Stride;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_tri_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-      attr = true;
-    }
-    gram_tri_kernel<<<2 * q.R, kG2NT, lds, stream>>>(num, cnt, n, d, q.nt, q.R, q.chunk, q.xcd, part);
+    const size_t lds = gram2_lds();
+    gram_tri_kernel<<<2 * q.R, kG2NT, lds, stream>>>(num, cnt, n, d, q.nt, q.R, q.chunk, q.xcd, 0, part);
     MMB_LAUNCH_CHECK();
     gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, q.nt, q.R, accumulate, g);
     MMB_LAUNCH_CHECK();
@@ -1255,6 +1265,28 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
                                                          p.chunk, p.xcd, part);
   MMB_LAUNCH_CHECK();
   gram_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, p.nb, p.npairs, p.S, accumulate, g);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_gram_part(const float* num, const float* cnt, int64_t n, int64_t n_plan, int d,
+                             int accumulate, void* ws, hipStream_t stream) {
+  MMB_REQUIRE(num && ws && n >= 0 && n <= n_plan && d > 0 && gram2_ok(num, d));
+  const Gram2Plan q = gram2_plan(n_plan, d);
+  gram_tri_kernel<<<2 * q.R, kG2NT, gram2_lds(), stream>>>(num, cnt, n, d, q.nt, q.R, q.chunk, q.xcd,
+                                                           accumulate ? 1 : 0,
+                                                           static_cast<double*>(ws));
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate, const void* ws,
+                               hipStream_t stream) {
+  MMB_REQUIRE(g && ws && n_plan >= 0 && d > 0 && d % 4 == 0 && d <= 320);
+  const Gram2Plan q = gram2_plan(n_plan, d);
+  const int64_t total = static_cast<int64_t>(d) * d;
+  gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(
+      static_cast<const double*>(ws), d, q.nt, q.R, accumulate, g);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

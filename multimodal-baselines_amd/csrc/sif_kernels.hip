@@ -542,8 +542,9 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
 }
 
 template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false>
-static int launch_wave(const StreamArgs& a, hipStream_t stream, int grid_cap = 256 * 8) {
+static int launch_wave(const StreamArgs& a, hipStream_t stream) {
   const int64_t blocks = ceil_div(a.N, 4);
+  const int grid_cap = 8 * stream_cu_count(stream);
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
   if (MM2 && a.ids == nullptr && a.emb_dense != a.text_dense) {
     utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, true><<<grid, 256, 0, stream>>>(a);
@@ -587,9 +588,27 @@ __global__ void calc_weights_kernel(const float* __restrict__ x, int64_t total, 
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+int stream_cu_count(hipStream_t stream) {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return 256;
+  }
+  if (stream == nullptr) return n;
+  uint32_t mask[32] = {};
+  if (hipExtStreamGetCUMask(stream, 32, mask) != hipSuccess) {
+    (void)hipGetLastError();  // a query failure is not a launch error
+    return n;
+  }
+  int c = 0;
+  for (int b = 0; b < n && b < 32 * 32; ++b) c += (mask[b >> 5] >> (b & 31)) & 1;
+  return (c > 0 && c < n) ? c : n;
+}
+
 template <bool MM2, int VT, int VA, int VV>
 static int launch_stream(const StreamArgs& a, hipStream_t stream) {
-  const int grid = stream_grid(a.N, 6);
+  const int grid = stream_grid(a.N, 6, stream);
   utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;

@@ -35,6 +35,8 @@ SIGNATURES = {
     "mmb_sif_wavg": (_I, [_P, _L, _I, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_gram_workspace_bytes": (_S, [_L, _I]),
     "mmb_gram": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
+    "mmb_gram_part": (_I, [_P, _P, _L, _L, _I, _I, _P, _P]),
+    "mmb_gram_finish": (_I, [_L, _I, _P, _I, _P, _P]),
     "mmb_xt_omega": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
     "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "mmb_pc_remove": (_I, [_P, _P, _L, _I, _P, _I, _P, _P, _P]),

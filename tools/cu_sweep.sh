@@ -7,5 +7,5 @@ run() {
   python3 -c "import json,sys;d=json.load(open('$OUT/b.json'));print(sys.argv[1:], round(d['value']/1e6,2), d['ms_per_step'], {k: round(v,2) for k,v in d['phase_ms'].items()})" "$@"
 }
 run --chunks 1
-for s in ${CU_SET:-48 64 80 96}; do run --chunks 8 --side-cus $s; done
-run --chunks 8 --side-cus 64 --side-layout high
+for s in ${CU_SET:-64 96 128}; do run --chunks 8 --side-cus $s --side-layout ${LAYOUT:-high}; done
+run --chunks 8 --side-cus 96 --side-layout strided
