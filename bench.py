@@ -97,7 +97,7 @@ def main():
                          "default 1")
     ap.add_argument("--side-cus", type=int, default=0,
                     help="with --chunks > 1: CUs reserved for the projection + Gram stream")
-    ap.add_argument("--side-layout", default="strided", choices=["strided", "high"])
+    ap.add_argument("--side-layout", default="balanced", choices=["balanced", "strided", "high"])
     ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))

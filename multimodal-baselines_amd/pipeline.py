@@ -322,6 +322,29 @@ class _EventSpan:
         return False
 
 
+def side_cu_set(n_cu: int, side: int, layout: str = "balanced") -> list[int]:
+    """CU-mask bits for the side stream of the overlapped step.
+
+    strided: evenly spaced bits; high: the top `side` bits; balanced: the same
+    count in every block of 32 bits AND in every residue class mod 8, with the
+    residues rotated from block to block -- even over the XCDs whether the
+    driver deals mask bits to XCDs round-robin or in blocks of 32."""
+    if layout == "strided":
+        step = n_cu / side
+        return sorted({int(i * step) for i in range(side)})
+    if layout == "high":
+        return list(range(n_cu - side, n_cu))
+    if layout != "balanced":
+        raise ValueError(f"unknown side CU layout {layout!r}")
+    blocks = max(1, n_cu // 32)
+    per = max(1, side // blocks)
+    out = []
+    for b in range(blocks):
+        for j in range(per):
+            out.append(32 * b + 8 * (j // 8) + (j + b * per) % 8)
+    return sorted(set(c for c in out if c < n_cu))
+
+
 class FusedStep:
     """One pass of the north-star hot path over a batch of utterances resident
     in HBM (bench 'step'): both the SIF text embedding (a1-a5, PC-removed) and
@@ -334,19 +357,23 @@ class FusedStep:
       mm2_prepare  generator weights -> Wm, c0, fp16 hi/lo split
       mm2_project  s, num, aux, Wm -> mmb2 (fp16-split MFMA + fused normalisation)
 
-    With `chunks` > 1 the utterances are cut into row chunks: the HBM-bound
-    stream kernel runs chunk c+1 on the caller's stream while the MFMA-bound
-    projection and the Gram accumulation of chunk c run on a second HIP stream
-    (they read only chunk c's num/s/aux).  The PC solve needs the Gram of every
-    row, so it and the removal run after the last chunk.  Measured on MI355X
-    (1M utterances) the overlap does not pay: the stream kernel occupies every
-    CU and the projection only runs in its gaps (chunks 1/4/8/16: 31.3 / 30.8
-    / 32.3 / 32.0 ms), so the default is one chunk.
+    With `chunks` > 1 the utterances are cut into row chunks (multiples of 256
+    rows) and pipelined: chunk 0's stream kernel runs on every CU; then chunk
+    c's stream kernel runs on the main stream while chunk c-1's projection and
+    Gram partials (mmb_gram_part) run on a side stream; the last chunk's
+    projection runs on every CU again, one mmb_gram_finish sums the partials,
+    and the PC solve and removal follow.  `side_cus` > 0 puts the two streams
+    on disjoint CU sets (CU-masked HIP streams; grid-stride kernels size their
+    grids from the mask).  Measured on MI355X (1M utterances)
+    the overlap does not pay: beside the MFMA-bound kernels the HBM-bound
+    stream kernel slows by about what the projection hides (8 chunks, shared
+    CUs / 64 balanced side CUs / 96 'high' side CUs: 28.5 / 30.7 / 28.8 ms per
+    step against 28.6 ms unpipelined), so the default is one chunk.
     """
 
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
-                 side_cus: int = 0, side_layout: str = "strided"):
+                 side_cus: int = 0, side_layout: str = "balanced"):
         self.inp = inputs
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
@@ -374,22 +401,22 @@ class FusedStep:
             chunks = 1
         chunks = max(1, min(chunks, self.n))
         step = -(-self.n // chunks)
+        step = -(-step // 256) * 256  # 16-byte aligned chunk starts (two-phase Gram)
         self.bounds = [(r, min(r + step, self.n)) for r in range(0, self.n, step)] or [(0, 0)]
+        self.step_rows = step
         # aux is planar per chunk: chunk [r0, r1) owns flat[3 r0 : 3 r1] as [3][r1 - r0]
         self.aux_flat = torch.empty((3 * self.n,), dtype=torch.float32, device=dev)
+        self.gram_parts = len(self.bounds) > 1 and self.d % 4 == 0 and self.d <= 320
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
         self.main = None
         self._cu_streams = []
+        self._events = [torch.cuda.Event() for _ in self.bounds]
         if side_cus and self.side is not None:
             # disjoint CU sets: the stream kernel on `main`, the projection +
             # Gram of the previous chunk on `side`
             n_cu = L.cu_count(dev)
-            if side_layout == "strided":
-                step_cu = n_cu / side_cus
-                side_set = sorted({int(i * step_cu) for i in range(side_cus)})
-            else:
-                side_set = list(range(n_cu - side_cus, n_cu))
+            side_set = side_cu_set(n_cu, side_cus, side_layout)
             main_set = [c for c in range(n_cu) if c not in set(side_set)]
             self._cu_streams = [L.CUStream(main_set, dev), L.CUStream(side_set, dev)]
             self.main, self.side = self._cu_streams[0].torch, self._cu_streams[1].torch
@@ -417,7 +444,11 @@ class FusedStep:
         r0, r1 = self.bounds[c]
         aux = self.aux_of(c)
         mm2_project(self.s[r0:r1], self.num[r0:r1], aux, self.proj, out=self.mmb2[r0:r1])
-        gram(self.num[r0:r1], aux[0], self.G, accumulate=c > 0, ws=self.gws)
+        if self.gram_parts:
+            L.call("mmb_gram_part", L.ptr(self.num[r0:r1]), L.ptr(aux[0]), r1 - r0,
+                   self.step_rows, self.d, int(c > 0), L.ptr(self.gws.buf), L.stream_ptr())
+        else:
+            gram(self.num[r0:r1], aux[0], self.G, accumulate=c > 0, ws=self.gws)
 
     def run(self, trace: dict | None = None):
         """One step.  With `trace` (a dict), HIP events are recorded on the
@@ -428,32 +459,39 @@ class FusedStep:
             return _EventSpan(trace.setdefault(name, []))
 
         d, k = self.d, self.npc + N_OVERSAMPLES
-        if self.side is None:
-            with mark("mm2_prepare"):
-                self.proj.refresh()
-            with mark("mm2_stream"):
-                self._stream_chunk(0)
-            with mark("mm2_project+gram"):
-                self._consume_chunk(0)
-        else:
+        nb = len(self.bounds)
+        with mark("mm2_prepare"):
+            self.proj.refresh()
+        with mark("mm2_stream"):
+            self._stream_chunk(0)  # every CU
+        if nb > 1:
             caller = torch.cuda.current_stream(self.table.device)
             main = self.main if self.main is not None else caller
+            side = self.side
+            ev = self._events
+            ev[0].record(caller)
             if main is not caller:
                 main.wait_stream(caller)
-            self.side.wait_stream(caller)
-            with torch.cuda.stream(self.side), mark("mm2_prepare"):
-                self.proj.refresh()
-            with torch.cuda.stream(main):
-                for c in range(len(self.bounds)):
+            side.wait_stream(caller)
+            for c in range(1, nb):
+                with torch.cuda.stream(main):
                     with mark("mm2_stream"):
                         self._stream_chunk(c)
-                    self.side.wait_stream(main)
-                    with torch.cuda.stream(self.side), mark("mm2_project+gram"):
-                        self._consume_chunk(c)
-            with mark("join"):
-                caller.wait_stream(self.side)
-                if main is not caller:
-                    caller.wait_stream(main)
+                    if c < nb - 1:
+                        ev[c].record(main)
+                with torch.cuda.stream(side):
+                    side.wait_event(ev[c - 1])
+                    with mark("mm2_project+gram"):
+                        self._consume_chunk(c - 1)
+            if main is not caller:
+                caller.wait_stream(main)
+            caller.wait_stream(side)
+        with mark("mm2_project+gram"):
+            self._consume_chunk(nb - 1)  # every CU
+        if self.gram_parts:
+            with mark("gram_finish"):
+                L.call("mmb_gram_finish", self.step_rows, d, L.ptr(self.G), 0, L.ptr(self.gws.buf),
+                       L.stream_ptr())
         with mark("pc_start"):
             if self.n_total >= d:
                 z0, transposed = omega(d, k, self.table.device), False

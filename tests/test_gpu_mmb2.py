@@ -208,3 +208,23 @@ def test_chunked_overlapped_step_matches_single_chunk(gpu):
     assert len(trace["mm2_stream"]) == 3 and len(trace["mm2_project+gram"]) == 3
     with pytest.raises(ValueError):
         three.aux
+
+
+@pytest.mark.parametrize("side_cus", [0, 96])
+def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
+    """The chunk pipeline (two-phase Gram, last chunk on every CU), with and
+    without CU-masked side/main streams: MMB2 rows bit-identical to one
+    chunk, SIF rows to fp64 summation order."""
+    N, T, V = 6000, 40, 20_000
+    inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=12, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    one = P.FusedStep(inp, gen.networks(), chunks=1)
+    s1, m1 = [t.clone() for t in one.run()]
+    four = P.FusedStep(inp, gen.networks(), chunks=4, side_cus=side_cus)
+    assert len(four.bounds) == 4 and four.gram_parts
+    for _ in range(2):  # a second step re-uses the buffers and the Gram partials
+        s4, m4 = four.run()
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m4)
+    assert M.row_rel_err(s4.cpu().numpy(), s1.cpu().numpy()) < 1e-6

@@ -8,7 +8,7 @@ TAG=${1:-session}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python3 -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 300 --timeout-method thread \
     > "$OUT/pytest.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest.log"; [ "$rc" -eq 0 ] || exit "$rc"
 fi
