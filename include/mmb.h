@@ -131,7 +131,8 @@ int mmb_calc_weights(const float* x, int64_t rows, int f, const float* b_mean,
  * or from dense [n,t,d] tensors (ids null: text_dense for the modality sums,
  * emb_dense for the weighted sum, w_dense [n,t] the sentence weights).
  * Writes, per utterance i:
- *   num[i,:d]  = sum_t w_t E_t                      (weighted text sum)
+ *   num[i,:d]  = (sum_t w_t E_t) / count_nonzero(w)  (the a2 row x_i, f32
+ *                division as sif_functions.py:55; NaN when every weight is 0)
  *   s[i,:]     = [Sx_e | Sxx_e | Sx_a | Sxx_a | Sx_v | Sxx_v | 0-pad]  (sum
  *                over t of x and x^2 per feature; row stride mmb_mm2_k());
  *                s_half = 0: fp32 [n][k]; s_half = 1: fp16 [n][2][k], the hi
@@ -169,8 +170,10 @@ int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_mu,
  * them), then the per-column 1/scale [ldw] f32.                             */
 size_t mmb_mm2_split_bytes(int d, int a, int vd);
 
-/* cs = (num + s @ wm[:, :d] + c0) / (aux[1] + s @ wm[:, d] + c0[d]);
- * out = cs / ||cs||_2 (fp32 MFMA GEMM + fused epilogue).
+/* cs = (t + s @ wm[:, :d] + c0) / (aux[1] + s @ wm[:, d] + c0[d]) with the
+ * weighted text sum t = num * aux[0] (0 where aux[0] == 0), num as
+ * mmb_mm2_stream writes it; out = cs / ||cs||_2 (fp32 MFMA GEMM + fused
+ * epilogue).
  * replaces: sif2.py:186-207                                                  */
 int mmb_mm2_project(const float* s, const float* num, const float* aux, const float* wm,
                     int ldw, const float* c0, int64_t n, int k, int d, float* out,

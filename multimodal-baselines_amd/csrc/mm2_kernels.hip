@@ -169,6 +169,14 @@ __global__ void mm2_c0_reduce_kernel(const double* __restrict__ part, int D, int
 // C/D: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
+// The weighted text sum sum_t w_t E_t of a row from the a2 row x = sum / count
+// that mmb_mm2_stream writes (count = count_nonzero(w), aux[0]): x * count,
+// within one rounding of the sum; 0 for a row whose weights are all zero
+// (x is then 0/0 = NaN, like the reference's a2, but the MMB2 text term is 0).
+__device__ __forceinline__ float text_sum(float x, float count) {
+  return count != 0.f ? x * count : 0.f;
+}
+
 constexpr int kPM = 64;   // rows per workgroup
 constexpr int kPK = 32;   // K chunk staged in LDS
 
@@ -237,7 +245,7 @@ __global__ __launch_bounds__(256) void mm2_project_kernel(const float* __restric
       const int64_t row = n0 + rl;
       float add = 0.f;
       if (row < N) {
-        if (col < D) add = num[row * D + col] + c0[col];
+        if (col < D) add = text_sum(num[row * D + col], aux[row]) + c0[col];
         else if (col == D) add = aux[N + row] + c0[D];
       }
       acc[t][r] += add;
@@ -485,12 +493,13 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
     // all 16 x (CT + 1) loads of this lane first, then the arithmetic: one
     // memory latency for the whole epilogue instead of one per row group
     // (the fragment registers are dead here, so the loads fit)
-    float nv[16][CT], tv[16];
+    float nv[16][CT], tv[16], cv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
       const int64_t rowc = min(n0 + rl, N - 1);
       tv[r] = aux[N + rowc];
+      cv[r] = aux[rowc];
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
         const int col = (wc * CT + t) * 32 + cl;
@@ -511,7 +520,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
         const int col = (wc * CT + t) * 32 + cl;
-        const float add = col < D ? nv[r][t] : (col == D ? tv[r] : 0.f);
+        const float add = col < D ? text_sum(nv[r][t], cv[r]) : (col == D ? tv[r] : 0.f);
         const float y = acc[t][r] * (cinv[t] * inv_rs) + add + cadd[t];
         acc[t][r] = y;
         if (col == D) s_tot[rl] = y;

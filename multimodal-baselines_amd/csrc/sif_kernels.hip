@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
           x1 += s_red[kRedFloats + r * a.D + f];
           x2 += s_red[2 * kRedFloats + r * a.D + f];
         }
-        a.num_out[i * a.D + f] = n_;
+        a.num_out[i * a.D + f] = n_ / cnt;  // x = the a2 row (sif_functions.py:55)
         a.s_out[i * a.Kp + f] = x1;
         a.s_out[i * a.Kp + a.D + f] = x2;
         smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       for (int c = 0; c < CT; ++c) {
         const int u = lane + kWave * c;
         if (u < UT) {
-          st4(a.num_out + i * a.D + 4 * u, num[c]);
+          st4(a.num_out + i * a.D + 4 * u, div4(num[c], cnt));  // x = the a2 row
           put(4 * u, sx[c]);
           put(a.D + 4 * u, sxx[c]);
         }

@@ -8,7 +8,7 @@ reference-signature mirrors (`sif_functions.py`, `sif.py`, `sif2.py`) and
 Data layout in HBM (one utterance per row, row-major, fp32 unless noted):
   table [V, D], wtab [V] (f32 rounding of the f64 SIF weights), ids [N, L] int32,
   audio [N, T, A], visual [N, T, Vd]                                  (inputs)
-  num [N, D]   weighted text sum           s [N, Kp] frame sums       aux [2, N]
+  x [N, D]     a2 rows (weighted text sum / count)   s [N, Kp] frame sums   aux [3, N]
   G [D, D] f64 Gram   pc [npc, D] f64                                  (intermediates)
   sif [N, D] (f32 or f64)   mmb2 [N, D]                               (outputs)
 """
@@ -249,9 +249,11 @@ def ctypes_ptr_array(ptrs):
 def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=None,
                text_dense=None, emb_dense=None, w_dense=None, flag=None, out=None,
                s_half: bool = True):
-    """a6-a8 frame sums.  s_half=True (default) writes s as fp16 [n, 2*kp]
-    (hi | lo planes of the row-scaled sums, the x3 projection's A operand);
-    s_half=False writes fp32 [n, kp] for the fp32-MFMA projection."""
+    """a6-a8 frame sums.  Returns (x, s, aux): x [n, d] the a2 rows (weighted
+    text sum / count_nonzero(w)), aux [3, n] (count, total weight, row scale).
+    s_half=True (default) writes s as fp16 [n, 2*kp] (hi | lo planes of the
+    row-scaled sums, the x3 projection's A operand); s_half=False writes fp32
+    [n, kp] for the fp32-MFMA projection."""
     kp, _ = mm2_dims(d, a, vd)
     dev = audio.device
     if out is None:
@@ -350,12 +352,17 @@ class FusedStep:
     in HBM (bench 'step'): both the SIF text embedding (a1-a5, PC-removed) and
     the closed-form MMB2 embedding (a6-a8) of every utterance.
 
-      mm2_stream   ids/table/wtab + audio + visual -> num, s, aux  (HBM-bound)
-      gram         num/cnt -> G (fp64 MFMA)            [+ RCCL all-reduce of G]
+      mm2_stream   ids/table/wtab + audio + visual -> x, s, aux  (HBM-bound)
+      gram         x -> G (fp64 MFMA)                  [+ RCCL all-reduce of G]
       pc_solve     G -> pc (1 workgroup)
-      pc_remove    num/cnt, pc -> sif                    (HBM-bound)
+      pc_remove    x, pc -> sif                          (HBM-bound)
       mm2_prepare  generator weights -> Wm, c0, fp16 hi/lo split
-      mm2_project  s, num, aux, Wm -> mmb2 (fp16-split MFMA + fused normalisation)
+      mm2_project  s, x, aux, Wm -> mmb2 (fp16-split MFMA + fused normalisation;
+                   the weighted text sum is x * count)
+
+    x is the a2 row (weighted text sum / count, the exact f32 division of
+    sif_functions.py:55) written once by the stream kernel, so the Gram and
+    the removal read it without dividing.
 
     With `chunks` > 1 the utterances are cut into row chunks (multiples of 256
     rows) and pipelined: chunk 0's stream kernel runs on every CU; then chunk
@@ -384,7 +391,7 @@ class FusedStep:
         dev = self.table.device
         self.proj = MMB2Projection(networks, self.d, self.a, self.vd, self.t, dev)
         kp = self.proj.kp
-        self.num = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
+        self.x = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.s_half = x3_supported(self.proj)
         self.s = s_buffer(self.n, kp, self.s_half, dev)
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
@@ -438,17 +445,17 @@ class FusedStep:
         mm2_stream(r1 - r0, self.t, self.d, self.a, self.vd, inp["audio"][r0:r1],
                    inp["visual"][r0:r1], ids32=self.ids[r0:r1], table=self.table,
                    wtab32=inp["wtab"], flag=self.flag, s_half=self.s_half,
-                   out=(self.num[r0:r1], self.s[r0:r1], self.aux_of(c)))
+                   out=(self.x[r0:r1], self.s[r0:r1], self.aux_of(c)))
 
     def _consume_chunk(self, c: int):
         r0, r1 = self.bounds[c]
         aux = self.aux_of(c)
-        mm2_project(self.s[r0:r1], self.num[r0:r1], aux, self.proj, out=self.mmb2[r0:r1])
+        mm2_project(self.s[r0:r1], self.x[r0:r1], aux, self.proj, out=self.mmb2[r0:r1])
         if self.gram_parts:
-            L.call("mmb_gram_part", L.ptr(self.num[r0:r1]), L.ptr(aux[0]), r1 - r0,
+            L.call("mmb_gram_part", L.ptr(self.x[r0:r1]), None, r1 - r0,
                    self.step_rows, self.d, int(c > 0), L.ptr(self.gws.buf), L.stream_ptr())
         else:
-            gram(self.num[r0:r1], aux[0], self.G, accumulate=c > 0, ws=self.gws)
+            gram(self.x[r0:r1], None, self.G, accumulate=c > 0, ws=self.gws)
 
     def run(self, trace: dict | None = None):
         """One step.  With `trace` (a dict), HIP events are recorded on the
@@ -497,7 +504,7 @@ class FusedStep:
                 z0, transposed = omega(d, k, self.table.device), False
             else:
                 om = omega(self.n_total, k, self.table.device)[self.row0:self.row0 + self.n]
-                z0, transposed = xt_omega(self.num, self.aux_of(0)[0], om.contiguous()), True
+                z0, transposed = xt_omega(self.x, None, om.contiguous()), True
         if self.allreduce is not None:
             with mark("allreduce"):
                 self.allreduce(self.G)
@@ -507,6 +514,6 @@ class FusedStep:
             pc = pc_solve(self.G, z0, self.npc, transposed)
         with mark("pc_remove"):
             for c, (r0, r1) in enumerate(self.bounds):
-                remove_pc(self.num[r0:r1], self.aux_of(c)[0], pc, out=self.sif[r0:r1])
+                remove_pc(self.x[r0:r1], None, pc, out=self.sif[r0:r1])
         self.pc = pc
         return self.sif, self.mmb2

@@ -228,3 +228,36 @@ def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
     torch.cuda.synchronize()
     assert torch.equal(m1, m4)
     assert M.row_rel_err(s4.cpu().numpy(), s1.cpu().numpy()) < 1e-6
+
+
+def test_zero_weight_rows_sif_nan_mmb2_finite(gpu):
+    """A row whose SIF weights are all zero: its a2 row is 0/0 = NaN (numpy,
+    sif_functions.py:55; the reference's TruncatedSVD then rejects the split,
+    here the NaN reaches the Gram and every SIF row), while its MMB2
+    embedding is finite -- the text term is 0 (sif2.py:196-201) -- and every
+    MMB2 row matches the oracle."""
+    from oracle import sif_oracle as O
+
+    N, T, A, Vd, V = 600, 40, 300, 300, 5000
+    torch.manual_seed(2)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None)
+    E = synth.word_table(V, 300, seed=3)
+    wt = synth.sif_weights(V, w0=0.0)
+    ids = synth.token_ids(N, T, V, seed=4, ragged=True)
+    ids[7] = 0  # all padding, weight 0
+    audio = synth.frames(N, T, A, seed=5)
+    visual = synth.frames(N, T, Vd, seed=6)
+    inputs = {"table": torch.tensor(E, device=gpu),
+              "wtab": torch.tensor(wt, device=gpu, dtype=torch.float32),
+              "ids": torch.as_tensor(ids, dtype=torch.int32, device=gpu),
+              "audio": torch.tensor(audio, device=gpu), "visual": torch.tensor(visual, device=gpu)}
+    step = P.FusedStep(inputs, gen.to(gpu).networks())
+    sif_out, mm2_out = [t.cpu().numpy() for t in step.run()]
+    x = step.x.cpu().numpy()
+    assert np.isnan(x[7]).all() and np.isfinite(np.delete(x, 7, 0)).all()
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    text = E[ids]
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                            M.params_from_module(gen.cpu()), sw, text)
+    assert np.isfinite(mm2_out).all()
+    assert M.row_rel_err(mm2_out, ref) < TOL

@@ -63,23 +63,23 @@ def main():
         res["stream"] = timed(lambda: P.mm2_stream(step.n, step.t, 300, 300, 300, inp["audio"],
                                                    inp["visual"], ids32=inp["ids"],
                                                    table=inp["table"], wtab32=inp["wtab"],
-                                                   out=(step.num, step.s, step.aux)), args.reps)
+                                                   out=(step.x, step.s, step.aux)), args.reps)
     if "gram" in which:
-        res["gram"] = timed(lambda: P.gram(step.num, cnt, step.G, ws=step.gws), args.reps)
+        res["gram"] = timed(lambda: P.gram(step.x, None, step.G, ws=step.gws), args.reps)
     if "pcsolve" in which:
         res["pcsolve"] = timed(lambda: P.pc_solve(step.G, z0, 1, False), args.reps)
     if "remove" in which:
         pc = P.pc_solve(step.G, z0, 1, False)
-        res["remove"] = timed(lambda: P.remove_pc(step.num, cnt, pc, out=step.sif), args.reps)
+        res["remove"] = timed(lambda: P.remove_pc(step.x, None, pc, out=step.sif), args.reps)
     if "project" in which:
-        res["project"] = timed(lambda: P.mm2_project(step.s, step.num, step.aux, step.proj,
+        res["project"] = timed(lambda: P.mm2_project(step.s, step.x, step.aux, step.proj,
                                                      out=step.mmb2), args.reps)
     if "project32" in which:
         s32 = P.s_buffer(step.n, step.proj.kp, False, dev)
         P.mm2_stream(step.n, step.t, 300, 300, 300, inp["audio"], inp["visual"], ids32=inp["ids"],
                      table=inp["table"], wtab32=inp["wtab"], s_half=False,
-                     out=(step.num, s32, step.aux))
-        res["project32"] = timed(lambda: P.mm2_project(s32, step.num, step.aux, step.proj,
+                     out=(step.x, s32, step.aux))
+        res["project32"] = timed(lambda: P.mm2_project(s32, step.x, step.aux, step.proj,
                                                        out=step.mmb2), args.reps)
     for k, v in res.items():
         print(f"{k}: {v:.4f} ms")
