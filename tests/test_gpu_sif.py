@@ -168,3 +168,30 @@ def test_device_sif_properties_large(gpu):
     # idempotence: removing the same pc again changes nothing beyond rounding
     again = out1 - (out1 @ pc.T) * pc
     assert (again - out1).abs().max().item() < 1e-12
+
+
+def test_two_phase_gram_equals_one_shot_and_fp64(gpu):
+    """mmb_gram_part over row chunks + one mmb_gram_finish equals the one-shot
+    mmb_gram and the exact f64 X^T X (products of f32 values are exact in
+    f64; only the summation order differs)."""
+    import mmb_lib as L
+
+    n_plan, d = 4096, 300
+    rng = np.random.default_rng(5)
+    X = (rng.standard_normal((3 * n_plan - 100, d)) * 0.4 + 0.3).astype(np.float32)
+    x = torch.tensor(X, device=gpu)
+    ws = P.GramWorkspace(n_plan, d, gpu)
+    G2 = torch.empty((d, d), dtype=torch.float64, device=gpu)
+    for c, r0 in enumerate(range(0, x.shape[0], n_plan)):
+        part = x[r0:r0 + n_plan]
+        L.call("mmb_gram_part", L.ptr(part), None, part.shape[0], n_plan, d, int(c > 0),
+               L.ptr(ws.buf), L.stream_ptr())
+    L.call("mmb_gram_finish", n_plan, d, L.ptr(G2), 0, L.ptr(ws.buf), L.stream_ptr())
+    G1 = P.gram(x, None)
+    ref = X.astype(np.float64).T @ X.astype(np.float64)
+    scale = np.abs(ref).max()
+    assert np.abs(G2.cpu().numpy() - ref).max() / scale < 1e-13
+    assert np.abs(G1.cpu().numpy() - ref).max() / scale < 1e-13
+    with pytest.raises(L.MMBError):  # a chunk larger than the plan is rejected
+        L.call("mmb_gram_part", L.ptr(x), None, x.shape[0], n_plan, d, 0, L.ptr(ws.buf),
+               L.stream_ptr())

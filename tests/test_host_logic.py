@@ -59,3 +59,21 @@ def test_sentiment_model_init_matches_reference_order():
     h = torch.nn.Linear(300, 100)
     o = torch.nn.Linear(100, 1)
     assert torch.equal(m.hidden1.weight, h.weight) and torch.equal(m.out.bias, o.bias)
+
+
+def test_side_cu_sets_are_balanced_and_disjoint():
+    """The overlapped step's side CU set (pipeline.side_cu_set): the requested
+    count, evenly spread over the 8 residues mod 8 and the 8 blocks of 32 mask
+    bits (either way the driver may deal bits to XCDs) for the balanced
+    layout."""
+    import collections
+
+    import pipeline as P
+
+    for side in (64, 80, 96, 112, 128):
+        s = P.side_cu_set(256, side, "balanced")
+        assert len(s) == side and len(set(s)) == side and max(s) < 256
+        assert set(collections.Counter(c % 8 for c in s).values()) == {side // 8}
+        assert set(collections.Counter(c // 32 for c in s).values()) == {side // 8}
+        assert len(P.side_cu_set(256, side, "high")) == side
+        assert len(P.side_cu_set(256, side, "strided")) == side
