@@ -188,6 +188,16 @@ int mmb_mm2_project_x3(const void* s_split, const float* num, const float* aux, 
                        int ldw, const float* c0, int64_t n, int k, int d, float* out,
                        hipStream_t stream);
 
+/* mmb_mm2_project_x3 with the first-PC removal of the a2 rows fused into its
+ * epilogue (npc = 1): sif_out[i,:] = num[i,:] - (num[i,:] . pc) pc in f64,
+ * rounded to f32 -- what mmb_pc_remove(num, NULL, n, d, pc, 1, sif_out, NULL)
+ * writes, without re-reading num.  pc and sif_out both null = plain x3.
+ * replaces: sif2.py:186-207 and sif_functions.remove_pc
+ *   /root/reference/sif_functions.py:69-81 (npc = 1 branch :77-78)           */
+int mmb_mm2_project_x3_rmpc(const void* s_split, const float* num, const float* aux,
+                            const void* wsplit, int ldw, const float* c0, int64_t n, int k, int d,
+                            float* out, const double* pc, float* sif_out, hipStream_t stream);
+
 /* ---------------------------------------------------------------- a10/a11
  * SentimentModel(d -> h -> o): y = squeeze(W2 relu(W1 x + b1) + b2).
  * Forward for rows idx[0..b) (idx nullable = 0..b) of latents [*, d].

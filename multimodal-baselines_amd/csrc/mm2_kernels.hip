@@ -376,7 +376,8 @@ template <int CT>
 __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
     const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
     const _Float16* __restrict__ img, const float* __restrict__ col_inv,
-    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out) {
+    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
+    const double* __restrict__ pc, float* __restrict__ sif) {
   constexpr int LDW = 64 * CT;
   constexpr int BBUF = x3_bbuf_halves<CT>();
   constexpr int BQ = BBUF * 2 / 16 / kXT;  // 16-byte pieces per thread per B chunk (= CT)
@@ -561,12 +562,52 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
       }
     }
   }
+
+  if (pc) {
+    // fused first-PC removal of the a2 rows (sif_functions.py:77-78, npc = 1):
+    // sif = x - (x . pc) pc in f64, with the accumulators dead.  Wave w owns
+    // rows w, w + 8, ... of the tile (4 at a time, every load issued first);
+    // lane l columns l + 64 m.  The x rows come back from L2 / Infinity Cache
+    // (this workgroup read them for the text sum above).
+    constexpr int PER = (LDW + 63) / 64;
+    double pcv[PER];
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+      const int col = lane + 64 * m;
+      pcv[m] = col < D ? pc[col] : 0.0;
+    }
+    for (int g = wave; g < kXM; g += 4 * (kXT / 64)) {
+      float xv[4][PER];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t rowc = min(n0 + g + q * (kXT / 64), N - 1);
+#pragma unroll
+        for (int m = 0; m < PER; ++m) xv[q][m] = num[rowc * D + min(lane + 64 * m, D - 1)];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = n0 + g + q * (kXT / 64);
+        double dp = 0.0;
+#pragma unroll
+        for (int m = 0; m < PER; ++m) dp = fma(static_cast<double>(xv[q][m]), pcv[m], dp);
+        const double dot = wave_sum(dp);
+        if (row < N) {
+#pragma unroll
+          for (int m = 0; m < PER; ++m) {
+            const int col = lane + 64 * m;
+            if (col < D) sif[row * D + col] = static_cast<float>(static_cast<double>(xv[q][m]) - dot * pcv[m]);
+          }
+        }
+      }
+    }
+  }
 }
 
 template <int CT>
 static int launch_project_x3(const _Float16* s, const float* num, const float* aux,
                              const _Float16* img, const float* ci, const float* c0, int64_t n,
-                             int kp, int d, float* out, hipStream_t stream) {
+                             int kp, int d, float* out, const double* pc, float* sif,
+                             hipStream_t stream) {
   const int grid = static_cast<int>(ceil_div(n, kXM));
   constexpr size_t lds = x3_lds_bytes<CT>();
   static_assert(lds <= 160 * 1024, "x3 chunk rings exceed LDS");
@@ -576,7 +617,8 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
-  mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out);
+  mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out,
+                                                        pc, sif);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -642,11 +684,13 @@ extern "C" int mmb_mm2_prepare(const float* const* w_mu, const float* const* b_m
   return MMB_OK;
 }
 
-extern "C" int mmb_mm2_project_x3(const void* s_split, const float* num, const float* aux,
-                                  const void* wsplit, int ldw, const float* c0, int64_t n, int k,
-                                  int d, float* out, hipStream_t stream) {
+extern "C" int mmb_mm2_project_x3_rmpc(const void* s_split, const float* num, const float* aux,
+                                       const void* wsplit, int ldw, const float* c0, int64_t n,
+                                       int k, int d, float* out, const double* pc, float* sif_out,
+                                       hipStream_t stream) {
   MMB_REQUIRE(s_split && num && aux && wsplit && c0 && out && n >= 0 && d > 0);
   MMB_REQUIRE(ldw == mmb_mm2_ldw(d) && k % 32 == 0 && k >= 32);
+  MMB_REQUIRE((pc == nullptr) == (sif_out == nullptr));
   MMB_REQUIRE((reinterpret_cast<uintptr_t>(s_split) & 15) == 0 &&
               (reinterpret_cast<uintptr_t>(wsplit) & 15) == 0);
   if (n == 0) return MMB_OK;
@@ -654,13 +698,20 @@ extern "C" int mmb_mm2_project_x3(const void* s_split, const float* num, const f
   const _Float16* img = static_cast<const _Float16*>(wsplit);
   const float* ci = reinterpret_cast<const float*>(img + 2 * static_cast<size_t>(ldw) * k);
   switch (ldw / 64) {
-    case 1: return launch_project_x3<1>(s, num, aux, img, ci, c0, n, k, d, out, stream);
-    case 2: return launch_project_x3<2>(s, num, aux, img, ci, c0, n, k, d, out, stream);
-    case 3: return launch_project_x3<3>(s, num, aux, img, ci, c0, n, k, d, out, stream);
-    case 4: return launch_project_x3<4>(s, num, aux, img, ci, c0, n, k, d, out, stream);
-    case 5: return launch_project_x3<5>(s, num, aux, img, ci, c0, n, k, d, out, stream);
+    case 1: return launch_project_x3<1>(s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, stream);
+    case 2: return launch_project_x3<2>(s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, stream);
+    case 3: return launch_project_x3<3>(s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, stream);
+    case 4: return launch_project_x3<4>(s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, stream);
+    case 5: return launch_project_x3<5>(s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, stream);
     default: return MMB_EINVAL;  // d >= 320: the chunk rings exceed the 160 KB LDS
   }
+}
+
+extern "C" int mmb_mm2_project_x3(const void* s_split, const float* num, const float* aux,
+                                  const void* wsplit, int ldw, const float* c0, int64_t n, int k,
+                                  int d, float* out, hipStream_t stream) {
+  return mmb_mm2_project_x3_rmpc(s_split, num, aux, wsplit, ldw, c0, n, k, d, out, nullptr,
+                                 nullptr, stream);
 }
 
 extern "C" int mmb_mm2_project(const float* s, const float* num, const float* aux,

@@ -348,7 +348,18 @@ __device__ __forceinline__ float4 div4(float4 v, float c) {
   return make_float4(v.x / c, v.y / c, v.z / c, v.w / c);
 }
 using h4 = _Float16 __attribute__((ext_vector_type(4)));
+// Output rows (x, s planes) are written once and read back by a later kernel,
+// far beyond what L2 / Infinity Cache hold: NTS=true writes them non-temporal.
+template <bool NTS>
+__device__ __forceinline__ void stnt4(float* p, float4 v) {
+  if constexpr (NTS) {
+    __builtin_nontemporal_store(nf4{v.x, v.y, v.z, v.w}, reinterpret_cast<nf4*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
 // x * rs (rs a power of two: exact) as fp16 hi + fp16 lo = the residual
+template <bool NTS = false>
 __device__ __forceinline__ void split_store4(_Float16* hi, _Float16* lo, float4 v, float rs) {
   const float x[4] = {v.x * rs, v.y * rs, v.z * rs, v.w * rs};
   h4 h, l;
@@ -357,11 +368,17 @@ __device__ __forceinline__ void split_store4(_Float16* hi, _Float16* lo, float4 
     h[e] = static_cast<_Float16>(x[e]);
     l[e] = static_cast<_Float16>(x[e] - static_cast<float>(h[e]));
   }
-  *reinterpret_cast<h4*>(hi) = h;
-  *reinterpret_cast<h4*>(lo) = l;
+  if constexpr (NTS) {
+    __builtin_nontemporal_store(h, reinterpret_cast<h4*>(hi));
+    __builtin_nontemporal_store(l, reinterpret_cast<h4*>(lo));
+  } else {
+    *reinterpret_cast<h4*>(hi) = h;
+    *reinterpret_cast<h4*>(lo) = l;
+  }
 }
 
-template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false, bool SPLIT = false>
+template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false, bool SPLIT = false,
+          bool NTS = false>
 __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
@@ -484,16 +501,16 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       _Float16* hrow = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * a.Kp;
       auto put = [&](int f, float4 v) {
         if (a.s_half) {
-          split_store4(hrow + f, hrow + a.Kp + f, v, rs);
+          split_store4<NTS>(hrow + f, hrow + a.Kp + f, v, rs);
         } else {
-          st4(srow + f, v);
+          stnt4<NTS>(srow + f, v);
         }
       };
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
         const int u = lane + kWave * c;
         if (u < UT) {
-          st4(a.num_out + i * a.D + 4 * u, div4(num[c], cnt));  // x = the a2 row
+          stnt4<NTS>(a.num_out + i * a.D + 4 * u, div4(num[c], cnt));  // x = the a2 row
           put(4 * u, sx[c]);
           put(a.D + 4 * u, sxx[c]);
         }
@@ -541,15 +558,44 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
   }
 }
 
-template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false>
+// Load/store policy of the MMB2 wave kernel: bit 0 = frame loads
+// non-temporal, bit 1 = output stores non-temporal, bit 2 = 4 frames per load
+// group instead of 2.  Default 5 (4-frame groups, non-temporal frame loads):
+// measured on MI355X at 1M x 40 x 3 x 300-d, Zipf ids (tools/policy_sweep.sh):
+// policy 0/1/2/3/4/5/6/7 = 20.65/20.62/21.00/19.94/20.54/19.80/20.57/20.09 ms;
+// uniform ids 26.87 (0) -> 24.23 (5).  MMB_STREAM_POLICY overrides it (read
+// once) for such sweeps.
+static int stream_policy() {
+  static const int p = [] {
+    const char* e = getenv("MMB_STREAM_POLICY");
+    return e ? atoi(e) : 5;
+  }();
+  return p;
+}
+
+template <bool MM2, int CT, int CA, int CV, int UNR, bool NT, bool NTS>
+static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
+  if (MM2 && a.ids == nullptr && a.emb_dense != a.text_dense) {
+    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, true, NTS><<<grid, 256, 0, stream>>>(a);
+  } else {
+    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, false, NTS><<<grid, 256, 0, stream>>>(a);
+  }
+}
+
+template <bool MM2, int CT, int CA, int CV>
 static int launch_wave(const StreamArgs& a, hipStream_t stream) {
   const int64_t blocks = ceil_div(a.N, 4);
   const int grid_cap = 8 * stream_cu_count(stream);
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
-  if (MM2 && a.ids == nullptr && a.emb_dense != a.text_dense) {
-    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, true><<<grid, 256, 0, stream>>>(a);
-  } else {
-    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, false><<<grid, 256, 0, stream>>>(a);
+  switch (MM2 ? stream_policy() & 7 : 0) {
+    case 1: launch_wave_v<MM2, CT, CA, CV, 2, true, false>(a, grid, stream); break;
+    case 2: launch_wave_v<MM2, CT, CA, CV, 2, false, true>(a, grid, stream); break;
+    case 3: launch_wave_v<MM2, CT, CA, CV, 2, true, true>(a, grid, stream); break;
+    case 4: launch_wave_v<MM2, CT, CA, CV, 4, false, false>(a, grid, stream); break;
+    case 5: launch_wave_v<MM2, CT, CA, CV, 4, true, false>(a, grid, stream); break;
+    case 6: launch_wave_v<MM2, CT, CA, CV, 4, false, true>(a, grid, stream); break;
+    case 7: launch_wave_v<MM2, CT, CA, CV, 4, true, true>(a, grid, stream); break;
+    default: launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream); break;
   }
   MMB_LAUNCH_CHECK();
   return MMB_OK;

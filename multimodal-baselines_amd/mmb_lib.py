@@ -53,6 +53,7 @@ SIGNATURES = {
     "mmb_mm2_split_bytes": (_S, [_I, _I, _I]),
     "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
     "mmb_mm2_project_x3": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
+    "mmb_mm2_project_x3_rmpc": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P, _P, _P]),
     "mmb_mlp_forward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_eval": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_workspace_bytes": (_S, [_I, _I]),

@@ -281,12 +281,21 @@ def x3_supported(proj: "MMB2Projection") -> bool:
     return proj.ldw <= 320
 
 
-def mm2_project(s, num, aux, proj: MMB2Projection, out=None):
+def mm2_project(s, num, aux, proj: MMB2Projection, out=None, pc=None, sif_out=None):
     """fp16 s (s_half stream output): the fp16 hi/lo split MFMA GEMM
-    (mmb_mm2_project_x3); fp32 s: the fp32-MFMA GEMM.  Same epilogue."""
+    (mmb_mm2_project_x3); fp32 s: the fp32-MFMA GEMM.  Same epilogue.
+    With `pc` ([1, D] f64) and `sif_out` the x3 kernel also writes the
+    PC-removed a2 rows (mmb_mm2_project_x3_rmpc, fp16 s only)."""
     n = num.shape[0]
     if out is None:
         out = torch.empty((n, proj.d), dtype=torch.float32, device=num.device)
+    if pc is not None:
+        if s.dtype != torch.float16 or pc.shape[0] != 1 or sif_out is None:
+            raise L.MMBError("fused PC removal needs fp16 s, npc = 1 and sif_out")
+        L.call("mmb_mm2_project_x3_rmpc", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wsplit),
+               proj.ldw, L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.ptr(pc),
+               L.ptr(sif_out), L.stream_ptr())
+        return out
     if s.dtype == torch.float32:
         L.call("mmb_mm2_project", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wm), proj.ldw,
                L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.stream_ptr())
@@ -360,6 +369,12 @@ class FusedStep:
       mm2_project  s, x, aux, Wm -> mmb2 (fp16-split MFMA + fused normalisation;
                    the weighted text sum is x * count)
 
+    With one chunk, npc = 1 and the fp16 split (the bench shape) the order is
+    stream, Gram, PC solve, then ONE projection kernel that also writes the
+    PC-removed rows (mmb_mm2_project_x3_rmpc): the removal re-reads x from
+    cache instead of a separate HBM pass (`fuse_remove=False` keeps the
+    separate pc_remove kernel).
+
     x is the a2 row (weighted text sum / count, the exact f32 division of
     sif_functions.py:55) written once by the stream kernel, so the Gram and
     the removal read it without dividing.
@@ -380,7 +395,7 @@ class FusedStep:
 
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
-                 side_cus: int = 0, side_layout: str = "balanced"):
+                 side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True):
         self.inp = inputs
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
@@ -414,6 +429,7 @@ class FusedStep:
         # aux is planar per chunk: chunk [r0, r1) owns flat[3 r0 : 3 r1] as [3][r1 - r0]
         self.aux_flat = torch.empty((3 * self.n,), dtype=torch.float32, device=dev)
         self.gram_parts = len(self.bounds) > 1 and self.d % 4 == 0 and self.d <= 320
+        self.fused_remove = fuse_remove and len(self.bounds) == 1 and npc == 1 and self.s_half
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
         self.main = None
@@ -457,6 +473,23 @@ class FusedStep:
         else:
             gram(self.x[r0:r1], None, self.G, accumulate=c > 0, ws=self.gws)
 
+    def _solve(self, trace, mark):
+        """G (this rank's rows) -> pc: Omega, RCCL all-reduce of G, the solve."""
+        d, k = self.d, self.npc + N_OVERSAMPLES
+        with mark("pc_start"):
+            if self.n_total >= d:
+                z0, transposed = omega(d, k, self.table.device), False
+            else:
+                om = omega(self.n_total, k, self.table.device)[self.row0:self.row0 + self.n]
+                z0, transposed = xt_omega(self.x, None, om.contiguous()), True
+        if self.allreduce is not None:
+            with mark("allreduce"):
+                self.allreduce(self.G)
+                if transposed:
+                    self.allreduce(z0)
+        with mark("pc_solve"):
+            return pc_solve(self.G, z0, self.npc, transposed)
+
     def run(self, trace: dict | None = None):
         """One step.  With `trace` (a dict), HIP events are recorded on the
         stream each phase runs on: trace[phase] gets (start, end) pairs."""
@@ -471,6 +504,15 @@ class FusedStep:
             self.proj.refresh()
         with mark("mm2_stream"):
             self._stream_chunk(0)  # every CU
+        if self.fused_remove:
+            with mark("gram"):
+                gram(self.x, None, self.G, ws=self.gws)
+            pc = self._solve(trace, mark)
+            with mark("mm2_project+pc_remove"):
+                mm2_project(self.s, self.x, self.aux_of(0), self.proj, out=self.mmb2, pc=pc,
+                            sif_out=self.sif)
+            self.pc = pc
+            return self.sif, self.mmb2
         if nb > 1:
             caller = torch.cuda.current_stream(self.table.device)
             main = self.main if self.main is not None else caller
@@ -499,19 +541,7 @@ class FusedStep:
             with mark("gram_finish"):
                 L.call("mmb_gram_finish", self.step_rows, d, L.ptr(self.G), 0, L.ptr(self.gws.buf),
                        L.stream_ptr())
-        with mark("pc_start"):
-            if self.n_total >= d:
-                z0, transposed = omega(d, k, self.table.device), False
-            else:
-                om = omega(self.n_total, k, self.table.device)[self.row0:self.row0 + self.n]
-                z0, transposed = xt_omega(self.x, None, om.contiguous()), True
-        if self.allreduce is not None:
-            with mark("allreduce"):
-                self.allreduce(self.G)
-                if transposed:
-                    self.allreduce(z0)
-        with mark("pc_solve"):
-            pc = pc_solve(self.G, z0, self.npc, transposed)
+        pc = self._solve(trace, mark)
         with mark("pc_remove"):
             for c, (r0, r1) in enumerate(self.bounds):
                 remove_pc(self.x[r0:r1], None, pc, out=self.sif[r0:r1])

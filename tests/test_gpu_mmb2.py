@@ -13,6 +13,7 @@ import pipeline as P
 import sif2
 import synth
 from oracle import mmb2_oracle as M
+from oracle import sif_oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -185,6 +186,35 @@ def test_fused_step_large_properties(gpu):
     assert torch.isfinite(m1).all() and torch.isfinite(s1).all()
     norms = torch.linalg.norm(m1.double(), dim=1)
     assert (norms - 1).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("N", [1000, 129, 300])
+def test_fused_pc_removal_matches_separate_kernel(gpu, N):
+    """The bench order (Gram -> PC solve -> one projection kernel that also
+    writes the PC-removed a2 rows, mmb_mm2_project_x3_rmpc) equals the
+    separate mmb_pc_remove pass: MMB2 rows bit-identical, SIF rows to the
+    fp64 dot's summation order; ragged last tiles (N % 128 != 0) included.
+    Both against the CPU oracle of sif_functions.SIF_embedding too."""
+    T, V = 40, 5000
+    inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=21, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    fused = P.FusedStep(inp, gen.networks())
+    assert fused.fused_remove
+    trace = {}
+    s1, m1 = [t.clone() for t in fused.run(trace=trace)]
+    assert "mm2_project+pc_remove" in trace and "pc_remove" not in trace
+    sep = P.FusedStep(inp, gen.networks(), fuse_remove=False)
+    assert not sep.fused_remove
+    s2, m2 = sep.run()
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m2)
+    assert M.row_rel_err(s1.cpu().numpy(), s2.cpu().numpy()) < 1e-6
+    assert torch.equal(fused.pc, sep.pc)
+    E = inp["table"].cpu().numpy()
+    wt = inp["wtab"].cpu().numpy().astype(np.float64)
+    ref = O.get_sentence_embeddings(E, wt, inp["ids"].cpu().numpy().astype(np.int64))
+    assert M.row_rel_err(s1.cpu().numpy(), ref) < TOL
 
 
 def test_chunked_overlapped_step_matches_single_chunk(gpu):
