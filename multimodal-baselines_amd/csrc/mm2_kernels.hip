@@ -604,6 +604,248 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
 }
 
 template <int CT>
+__global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
+    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
+    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
+    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
+    const double* __restrict__ pc, float* __restrict__ sif) {
+  constexpr int LDW = 64 * CT;
+  constexpr int BBUF = x3_bbuf_halves<CT>();
+  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 16-byte pieces per thread per B chunk (= CT)
+  constexpr int AQ = kXAbufHalves * 2 / 16 / kXT;  // = 2
+  static_assert(BQ * kXT * 16 == BBUF * 2 && AQ * kXT * 16 == kXAbufHalves * 2, "staging split");
+  // one dynamic LDS array: B ring, A ring, per-row scalars
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  _Float16* bring = lds;
+  _Float16* aring = lds + kXBbuf * BBUF;
+  float* s_rs = reinterpret_cast<float*>(aring + kXAbuf * kXAbufHalves);
+  float* s_tot = s_rs + kXM;
+  float(*s_ss)[kXM] = reinterpret_cast<float(*)[kXM]>(s_tot + kXM);  // [4][kXM]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave (wr, wc): rows wr*64 + [0,64) as 4 16-row tiles, columns
+  // wc*16*CT + [0,16*CT) as CT 16-column tiles (v_mfma_f32_16x16x32_f16:
+  // lane l holds A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15],
+  // D[row 4(l>>4)+j][col l&15])
+  const int wr = wave >> 2, wc = wave & 3;
+  const int lq = lane >> 4, lc = lane & 15;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
+  const int nch = Kp / kXK;
+
+  // A piece g = q * kXT + tid of a chunk: plane g >> 9, row (g >> 2) & 127,
+  // LDS slot position g & 3 <- data slot (g & 3) ^ swz(row); rows past N
+  // re-read row N-1 (never stored)
+  const _Float16* asrc[AQ];
+#pragma unroll
+  for (int q = 0; q < AQ; ++q) {
+    const int g = q * kXT + tid;
+    const int plane = g >> 9, row = (g >> 2) & (kXM - 1);
+    const int64_t r = min(n0 + row, N - 1);
+    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
+  }
+  auto stage_a = [&](int c) {
+    const int cc = min(c, nch - 1);
+    _Float16* dst = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
+#pragma unroll
+    for (int q = 0; q < AQ; ++q)
+      glds16(asrc[q] + cc * kXK, dst + (q * kXT + wave * 64) * 8);
+  };
+  auto stage_b = [&](int c) {
+    const int cc = min(c, nch - 1);
+    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
+    _Float16* dst = bring + (c & (kXBbuf - 1)) * BBUF;
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, dst + (q * kXT + wave * 64) * 8);
+  };
+
+  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? aux[2 * N + n0 + tid] : 1.f;
+  stage_b(0);
+  stage_a(0);
+  stage_a(1);
+  stage_a(2);
+
+  f32x4 acc[4][CT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed: this wave's copies of B(c) and A(c) retired (only the
+    // newest A chunk, AQ copies, may still be in flight; in the first
+    // iteration A(1) and A(2) too), then every wave's, by the barrier; the
+    // barrier also retires all reads of the buffers restaged below
+    if (c == 0) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage_b(c + 1);
+    stage_a(c + 3);
+    const _Float16* a = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
+    const _Float16* b = bring + (c & (kXBbuf - 1)) * BBUF;
+    // the whole 32-deep chunk is one k-step: 8 A + 2 CT B fragment reads,
+    // 12 CT MFMAs (ah bh + ah bl + al bh per 16x16 output tile)
+    half8 ah[4], al[4], bh[CT], bl[CT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + i * 16 + lc;
+      const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
+      ah[i] = *reinterpret_cast<const half8*>(a + ao);
+      al[i] = *reinterpret_cast<const half8*>(a + kXM * kXK + ao);
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int col = (wc * CT + t) * 16 + lc;
+      const int bo = col * kXK + ((lq ^ x3_swz(col)) * 8);
+      bh[t] = *reinterpret_cast<const half8*>(b + bo);
+      bl[t] = *reinterpret_cast<const half8*>(b + LDW * kXK + bo);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh[t], acc[i][t], 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl[t], acc[i][t], 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[t], acc[i][t], 0, 0, 0);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue (as mm2_project_kernel): unscale, add weighted text sum + c0,
+  // divide by the total weight (column D), L2-normalise the row.  Every load
+  // is unconditional (row and column clamped in range, results selected
+  // afterwards).  Lane value (i, t, j): row wr*64 + 16 i + 4 lq + j, column
+  // (wc*CT + t)*16 + lc.
+  {
+    float nv[16][CT], tv[16], cv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3);
+      const int64_t rowc = min(n0 + rl, N - 1);
+      tv[r] = aux[N + rowc];
+      cv[r] = aux[rowc];
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 16 + lc;
+        nv[r][t] = num[rowc * D + min(col, D - 1)];
+      }
+    }
+    float cadd[CT], cinv[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int col = (wc * CT + t) * 16 + lc;
+      cinv[t] = col_inv[col];
+      cadd[t] = c0[col];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3);
+      const float inv_rs = 1.f / s_rs[rl];
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 16 + lc;
+        const float add = col < D ? text_sum(nv[r][t], cv[r]) : (col == D ? tv[r] : 0.f);
+        const float y = acc[r >> 2][t][r & 3] * (cinv[t] * inv_rs) + add + cadd[t];
+        acc[r >> 2][t][r & 3] = y;
+        if (col == D) s_tot[rl] = y;
+      }
+    }
+  }
+  __syncthreads();
+  float ss[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ss[r] = 0.f;
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const int col = (wc * CT + t) * 16 + lc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3);
+      const float cs = acc[r >> 2][t][r & 3] / s_tot[rl];
+      acc[r >> 2][t][r & 3] = cs;
+      if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = ss[r];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);  // the 16 lanes of a row
+    if (lc == 0) s_ss[wc][wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3)] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rl = wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3);
+    const int64_t row = n0 + rl;
+    const float inv = 1.f / sqrtf((s_ss[0][rl] + s_ss[1][rl]) + (s_ss[2][rl] + s_ss[3][rl]));
+    if (row < N) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 16 + lc;
+        if (col < D) out[row * D + col] = acc[r >> 2][t][r & 3] * inv;
+      }
+    }
+  }
+
+  if (pc) {
+    // fused first-PC removal of the a2 rows (sif_functions.py:77-78, npc = 1):
+    // sif = x - (x . pc) pc in f64, with the accumulators dead.  Wave w owns
+    // rows w, w + 8, ... of the tile (4 at a time, every load issued first);
+    // lane l columns l + 64 m.  The x rows come back from L2 / Infinity Cache
+    // (this workgroup read them for the text sum above).
+    constexpr int PER = (LDW + 63) / 64;
+    double pcv[PER];
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+      const int col = lane + 64 * m;
+      pcv[m] = col < D ? pc[col] : 0.0;
+    }
+    for (int g = wave; g < kXM; g += 4 * (kXT / 64)) {
+      float xv[4][PER];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t rowc = min(n0 + g + q * (kXT / 64), N - 1);
+#pragma unroll
+        for (int m = 0; m < PER; ++m) xv[q][m] = num[rowc * D + min(lane + 64 * m, D - 1)];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = n0 + g + q * (kXT / 64);
+        double dp = 0.0;
+#pragma unroll
+        for (int m = 0; m < PER; ++m) dp = fma(static_cast<double>(xv[q][m]), pcv[m], dp);
+        const double dot = wave_sum(dp);
+        if (row < N) {
+#pragma unroll
+          for (int m = 0; m < PER; ++m) {
+            const int col = lane + 64 * m;
+            if (col < D) sif[row * D + col] = static_cast<float>(static_cast<double>(xv[q][m]) - dot * pcv[m]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int CT>
+constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(float); }
+
+// Projection kernel variant: 0 = 32x32x16 MFMA tiles (wave = 32 rows x 32 CT
+// columns), 1 = 16x16x32 tiles (wave = 64 rows x 16 CT columns: 18 instead of
+// 24 fragment reads per chunk).  MMB_PROJ_VARIANT overrides (read once).
+static int proj_variant() {
+  static const int v = [] {
+    const char* e = getenv("MMB_PROJ_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <int CT>
 static int launch_project_x3(const _Float16* s, const float* num, const float* aux,
                              const _Float16* img, const float* ci, const float* c0, int64_t n,
                              int kp, int d, float* out, const double* pc, float* sif,
@@ -617,8 +859,21 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
-  mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out,
-                                                        pc, sif);
+  if (proj_variant() == 1) {
+    constexpr size_t ldsb = x3b_lds_bytes<CT>();
+    static_assert(ldsb <= 160 * 1024, "x3b chunk rings exceed LDS");
+    static bool attr_b = false;
+    if (!attr_b) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+      attr_b = true;
+    }
+    mm2_project_x3b_kernel<CT><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp, d,
+                                                            out, pc, sif);
+  } else {
+    mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out,
+                                                          pc, sif);
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
