@@ -50,6 +50,17 @@ __device__ __forceinline__ void ldv(const float* p, float (&v)[VEC]) {
     v[0] = *p;
   }
 }
+// the same, non-temporal: for the read-once frame streams
+template <int VEC>
+__device__ __forceinline__ void ldv_nt(const float* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    using f4 = float __attribute__((ext_vector_type(4)));
+    const f4 q = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    v[0] = __builtin_nontemporal_load(p);
+  }
+}
 
 // Power-of-2 scale that brings a row's max |value| into [2^14, 2^15): the
 // projection GEMM splits the sums into fp16 hi/lo pairs (mm2_kernels.hip) and
@@ -136,18 +147,25 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       }
       __syncthreads();
       if (actT) {
+        // branch-free: a negative offset (negative or flagged id) loads row
+        // 0 and contributes nothing, so the unrolled iterations keep their
+        // loads in flight together (a `continue` per token would wait on
+        // each load right after its branch)
 #pragma unroll 4
         for (int t = rT; t < tl; t += RT) {
           const float w = s_w[t];
           const int64_t off = s_off[t];
-          if (off < 0 || (!MM2 && w == 0.f)) continue;
+          const bool ok = off >= 0;
+          const int64_t o = ok ? off : 0;
           float v[VT];
-          ldv<VT>(tsrc + off + cT * VT, v);
+          ldv<VT>(tsrc + o + cT * VT, v);
+#pragma unroll
+          for (int e = 0; e < VT; ++e) v[e] = ok ? v[e] : 0.f;
           if (split_emb) {
             float u[VT];
-            ldv<VT>(esrc + off + cT * VT, u);
+            ldv<VT>(esrc + o + cT * VT, u);
 #pragma unroll
-            for (int e = 0; e < VT; ++e) num[e] = fmaf(w, u[e], num[e]);
+            for (int e = 0; e < VT; ++e) num[e] = fmaf(w, ok ? u[e] : 0.f, num[e]);
           } else {
 #pragma unroll
             for (int e = 0; e < VT; ++e) num[e] = fmaf(w, v[e], num[e]);
@@ -176,7 +194,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
 #pragma unroll 4
         for (int t = rA; t < a.L; t += RA) {
           float v[VA];
-          ldv<VA>(base + static_cast<int64_t>(t) * a.A, v);
+          ldv_nt<VA>(base + static_cast<int64_t>(t) * a.A, v);
 #pragma unroll
           for (int e = 0; e < VA; ++e) {
             sa[e] += v[e];
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
 #pragma unroll 4
         for (int t = rV; t < a.L; t += RV) {
           float v[VV];
-          ldv<VV>(base + static_cast<int64_t>(t) * a.Vd, v);
+          ldv_nt<VV>(base + static_cast<int64_t>(t) * a.Vd, v);
 #pragma unroll
           for (int e = 0; e < VV; ++e) {
             sv[e] += v[e];
