@@ -600,10 +600,23 @@ static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
   }
 }
 
+// Workgroups per CU of the grid-stride wave kernel: 2 = exactly the resident
+// waves at its occupancy (2 waves / SIMD), one even share of utterances per
+// wave.  Measured (tools/grid_sweep.sh, MI355X): 2/4/8/16/32 = 20.88/20.94/
+// 21.04/21.01/21.18 ms.  MMB_STREAM_GRID_MULT overrides it (read once).
+static int stream_grid_mult() {
+  static const int m = [] {
+    const char* e = getenv("MMB_STREAM_GRID_MULT");
+    const int v = e ? atoi(e) : 2;
+    return v > 0 ? v : 2;
+  }();
+  return m;
+}
+
 template <bool MM2, int CT, int CA, int CV>
 static int launch_wave(const StreamArgs& a, hipStream_t stream) {
   const int64_t blocks = ceil_div(a.N, 4);
-  const int grid_cap = 8 * stream_cu_count(stream);
+  const int grid_cap = stream_grid_mult() * stream_cu_count(stream);
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
   switch (MM2 ? stream_policy() & 7 : 0) {
     case 1: launch_wave_v<MM2, CT, CA, CV, 2, true, false>(a, grid, stream); break;
