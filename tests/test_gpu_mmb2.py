@@ -103,10 +103,12 @@ def test_single_utterance_errors_like_reference(gpu, golden):
         _drop_in_call(gen, E, ids[:1], audio[:1], visual[:1], weights, gpu)
 
 
-@pytest.mark.parametrize("N,T,A,Vd", [(2048, 40, 300, 300), (1000, 20, 78, 50)])
+@pytest.mark.parametrize("N,T,A,Vd", [(2048, 40, 300, 300), (1000, 20, 78, 50), (256, 300, 300, 300),
+                                     (100, 130, 78, 50)])
 def test_fused_step_vs_oracle(gpu, N, T, A, Vd):
     """Both outputs of the bench step against the oracle at a mid size
-    (incl. feature widths that are not multiples of 4: scalar-load variants)."""
+    (incl. feature widths that are not multiples of 4: scalar-load variants, and
+    T > 64: the POM-shape workgroup-per-utterance stream kernel)."""
     from oracle import sif_oracle as O
 
     V = 30_000
