@@ -29,6 +29,8 @@ sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+F16_MFMA_PEAK_TFS = 2500.0  # dense f16 MFMA (no sparsity)
+F64_MFMA_PEAK_TFS = 78.6  # fp64 MFMA
 
 
 def log(*a):
@@ -194,6 +196,28 @@ def main():
                            else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)"),
                 "algorithmic_bytes_per_utt": kb, "utts_per_launch": utts_per_launch,
                 "avg_launch_ms": round(stream_launch_ms, 4)}
+        # MFMA-bound kernels of the step, from their HIP-event phase times:
+        # the projection as 3 f16 GEMMs [U, kp] x [kp, ldw] (hi/lo split; its
+        # phase includes the fused PC-removal tail), the Gram as the 16x16
+        # upper-triangle tiles it computes in fp64
+        mfma = {}
+        kp, ldw = step.proj.kp, step.proj.ldw
+        proj_ms = phase_ms.get("mm2_project+pc_remove", phase_ms.get("mm2_project+gram"))
+        if proj_ms and step.s_half:
+            tf = 3 * 2 * kp * ldw * U / (proj_ms / 1e3) / 1e12
+            mfma["mm2_project_x3b"] = {"bound": "mfma", "achieved": round(tf, 1),
+                                       "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                       "frac": round(tf / F16_MFMA_PEAK_TFS, 4),
+                                       "flop_per_utt": 3 * 2 * kp * ldw,
+                                       "includes": "fused PC-removal tail"}
+        if "gram" in phase_ms:
+            nt = (D + 15) // 16
+            gflop = nt * (nt + 1) // 2 * 16 * 16 * 2 * U
+            tf = gflop / (phase_ms["gram"] / 1e3) / 1e12
+            mfma["gram_tri (fp64)"] = {"bound": "mfma", "achieved": round(tf, 2),
+                                       "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                       "frac": round(tf / F64_MFMA_PEAK_TFS, 4),
+                                       "flop_per_utt": gflop // U}
         pb = path_bytes(T, D, 300, 300)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -227,6 +251,7 @@ def main():
             "path_roofline": {"bytes_per_utt": pb, "achieved": round(pb * U * world / (ms_per_step / 1e3) / world / 1e9, 1),
                               "unit": "GB/s per GPU", "peak": HBM_PEAK_GBS},
             "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
+            "mfma_rooflines": mfma,
             "chunks": len(step.bounds),
             "cpu_baseline": cpu,
         }
