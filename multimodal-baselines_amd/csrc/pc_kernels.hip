@@ -725,7 +725,9 @@ __device__ void p16_gram(const double* X, const double* Y, int Dp, int k, double
 
 // GZ = G Z (G symmetric [D][D] in global memory / L2).  16 k-steps of loads
 // are issued before their MFMAs (one L2 latency per batch, not per step);
-// two accumulators alternate so consecutive MFMAs are independent.
+// two accumulators alternate so consecutive MFMAs are independent.  (32-step
+// batches measured slower on MI355X: 24.3 vs 19.5 us per product.)
+constexpr int kGzBatch = 16;
 __device__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double* Z, double* GZ) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int mt = Dp / 16;
@@ -733,16 +735,16 @@ __device__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double
     const int p = t * 16 + (lane & 15);
     const int pc = min(p, D - 1);
     f64x4 acc0 = {0, 0, 0, 0}, acc1 = acc0;
-    for (int q0 = 0; q0 < Dp; q0 += 64) {
-      double g[16];
+    for (int q0 = 0; q0 < Dp; q0 += 4 * kGzBatch) {
+      double g[kGzBatch];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
+      for (int s = 0; s < kGzBatch; ++s) {
         const int q = q0 + 4 * s + (lane >> 4);
         // clamped address, unconditional load, selected after (keeps loads in flight)
         g[s] = G[static_cast<int64_t>(min(q, D - 1)) * D + pc];
       }
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
+      for (int s = 0; s < kGzBatch; ++s) {
         const int q = q0 + 4 * s + (lane >> 4);
         const double a = (p < D && q < D) ? g[s] : 0.0;
         const double b = Z[min(q, Dp - 1) * kP16W + (lane & 15)];
@@ -884,10 +886,14 @@ __device__ double p16_top_eig(const double* A, int k, int lane, double* u) {
 
 // Orthonormalise the k columns of Z [Dp][16]: equilibration, CholeskyQR twice;
 // wave-0 MGS^2 on a compact copy if a pivot fails (extreme ill-conditioning).
+// npass = 3: equilibration + CholeskyQR2 (orthonormal to rounding); npass =
+// 2: equilibration + one CholeskyQR -- a well-conditioned basis of the same
+// span, all the subspace iteration needs between products (the span, not the
+// basis, fixes the result: span(Q) = span(G^q Omega)).
 __device__ void p16_orth(double* Z, int D, int Dp, int k, double* part, double* sW, double* sL,
-                         double* sLi, int* s_fail) {
+                         double* sLi, int* s_fail, int npass = 3) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  for (int pass = 0; pass < 3; ++pass) {
+  for (int pass = 0; pass < npass; ++pass) {
     p16_gram(Z, Z, Dp, k, part, sW);
     if (pass == 0) {
       if (tid < D) {
@@ -955,7 +961,9 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve16_kernel(const double* __re
     sGZ[e] = 0.0;
   }
   __syncthreads();
-  p16_orth(sZ, D, Dp, k, part, sW, sL, sLi, &s_fail);
+  // one CholeskyQR pass between products, CholeskyQR2 for the block the
+  // final Rayleigh-Ritz step uses (orthonormal to rounding, as before)
+  p16_orth(sZ, D, Dp, k, part, sW, sL, sLi, &s_fail, n_iter > 0 ? 2 : 3);
   PC_MARK(1);
   double* Z = sZ;
   double* GZ = sGZ;
@@ -964,7 +972,7 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve16_kernel(const double* __re
     __syncthreads();
     PC_MARK(2 + 2 * it);
     double* t = Z; Z = GZ; GZ = t;  // the product becomes the block
-    p16_orth(Z, D, Dp, k, part, sW, sL, sLi, &s_fail);
+    p16_orth(Z, D, Dp, k, part, sW, sL, sLi, &s_fail, it == n_iter - 1 ? 3 : 2);
     PC_MARK(3 + 2 * it);
   }
   p16_gz(G, D, Dp, Z, GZ);
