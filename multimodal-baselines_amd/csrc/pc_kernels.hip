@@ -179,11 +179,17 @@ __global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict
       if (idx < kG2Rows * 80) {
         const int rr = idx / 80, uu = idx % 80;
         double* dst = s_x + (buf * kG2Rows + rr) * kG2Stride + 4 * uu;
-        // x = num / count in f32 (sif_functions.py:55), then exact f64 widening
-        dst[0] = static_cast<double>(cnt ? v[q].x / sc[q] : v[q].x);
-        dst[1] = static_cast<double>(cnt ? v[q].y / sc[q] : v[q].y);
-        dst[2] = static_cast<double>(cnt ? v[q].z / sc[q] : v[q].z);
-        dst[3] = static_cast<double>(cnt ? v[q].w / sc[q] : v[q].w);
+        // x = num / count in f32 (sif_functions.py:55), then exact f64
+        // widening; two 16-byte writes (ds_write_b128: the 8 lanes of a
+        // write phase hit disjoint banks at this 32-byte lane stride, where
+        // four 8-byte writes conflicted 2-way)
+        using d2 = double __attribute__((ext_vector_type(2)));
+        const d2 lo = {static_cast<double>(cnt ? v[q].x / sc[q] : v[q].x),
+                       static_cast<double>(cnt ? v[q].y / sc[q] : v[q].y)};
+        const d2 hi = {static_cast<double>(cnt ? v[q].z / sc[q] : v[q].z),
+                       static_cast<double>(cnt ? v[q].w / sc[q] : v[q].w)};
+        *reinterpret_cast<d2*>(dst) = lo;
+        *reinterpret_cast<d2*>(dst + 2) = hi;
       }
     }
   };
