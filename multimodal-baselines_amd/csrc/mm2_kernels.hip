@@ -364,6 +364,48 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)lds, 16, 0, 0);
 }
 
+// Sums over the 16 lanes of a DPP row (lanes 16k .. 16k+15), every lane
+// receiving the row's total: quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror and row_mirror -- register-to-register moves, where
+// __shfl_xor is an LDS-unit ds_bpermute waited on per step.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u & 0xffffffffu), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<unsigned long long>(static_cast<unsigned>(hi)) << 32) |
+                              static_cast<unsigned>(lo));
+}
+constexpr int kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppRowHalfMirror = 0x141,
+              kDppRowMirror = 0x140;
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<kDppQuad1032>(v);
+  v += dpp_f32<kDppQuad2301>(v);
+  v += dpp_f32<kDppRowHalfMirror>(v);
+  v += dpp_f32<kDppRowMirror>(v);
+  return v;
+}
+// 64-lane sum in f64, fixed order: the four row sums combined from lanes 0,
+// 16, 32, 48 (wave-uniform result)
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<kDppQuad1032>(v);
+  v += dpp_f64<kDppQuad2301>(v);
+  v += dpp_f64<kDppRowHalfMirror>(v);
+  v += dpp_f64<kDppRowMirror>(v);
+  auto rl = [&](int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane(static_cast<int>(u & 0xffffffffu), l);
+    const unsigned hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), l);
+    return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
+  };
+  return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+
+
 // out = L2-normalised (num + s @ Wm[:, :D] + c0) / (total), the fp16 hi/lo
 // split GEMM on the f16 MFMA pipe (sif2.py:186-207).
 //   S_split [N][2][Kp] fp16: hi | lo of the row-scaled sums (mmb_mm2_stream)
@@ -657,7 +699,8 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, dst + (q * kXT + wave * 64) * 8);
   };
 
-  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? aux[2 * N + n0 + tid] : 1.f;
+  // 1 / row scale (a power of two: exact)
+  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
   stage_b(0);
   stage_a(0);
   stage_a(1);
@@ -743,7 +786,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rl = wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3);
-      const float inv_rs = 1.f / s_rs[rl];
+      const float inv_rs = s_rs[rl];
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
         const int col = (wc * CT + t) * 16 + lc;
@@ -755,25 +798,27 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     }
   }
   __syncthreads();
-  float ss[16];
+  // one division per row: cs = y * (1 / total) (1 / 0 = inf keeps the
+  // reference's NaN rows for a zero total)
+  float ss[16], rt[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) ss[r] = 0.f;
+  for (int r = 0; r < 16; ++r) {
+    ss[r] = 0.f;
+    rt[r] = 1.f / s_tot[wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3)];
+  }
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const int col = (wc * CT + t) * 16 + lc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int rl = wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3);
-      const float cs = acc[r >> 2][t][r & 3] / s_tot[rl];
+      const float cs = acc[r >> 2][t][r & 3] * rt[r];
       acc[r >> 2][t][r & 3] = cs;
       if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
     }
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    float v = ss[r];
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);  // the 16 lanes of a row
+    const float v = row16_sum(ss[r]);  // the 16 lanes of a row
     if (lc == 0) s_ss[wc][wr * 64 + (r >> 2) * 16 + lq * 4 + (r & 3)] = v;
   }
   __syncthreads();
@@ -818,7 +863,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
         double dp = 0.0;
 #pragma unroll
         for (int m = 0; m < PER; ++m) dp = fma(static_cast<double>(xv[q][m]), pcv[m], dp);
-        const double dot = wave_sum(dp);
+        const double dot = wave_sum_dpp(dp);
         if (row < N) {
 #pragma unroll
           for (int m = 0; m < PER; ++m) {

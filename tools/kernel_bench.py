@@ -74,6 +74,11 @@ def main():
     if "project" in which:
         res["project"] = timed(lambda: P.mm2_project(step.s, step.x, step.aux, step.proj,
                                                      out=step.mmb2), args.reps)
+    if "project_rm" in which:  # the bench path: projection + fused PC removal
+        pc = P.pc_solve(step.G, z0, 1, False)
+        res["project_rm"] = timed(lambda: P.mm2_project(step.s, step.x, step.aux, step.proj,
+                                                        out=step.mmb2, pc=pc, sif_out=step.sif),
+                                  args.reps)
     if "project32" in which:
         s32 = P.s_buffer(step.n, step.proj.kp, False, dev)
         P.mm2_stream(step.n, step.t, 300, 300, 300, inp["audio"], inp["visual"], ids32=inp["ids"],
