@@ -96,6 +96,6 @@ def get_sentence_embeddings(word_embeddings, weights, text):
     text = np.asarray(text)
     if text.dtype.kind not in "iu":
         raise IndexError("arrays used as indices must be of integer type")
-    ids = P.narrow_ids(torch.from_numpy(np.ascontiguousarray(text.astype(np.int64))).to(dev))
+    ids = P.narrow_ids(torch.from_numpy(np.ascontiguousarray(text, dtype=np.int64)).to(dev))
     out, _ = P.sif_embeddings(table, ids, wtab32=wtab32, npc=1, out_dtype=torch.float64)
     return out.cpu().numpy()
