@@ -293,3 +293,42 @@ def test_zero_weight_rows_sif_nan_mmb2_finite(gpu):
                                             M.params_from_module(gen.cpu()), sw, text)
     assert np.isfinite(mm2_out).all()
     assert M.row_rel_err(mm2_out, ref) < TOL
+
+
+_VARIANT_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[2], sys.argv[2] + "/multimodal-baselines_amd"]
+import models, pipeline as P, synth
+dev = torch.device("cuda", 0)
+inp = synth.device_workload(700, 40, 5000, A=300, Vd=300, seed=31, device=dev)
+torch.manual_seed(0)
+gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
+s, m = P.FusedStep(inp, gen.networks()).run()
+np.savez(sys.argv[1], sif=s.cpu().numpy(), mmb2=m.cpu().numpy())
+"""
+
+
+@pytest.mark.parametrize("env", [{"MMB_PROJ_VARIANT": "0", "MMB_STREAM_POLICY": "0"},
+                                 {"MMB_STREAM_POLICY": "7", "MMB_STREAM_GRID_MULT": "8"}])
+def test_non_default_kernel_variants_agree(gpu, tmp_path, env):
+    """The measured-and-kept-selectable variants (32x32x16 projection tiles,
+    every stream-kernel load/store policy, grid size; read once per process,
+    so run in a child process) give the default path's rows: SIF to the
+    removal's dot order, MMB2 within the 1e-5 bar."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = str(tmp_path / "variant.npz")
+    subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, path, root], check=True, timeout=300,
+                   env={**os.environ, **env})
+    z = np.load(path)
+    inp = synth.device_workload(700, 40, 5000, A=300, Vd=300, seed=31, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    s, m = P.FusedStep(inp, gen.networks()).run()
+    # SIF: the same x, Gram and PC; the removal's f64 dot may sum in another
+    # order (the 32x32x16 kernel's tail reduces with shuffles, not DPP)
+    assert M.row_rel_err(z["sif"], s.cpu().numpy()) < 1e-6
+    assert M.row_rel_err(z["mmb2"], m.cpu().numpy()) < TOL
