@@ -404,6 +404,11 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   };
   return (rl(0) + rl(16)) + (rl(32) + rl(48));
 }
+__device__ __forceinline__ float wave_sum_dpp_f32(float v) {
+  v = row16_sum(v);
+  auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
 
 
 // out = L2-normalised (num + s @ Wm[:, :D] + c0) / (total), the fp16 hi/lo
@@ -645,7 +650,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
   }
 }
 
-template <int CT>
+template <int CT, bool ROWEPI>
 __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
     const _Float16* __restrict__ img, const float* __restrict__ col_inv,
@@ -757,6 +762,128 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  if constexpr (ROWEPI) {
+    // Row-wise epilogue (D % 4 == 0, 16-byte aligned rows): the raw
+    // accumulators of 64 rows at a time go through the idle LDS rings
+    // (row stride 324 floats: the 4 row groups of an MFMA store land on
+    // disjoint banks), then each wave finishes 8 whole rows with 16-byte
+    // loads / stores: lane l owns columns 4l.. and 256 + 4l.. .  One read of
+    // x serves the weighted text sum and the fused PC removal.
+    constexpr int kRS = 324;
+    float* sacc = reinterpret_cast<float*>(lds);
+    const int U = D >> 2;                 // float4 units of a row
+    const bool u1 = lane + 64 < U;        // second unit (columns 256 + 4l..)
+    const int c0a = 4 * lane, c1a = 256 + 4 * min(lane, 15);  // acc columns (LDW <= 320)
+    const int c0x = 4 * min(lane, U - 1), c1x = 4 * min(lane + 64, U - 1);
+    float4 ci0, ci1, ca0, ca1;
+    {
+      const int cA = min(c0a, LDW - 4), cB = c1a;
+      ci0 = make_float4(col_inv[cA], col_inv[cA + 1], col_inv[cA + 2], col_inv[cA + 3]);
+      ca0 = make_float4(c0[cA], c0[cA + 1], c0[cA + 2], c0[cA + 3]);
+      ci1 = make_float4(col_inv[cB], col_inv[cB + 1], col_inv[cB + 2], col_inv[cB + 3]);
+      ca1 = make_float4(c0[cB], c0[cB + 1], c0[cB + 2], c0[cB + 3]);
+    }
+    double pv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pv[e] = 0.0;
+    if (pc) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pv[e] = lane < U ? pc[c0x + e] : 0.0;
+        pv[4 + e] = u1 ? pc[c1x + e] : 0.0;
+      }
+    }
+    const int lane_tot = (D - 256) >> 2, e_tot = (D - 256) & 3;  // column D in unit 1
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+      __syncthreads();  // the rings' last reads / the previous pass's rows
+      if (wr == p) {
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2)
+#pragma unroll
+          for (int t = 0; t < CT; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              sacc[(i2 * 16 + lq * 4 + j) * kRS + (wc * CT + t) * 16 + lc] = acc[i2][t][j];
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int h = 0; h < 2; ++h) {
+        // 4 rows of this wave: all loads first
+        float4 xa[4], xb[4], aa[4], ab[4];
+        float cn[4], tw[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = p * 64 + wave * 8 + h * 4 + q;
+          const int64_t rowc = min(n0 + rl, N - 1);
+          xa[q] = *reinterpret_cast<const float4*>(num + rowc * D + c0x);
+          xb[q] = *reinterpret_cast<const float4*>(num + rowc * D + c1x);
+          cn[q] = aux[rowc];
+          tw[q] = aux[N + rowc];
+          const float* sr = sacc + (rl - p * 64) * kRS;
+          aa[q] = *reinterpret_cast<const float4*>(sr + c0a);
+          ab[q] = *reinterpret_cast<const float4*>(sr + c1a);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = p * 64 + wave * 8 + h * 4 + q;
+          const int64_t row = n0 + rl;
+          const float irs = s_rs[rl];
+          // y = unscaled product + (weighted text sum x * count, or the total
+          // weight sum_t w at column D) + c0 -- the tile epilogue's order
+          const float av[8] = {aa[q].x, aa[q].y, aa[q].z, aa[q].w, ab[q].x, ab[q].y, ab[q].z, ab[q].w};
+          const float civ[8] = {ci0.x, ci0.y, ci0.z, ci0.w, ci1.x, ci1.y, ci1.z, ci1.w};
+          const float cav[8] = {ca0.x, ca0.y, ca0.z, ca0.w, ca1.x, ca1.y, ca1.z, ca1.w};
+          const float xv[8] = {xa[q].x, xa[q].y, xa[q].z, xa[q].w, xb[q].x, xb[q].y, xb[q].z, xb[q].w};
+          float y[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int col = (e < 4 ? c0a : 256 + 4 * lane) + (e & 3);
+            const bool in = e < 4 ? lane < U : u1;
+            const float add = (in && col < D) ? text_sum(xv[e], cn[q]) : (col == D ? tw[q] : 0.f);
+            y[e] = av[e] * (civ[e] * irs) + add + cav[e];
+          }
+          // the total (column D) from its lane; cs = y / total
+          const float ysel = e_tot == 0 ? y[4] : e_tot == 1 ? y[5] : e_tot == 2 ? y[6] : y[7];
+          const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ysel), lane_tot));
+          const float rt = 1.f / tot;
+          float ss = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool in = e < 4 ? lane < U : u1;
+            y[e] *= rt;
+            if (in) ss = fmaf(y[e], y[e], ss);
+          }
+          const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
+          double dot = 0.0;
+          if (pc) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dot = fma(static_cast<double>(xv[e]), pv[e], dot);
+            dot = wave_sum_dpp(dot);
+          }
+          if (row < N) {
+            float* orow = out + row * D;
+            if (lane < U)
+              *reinterpret_cast<float4*>(orow + c0x) =
+                  make_float4(y[0] * inv, y[1] * inv, y[2] * inv, y[3] * inv);
+            if (u1)
+              *reinterpret_cast<float4*>(orow + c1x) =
+                  make_float4(y[4] * inv, y[5] * inv, y[6] * inv, y[7] * inv);
+            if (pc) {
+              float* srow = sif + row * D;
+              float o[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                o[e] = static_cast<float>(static_cast<double>(xv[e]) - dot * pv[e]);
+              if (lane < U) *reinterpret_cast<float4*>(srow + c0x) = make_float4(o[0], o[1], o[2], o[3]);
+              if (u1) *reinterpret_cast<float4*>(srow + c1x) = make_float4(o[4], o[5], o[6], o[7]);
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
   // epilogue (as mm2_project_kernel): unscale, add weighted text sum + c0,
   // divide by the total weight (column D), L2-normalise the row.  Every load
   // is unconditional (row and column clamped in range, results selected
@@ -882,6 +1009,16 @@ constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(
 // Projection kernel variant: 0 = 32x32x16 MFMA tiles (wave = 32 rows x 32 CT
 // columns), 1 = 16x16x32 tiles (wave = 64 rows x 16 CT columns: 18 instead of
 // 24 fragment reads per chunk).  MMB_PROJ_VARIANT overrides (read once).
+// Row-wise projection epilogue (1, default) or the MFMA-tile-layout one (0);
+// MMB_PROJ_ROWEPI overrides (read once).
+static bool proj_row_epilogue() {
+  static const bool v = [] {
+    const char* e = getenv("MMB_PROJ_ROWEPI");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 static int proj_variant() {
   static const int v = [] {
     const char* e = getenv("MMB_PROJ_VARIANT");
@@ -909,12 +1046,24 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
     static_assert(ldsb <= 160 * 1024, "x3b chunk rings exceed LDS");
     static bool attr_b = false;
     if (!attr_b) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
       attr_b = true;
     }
-    mm2_project_x3b_kernel<CT><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp, d,
-                                                            out, pc, sif);
+    auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    // the row-wise epilogue: D in [256, 320) (column D in a lane's second
+    // unit), whole float4 units, 16-byte aligned rows
+    const bool rowepi = CT == 5 && d >= 256 && d % 4 == 0 && a16(num) && a16(out) &&
+                        (sif == nullptr || a16(sif)) && proj_row_epilogue();
+    if (rowepi) {
+      mm2_project_x3b_kernel<CT, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp,
+                                                                    d, out, pc, sif);
+    } else {
+      mm2_project_x3b_kernel<CT, false><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n,
+                                                                     kp, d, out, pc, sif);
+    }
   } else {
     mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out,
                                                           pc, sif);
