@@ -57,6 +57,20 @@ def main(src, tag):
     bench = json.load(open(os.path.join(src, "bench.json")))
     lines += ["## bench line", "", "```json", json.dumps(bench, indent=1), "```", ""]
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    # the traced process's own bench line: its HIP-event stream-kernel average
+    # against rocprofv3's average for the same launches (same process; the
+    # untraced bench above is another process, and the stream kernel varies
+    # a few % from process to process on one box)
+    tb_path = os.path.join(src, "trace_bench.json")
+    if os.path.exists(tb_path):
+        tb = json.load(open(tb_path))
+        ev = tb["roofline"]["avg_launch_ms"]
+        rp = [float(r["AverageNs"]) / 1e6 for r in stats if "utt_wave_kernel" in r["Name"]
+              or "utt_stream_kernel" in r["Name"]]
+        lines += ["## traced run: HIP events vs rocprofv3 (same process)", "",
+                  f"stream kernel avg launch: HIP events {ev:.4f} ms, rocprofv3 "
+                  f"{rp[0] if rp else float('nan'):.4f} ms; traced-run value {tb['value']:.1f} utt/s, "
+                  f"{tb['ms_per_step']:.4f} ms/step", ""]
     lines += ["## kernel stats (`rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 "
               "--warmup 3 --no-cpu-baseline`)", "",
               "| kernel | calls | avg ms | total % |", "|---|---|---|---|"]
