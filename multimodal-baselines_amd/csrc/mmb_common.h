@@ -32,6 +32,59 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Sums over the 16 lanes of a DPP row (lanes 16k .. 16k+15), every lane
+// receiving the row's total: quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror and row_mirror -- register-to-register moves, where
+// __shfl_xor is an LDS-unit ds_bpermute waited on per step.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u & 0xffffffffu), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<unsigned long long>(static_cast<unsigned>(hi)) << 32) |
+                              static_cast<unsigned>(lo));
+}
+constexpr int kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppRowHalfMirror = 0x141,
+              kDppRowMirror = 0x140;
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<kDppQuad1032>(v);
+  v += dpp_f32<kDppQuad2301>(v);
+  v += dpp_f32<kDppRowHalfMirror>(v);
+  v += dpp_f32<kDppRowMirror>(v);
+  return v;
+}
+// 64-lane sum in f64, fixed order: the four row sums combined from lanes 0,
+// 16, 32, 48 (wave-uniform result)
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<kDppQuad1032>(v);
+  v += dpp_f64<kDppQuad2301>(v);
+  v += dpp_f64<kDppRowHalfMirror>(v);
+  v += dpp_f64<kDppRowMirror>(v);
+  auto rl = [&](int l) {
+    const unsigned long long u = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane(static_cast<int>(u & 0xffffffffu), l);
+    const unsigned hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), l);
+    return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
+  };
+  return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+__device__ __forceinline__ float wave_sum_dpp_f32(float v) {
+  v = row16_sum(v);
+  auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+// Broadcast of lane l's double (l wave-uniform): two v_readlane, no LDS.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane(static_cast<int>(u & 0xffffffffu), l);
+  const unsigned hi = __builtin_amdgcn_readlane(static_cast<int>(u >> 32), l);
+  return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+
 // Sum within each 32-lane half of the wave (lanes l and l^k for k < 32).
 __device__ __forceinline__ float half_sum(float v) {
 #pragma unroll

@@ -782,13 +782,13 @@ __device__ void p16_chol(const double* sW, double* sL, double* sLi, int k, int l
 #pragma unroll
   for (int j = 0; j < kMaxK; ++j) {
     if (j < k) {
-      const double djj = __shfl(w[j], j, kWave);
+      const double djj = readlane_f64(w[j], j);  // broadcast: no LDS round trip
       bad = bad || !(djj > 0.0);
       const double s = sqrt(djj > 0.0 ? djj : 1.0);
       const double lij = (lane == j) ? s : (lane > j ? w[j] / s : 0.0);
       l[j] = lij;
 #pragma unroll
-      for (int m = j + 1; m < kMaxK; ++m) w[m] -= lij * __shfl(lij, m, kWave);
+      for (int m = j + 1; m < kMaxK; ++m) w[m] -= lij * readlane_f64(lij, m);
     }
   }
   if (bad && lane == 0) *fail = 1;
@@ -842,7 +842,7 @@ __device__ double p16_top_eig(const double* A, int k, int lane, double* u) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (r0 + 4 * r == c) tr += acc[r];
-    tr = wave_sum(tr);
+    tr = wave_sum_dpp(tr);
     const double inv = tr > 0.0 ? 1.0 / tr : 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) b[r] = acc[r] * inv;
@@ -876,12 +876,12 @@ __device__ double p16_top_eig(const double* A, int k, int lane, double* u) {
       for (int m = 0; m < k; ++m) y += A[lane * k + m] * u[m];
     }
     const double ui = lane < k ? u[lane] : 0.0;
-    const double nrm2 = wave_sum(lane < k ? ui * ui : 0.0);
-    lam = wave_sum(ui * y) / nrm2;  // Rayleigh quotient of the current u
+    const double nrm2 = wave_sum_dpp(lane < k ? ui * ui : 0.0);
+    lam = wave_sum_dpp(ui * y) / nrm2;  // Rayleigh quotient of the current u
     if (step == 2) {
       if (lane < k) u[lane] = ui / sqrt(nrm2);
     } else {
-      const double yn = sqrt(wave_sum(y * y));
+      const double yn = sqrt(wave_sum_dpp(y * y));
       wave_lds_sync();
       if (lane < k) u[lane] = yn > 0.0 ? y / yn : ui;
     }
