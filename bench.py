@@ -10,16 +10,27 @@ produced in device memory.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--utts-per-gpu U]
 
-N > 1 runs one process per GPU (torch.distributed.run, RCCL): each rank owns
-its own U utterances (weak scaling: fixed work per GPU) and the ranks
-all-reduce the 300x300 Gram once per step — the only collective on the path.
-Rank 0 prints ONE JSON line.
+N > 1 runs one process per GPU with RCCL: each rank owns its own U utterances
+(weak scaling: fixed work per GPU) and the ranks all-reduce the 300x300 fp64
+Gram once per step -- the only collective on the path.  Launched without a
+torchrun environment (no WORLD_SIZE), `--gpus N` starts the N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU)
+and exits with its status.  Rank 0 prints ONE JSON line.
+
+At N = 1 the line also carries `configs_measured` -- the other BASELINE
+configs measured in the same run: the ragged configs[3] variant (Poisson(40)
+lengths in [1, 64]), configs[2] (POM transcript length 1357),
+configs[4] (the regressor's 400-epoch SGD loop at MOSI size) -- plus the
+fp32-MFMA projection timed beside the bench path's fp16x3 one, and the CPU
+baselines.  `--only-main` skips them (profiling passes).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,26 +41,67 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 F16_MFMA_PEAK_TFS = 2500.0  # dense f16 MFMA (no sparsity)
+F32_MFMA_PEAK_TFS = 157.3  # f32-input MFMA (= the f32 vector rate on gfx950)
 F64_MFMA_PEAK_TFS = 78.6  # fp64 MFMA
+METRIC = "utterance-embeds/sec (MMB2, 3 modalities, 300d) at 1/2/4/8 MI355X"
+DTYPE = ("f32 (MMB2 projection: fp16 hi/lo x3 split on the f16 MFMA pipe, fp32 accumulate; "
+         "Gram / PC solve / removal fp64)")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def stream_kernel_bytes(L, D, A, Vd):
-    """Algorithmic HBM bytes per utterance of mmb_mm2_stream (DESIGN.md §4):
+def stream_kernel_bytes(L, D, A, Vd, text_rows=None):
+    """Algorithmic HBM bytes per utterance of mmb_mm2_stream (DESIGN.md §3.1):
     ids + gathered weights + gathered text rows + audio + visual frames (read),
-    weighted sum + frame sums + (count, sum w) (write)."""
-    return 4 * L + 4 * L + 4 * D * L + 4 * A * L + 4 * Vd * L + 4 * D + 4 * 2 * (D + A + Vd) + 8
+    a2 row + frame sums + (count, sum w) (write).  `text_rows` (mean per
+    utterance) overrides L for the text gather: SURVEY §8d counts id-0
+    pad/OOV rows once per utterance."""
+    tr = L if text_rows is None else text_rows
+    return 4 * L + 4 * L + 4 * D * tr + 4 * A * L + 4 * Vd * L + 4 * D + 4 * 2 * (D + A + Vd) + 8
 
 
-def path_bytes(L, D, A, Vd):
+def path_bytes(L, D, A, Vd, text_rows=None):
     """SURVEY.md §8d B_utt for the whole step (149,120 B at the config-3 shape)."""
-    return 4 * L + 4 * L + 4 * D * L + 2 * 4 * A * L + 3 * 4 * D + 4 * D
+    tr = L if text_rows is None else text_rows
+    return 4 * L + 4 * L + 4 * D * tr + 4 * (A + Vd) * L + 3 * 4 * D + 4 * D
 
 
-def cpu_baseline(inp, gen, n_sample):
+def host_threads():
+    """Host threads the CPU legs use: this process's CPU affinity, capped by an
+    OMP_NUM_THREADS the environment sets (the GPU box sets 16, its share of
+    a machine whose affinity lists every core)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    n = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return n, aff
+
+
+class cpu_threads:
+    """torch and BLAS thread pools set to `n` for a CPU leg, restored after."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        import torch
+        from threadpoolctl import threadpool_limits
+
+        self.prev = torch.get_num_threads()
+        torch.set_num_threads(self.n)
+        self.tp = threadpool_limits(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        import torch
+
+        self.tp.restore_original_limits()
+        torch.set_num_threads(self.prev)
+        return False
+
+
+def cpu_baseline(sample, gen, n_sample):
     """The oracle (CPU restatement of the reference loops + sklearn randomized SVD
     + the MMB2 closed form in fp32 numpy) timed on a bounded sample of the same
     workload, on this host's cores."""
@@ -58,29 +110,363 @@ def cpu_baseline(inp, gen, n_sample):
     from oracle import mmb2_oracle as M
     from oracle import sif_oracle as O
 
+    cores, aff = host_threads()
+    table, wt, ids, audio, visual = sample
+    params = M.params_from_module(gen)
+    with cpu_threads(cores):
+        t0 = time.perf_counter()
+        w = O.seq2weight_loop(ids, np.ones(ids.shape), wt)          # sif_functions.py:8-15
+        emb = O.get_weighted_average(table, ids, w)                  # :28-56
+        O.remove_pc(emb, 1)                                          # :58-81
+        text = table[ids]
+        M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual), params, w, text,
+                                          dtype=np.float32)          # sif2.py:164-208
+        dt = time.perf_counter() - t0
+    return {"value": round(n_sample / dt, 1), "unit": "utterance-embeds/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{n_sample} utterances of the same workload (L=T={ids.shape[1]}, 3x300-d, "
+                      f"V={table.shape[0]}), one pass of oracle/ (python row loops like the "
+                      f"reference, sklearn-equivalent randomized SVD, numpy BLAS)",
+            "threads": {"used": cores, "affinity": aff,
+                        "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")},
+            "sample_note": "bounded to ~10-20 s of host work so the default bench stays within "
+                           "minutes (SURVEY §8d suggests 100k utterances: ~2.5 min at this rate)",
+            "seconds": round(dt, 3)}
+
+
+def host_sample(inp, n):
+    """Copy the first n utterances of a device workload to the host (before
+    the device inputs are freed)."""
+    return (inp["table"].cpu().numpy(), inp["wtab"].double().cpu().numpy(),
+            inp["ids"][:n].long().cpu().numpy(), inp["audio"][:n].cpu().numpy(),
+            inp["visual"][:n].cpu().numpy())
+
+
+def phase_times(traces, steps):
+    names = sorted({n for tr in traces for n in tr})
+    return {n: sum(a.elapsed_time(b) for tr in traces for a, b in tr.get(n, ())) / steps
+            for n in names}
+
+
+def load_traffic(name, utts_per_launch, tokens):
+    """PMC-measured HBM bytes per stream-kernel launch for this exact workload,
+    from the committed rocprofv3 summaries (profiles/), never this run."""
+    fn = {"synthetic": "traffic_latest.json"}.get(name, f"traffic_{name}_latest.json")
+    path = os.path.join(ROOT, "profiles", fn)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        tj = json.load(f)
+    if tj.get("utts_per_launch") == utts_per_launch and tj.get("tokens") == tokens:
+        return tj.get("mm2_stream_hbm_bytes_per_launch"), f"profiles/{fn} ({tj.get('tag')})"
+    return None, None
+
+
+def run_workload(P, inp, gen, steps, warmup, allreduce=None, world=1, rank=0):
+    """FusedStep over `inp`: warmup, then `steps` timed steps bracketed by
+    barrier + synchronize.  Returns (step, elapsed_s, per-step traces)."""
+    import torch
+    import torch.distributed as dist
+
+    U = inp["ids"].shape[0]
+    step = P.FusedStep(inp, gen.networks(), allreduce=allreduce, n_total=U * world, row0=rank * U)
+    for _ in range(warmup):
+        step.run()
+    torch.cuda.synchronize()
+    traces = [dict() for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step.run(trace=traces[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    step.check()  # ids in range, no all-zero-weight utterance (one sync, after timing)
+    return step, elapsed, traces
+
+
+def stream_roofline(phase_ms, traces, steps, kbytes, U, kernel, traffic_key, T):
+    n_launch = sum(len(tr["mm2_stream"]) for tr in traces)
+    launch_ms = phase_ms["mm2_stream"] * steps / n_launch
+    achieved = kbytes * U / (launch_ms / 1e3) / 1e9
+    traffic, src = load_traffic(traffic_key, U, T)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": (f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE passes of this workload, "
+                               f"{src} -- not measured in this run" if traffic else
+                               "no PMC summary of this workload committed"),
+            "kernel": kernel, "algorithmic_bytes_per_utt": round(kbytes, 1),
+            "utts_per_launch": U, "avg_launch_ms": round(launch_ms, 4),
+            "timing": "HIP events on the launch stream around every stream-kernel launch"}
+
+
+def mfma_rooflines(step, phase_ms, U, D):
+    """MFMA-bound kernels of the step on UNPADDED (algorithmic) FLOPs: the
+    projection [U, 2(D+A+Vd)] x [.., D+1] as 3 fp16 products (hi/lo split; its
+    phase includes the fused PC-removal tail), the Gram's upper triangle in
+    fp64 (D(D+1)/2 dot products of U terms)."""
+    out = {}
+    k_alg = 2 * (step.d + step.a + step.vd)
+    proj_ms = phase_ms.get("mm2_project+pc_remove", phase_ms.get("mm2_project+gram"))
+    if proj_ms and step.s_half:
+        flop = 3 * 2 * k_alg * (D + 1)
+        tf = flop * U / (proj_ms / 1e3) / 1e12
+        out["mm2_project_x3b"] = {"bound": "mfma", "achieved": round(tf, 1),
+                                  "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                  "frac": round(tf / F16_MFMA_PEAK_TFS, 4), "flop_per_utt": flop,
+                                  "padded_flop_per_utt": 3 * 2 * step.proj.kp * step.proj.ldw,
+                                  "ms": round(proj_ms, 4), "includes": "fused PC-removal tail"}
+    if "gram" in phase_ms:
+        flop = D * (D + 1)  # 2 * D(D+1)/2 per row
+        tf = flop * U / (phase_ms["gram"] / 1e3) / 1e12
+        out["gram_tri (fp64)"] = {"bound": "mfma", "achieved": round(tf, 2),
+                                  "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                                  "frac": round(tf / F64_MFMA_PEAK_TFS, 4), "flop_per_utt": flop,
+                                  "ms": round(phase_ms["gram"], 4)}
+    return out
+
+
+def time_fp32_projection(P, step, reps=3):
+    """The fp32-MFMA projection (mmb_mm2_project) on the same sums, timed
+    beside the bench path's fp16x3 kernel: one extra stream pass writes s in
+    fp32, then `reps` projections (HIP events)."""
     import torch
 
-    cores = torch.get_num_threads()  # the BLAS/OpenMP threads actually used (OMP_NUM_THREADS)
-    n = n_sample
-    table = inp["table"].cpu().numpy()
-    wt = inp["wtab"].double().cpu().numpy()
-    ids = inp["ids"][:n].long().cpu().numpy()
-    audio = inp["audio"][:n].cpu().numpy()
-    visual = inp["visual"][:n].cpu().numpy()
-    params = M.params_from_module(gen)
-    t0 = time.perf_counter()
-    w = O.seq2weight_loop(ids, np.ones(ids.shape), wt)          # sif_functions.py:8-15
-    emb = O.get_weighted_average(table, ids, w)                  # :28-56
-    O.remove_pc(emb, 1)                                          # :58-81
-    text = table[ids]
-    M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual), params, w, text,
-                                      dtype=np.float32)          # sif2.py:164-208
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "utterance-embeds/s", "cores": cores, "kind": "port",
-            "sample": f"{n} utterances of the same workload (L=T={ids.shape[1]}, 3x300-d, "
-                      f"V={table.shape[0]}), one pass: oracle/ restatement (python row loops, "
-                      f"sklearn-equivalent randomized SVD, numpy BLAS on {cores} threads)",
-            "seconds": dt}
+    if not step.s_half:
+        return None
+    inp = step.inp
+    s32 = P.s_buffer(step.n, step.proj.kp, False, step.table.device)
+    x, aux = torch.empty_like(step.x), torch.empty((3, step.n), device=step.table.device)
+    P.mm2_stream(step.n, step.t, step.d, step.a, step.vd, inp["audio"], inp["visual"],
+                 ids32=step.ids, table=step.table, wtab32=inp["wtab"], s_half=False,
+                 out=(x, s32, aux))
+    out = torch.empty_like(step.mmb2)
+    P.mm2_project(s32, x, aux, step.proj, out=out)
+    evs = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        P.mm2_project(s32, x, aux, step.proj, out=out)
+        b.record()
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in evs) / reps
+    # the fp32 path's rows against the bench path's (both meet the 1e-5 bar in
+    # tests/test_gpu_mmb2.py::test_fp16_split_projection_vs_fp32_and_oracle)
+    diff = ((out - step.mmb2).abs().amax(1) / step.mmb2.abs().amax(1)).max().item()
+    flop = 2 * 2 * (step.d + step.a + step.vd) * (step.d + 1)
+    tf = flop * step.n / (ms / 1e3) / 1e12
+    del s32, x, aux, out
+    return {"ms": round(ms, 4), "achieved": round(tf, 1), "peak": F32_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TFS, 4),
+            "row_rel_diff_vs_fp16x3": diff,
+            "note": "mmb_mm2_project: fp32-input MFMA (exact f32 products), no fused removal"}
+
+
+def ragged_config(P, models, synth, dev, steps, warmup, U):
+    """SURVEY §8d's second configs[3] run: Poisson(40) lengths clipped to
+    [1, 64], padded with id 0 (weight 1.0) and -10 frames, T = 64."""
+    import torch
+
+    T, V, D = 64, 400_000, 300
+    inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=2000, device=dev,
+                                poisson_len=40.0)
+    lens = inp.pop("lengths")
+    ids = inp["ids"]
+    nz = (ids != 0).sum().item() / U
+    any0 = (ids == 0).any(1).float().mean().item()
+    mean_len = lens.float().mean().item()
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
+    step, elapsed, traces = run_workload(P, inp, gen, steps, warmup)
+    ph = phase_times(traces, steps)
+    kb = stream_kernel_bytes(T, D, 300, 300, text_rows=nz + any0)
+    roof = stream_roofline(ph, traces, steps, kb, U, "utt_wave_kernel (one wave per utterance, "
+                           "T = 64)", "ragged", T)
+    pb = path_bytes(T, D, 300, 300, text_rows=nz + any0)
+    out = {"workload": "configs[3] ragged: Poisson(40) lengths clipped to [1, 64], padded to 64 "
+                       "with id 0 (w0 = 1.0) and -10 frames, V = 400k, Zipf(1.1) ids, 3 x 300-d",
+           "utts": U, "tokens": T, "mean_len": round(mean_len, 3),
+           "value": round(U * steps / elapsed, 1), "unit": "utterance-embeds/s",
+           "ms_per_step": round(elapsed * 1e3 / steps, 4), "roofline": roof,
+           "path_roofline": {"bytes_per_utt": round(pb, 1),
+                             "achieved": round(pb * U / (elapsed / steps) / 1e9, 1),
+                             "unit": "GB/s", "peak": HBM_PEAK_GBS},
+           "phase_ms": {k: round(v, 4) for k, v in ph.items()},
+           "text_rows_per_utt": round(nz + any0, 3)}
+    del step, inp
+    return out
+
+
+def pom_config(P, models, synth, dev, steps, warmup, U=10_000):
+    """configs[2]: POM transcript length (padded to 1357 like pom_test_ids.npy,
+    ~370 tokens, V = 7763, w0 = 1.0), aligned 300-d frames."""
+    import torch
+
+    T, V, D = 1357, 7763, 300
+    inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=3000, device=dev,
+                                mean_len=370.0)
+    inp.pop("lengths", None)
+    ids = inp["ids"]
+    nz = (ids != 0).sum().item() / U
+    any0 = (ids == 0).any(1).float().mean().item()
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
+    step, elapsed, traces = run_workload(P, inp, gen, steps, warmup)
+    ph = phase_times(traces, steps)
+    # the workgroup kernel loads every token's row (pads and OOV hit one cached
+    # row); algorithmic bytes count the id-0 row once (SURVEY §8d)
+    kb = stream_kernel_bytes(T, D, 300, 300, text_rows=nz + any0)
+    roof = stream_roofline(ph, traces, steps, kb, U, "utt_stream_kernel (one 320-thread "
+                           "workgroup per utterance, 512-token LDS chunks)", "pom", T)
+    out = {"workload": "configs[2] POM-shaped: V = 7763, w0 = 1.0, transcripts padded to 1357 "
+                       "(~370 tokens), aligned 300-d audio/visual frames (-10 pads)",
+           "utts": U, "tokens": T, "value": round(U * steps / elapsed, 1),
+           "unit": "utterance-embeds/s", "ms_per_step": round(elapsed * 1e3 / steps, 4),
+           "roofline": roof, "phase_ms": {k: round(v, 4) for k, v in ph.items()},
+           "text_rows_per_utt": round(nz + any0, 3)}
+    del step, inp
+    return out
+
+
+def regressor_config(dev, cpu_epochs=40):
+    """configs[4]: the sentiment regressor's training loop at MOSI size
+    (1284 / 229 / 686 rows, H = 100, n_out = 1, batch 32, SGD lr 0.1, 400
+    epochs, validation every 10 epochs, sentiment_model.py:76-163) through the
+    product's train_sentiment, plus the pure kernel (all 16,400 SGD steps in one
+    mmb_mlp_train launch) and the CPU restatement on a sample of epochs."""
+    import contextlib
+    import io
+
+    import numpy as np
+    import torch
+    from torch.utils.data import DataLoader
+
+    import mmb_lib as L
+    import sentiment_model as SM
+    from oracle import regressor_oracle as R
+
+    sizes, H, epochs, B, lr = (1284, 229, 686), 100, 400, 32, 0.1
+    rng = np.random.default_rng(7)
+    lat = [(rng.standard_normal((n, 300)) / np.sqrt(300)).astype(np.float32) for n in sizes]
+    wp = rng.standard_normal(300).astype(np.float32) * 2
+    lab = [np.clip(l @ wp + 0.9 * rng.standard_normal(len(l)), -3, 3).astype(np.float32)
+           for l in lat]
+    args = {"sentiment_hidden_size": H, "n_sentiment_epochs": epochs, "sentiment_lr": lr,
+            "early_stopping": False, "dataset": "mosi", "lr_decay": 0.5}
+    steps = epochs * ((sizes[0] + B - 1) // B)
+
+    # (1) the product loop (host early-stopping logic, a validation + host sync
+    # every 10 epochs, mmb_mlp_train per block of epochs)
+    def product_run():
+        torch.manual_seed(11)
+        model = SM.SentimentModel(300, H, 1).to(dev)
+        tr = DataLoader(SM.SentimentData(lab[0], dev), batch_size=B, shuffle=True)
+        va = DataLoader(SM.SentimentData(lab[1], dev), batch_size=B, shuffle=True)
+        tl, vl = (torch.tensor(l, device=dev) for l in lat[:2])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):
+            SM.train_sentiment(args, model, tr, tl, va, vl, None)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    product_run()  # warm-up (module load, first launches)
+    t_prod = min(product_run() for _ in range(2))
+
+    # (2) the kernel alone: one launch, every step of the 400 epochs
+    torch.manual_seed(11)
+    model = SM.SentimentModel(300, H, 1).to(dev)
+    w1, b1, w2, b2 = (p.detach() for p in (model.hidden1.weight, model.hidden1.bias,
+                                             model.out.weight, model.out.bias))
+    x = torch.tensor(lat[0], device=dev)
+    y = torch.tensor(lab[0], device=dev).reshape(-1, 1).contiguous()
+    perm = torch.cat([torch.randperm(sizes[0]) for _ in range(epochs)]).to(dev)
+    sl = torch.empty(steps, device=dev)
+    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", 300, H) // 4 + 4, device=dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    L.call("mmb_mlp_train", L.ptr(x), L.ptr(y), L.ptr(perm), sizes[0], epochs, B, 300, H, 1,
+           float(lr), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(sl), L.ptr(ws),
+           L.stream_ptr())
+    b.record()
+    torch.cuda.synchronize()
+    k_ms = a.elapsed_time(b)
+    flop_step = 2 * B * 300 * H * 2 + 2 * B * H * 1 * 3  # fwd + dW1 GEMMs (+ the O=1 head)
+    tf = flop_step * steps / (k_ms / 1e3) / 1e12
+
+    # (3) the CPU restatement of the reference loop (torch CPU, its own RNG
+    # order), a sample of epochs
+    cores, aff = host_threads()
+    with cpu_threads(cores):
+        cargs = dict(args, n_sentiment_epochs=cpu_epochs)
+        torch.manual_seed(11)
+        m = R.Regressor(300, H, 1)
+        loaders = [DataLoader(R._Labels(l), batch_size=B, shuffle=True) for l in lab[:2]]
+        t0 = time.perf_counter()
+        R.train(cargs, m, loaders[0], torch.tensor(lat[0]), loaders[1], torch.tensor(lat[1]))
+        t_cpu = time.perf_counter() - t0
+    cpu_steps = cpu_epochs * ((sizes[0] + B - 1) // B)
+    return {"workload": "configs[4]: regressor 300 -> 100 -> 1 on MOSI-sized splits 1284 / 229 / "
+                        "686, batch 32, SGD lr 0.1, 400 epochs, validation every 10 epochs",
+            "steps": steps, "train_s": round(t_prod, 4),
+            "ms_per_step": round(t_prod * 1e3 / steps, 5),
+            "kernel": {"name": "mlp_train_kernel (mmb_mlp_train: every SGD step in one launch of "
+                               "one 16-wave workgroup)",
+                       "ms_400_epochs": round(k_ms, 3), "us_per_step": round(k_ms * 1e3 / steps, 3),
+                       "mfma": {"achieved": round(tf, 3), "peak": F32_MFMA_PEAK_TFS,
+                                "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TFS, 5),
+                                "flop_per_step": flop_step,
+                                "bound": "latency: 16,400 dependent SGD steps in sequence on "
+                                         "one workgroup (a 32 x 300 x 100 step is ~0.6 us of "
+                                         "one CU's MFMA time)"}},
+            "cpu_baseline": {"ms_per_step": round(t_cpu * 1e3 / cpu_steps, 4),
+                             "train_s_400_epochs_extrapolated": round(t_cpu * epochs / cpu_epochs, 2),
+                             "cores": cores, "kind": "port",
+                             "sample": f"{cpu_epochs} of 400 epochs of oracle/regressor_oracle.py "
+                                       f"(torch CPU, the reference's per-batch loop)"},
+            "speedup_vs_cpu": round((t_cpu / cpu_steps) / (t_prod / steps), 1)}
+
+
+def self_launch(n, argv):
+    """`bench.py --gpus N` outside torchrun: start N ranks as a child
+    torch.distributed.run (this process has not touched the GPU) and return
+    its exit status.  The ranks inherit this environment (incl.
+    HSA_ENABLE_IPC_MODE_LEGACY=0 for RCCL's dmabuf IPC)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"bench: launching {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check():
+    """--launch-check: every rank joins the process group (gloo without a
+    GPU) and all-reduces a one; rank 0 prints the ranks it saw."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "ranks_seen": world,
+                          "allreduce_sum": int(t.item()), "pid": os.getpid()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -88,9 +474,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="synthetic", choices=["synthetic", "pom"],
-                    help="synthetic: BASELINE configs[3] (the metric's workload); pom: "
-                         "configs[2] shape (V=7763, transcripts padded to 1357, ~370 tokens)")
+    ap.add_argument("--workload", default="synthetic", choices=["synthetic", "pom", "ragged"],
+                    help="synthetic: BASELINE configs[3] (the metric's workload); pom: configs[2] "
+                         "shape (V=7763, transcripts padded to 1357, ~370 tokens); ragged: "
+                         "configs[3] with Poisson(40) lengths in [1, 64]")
     ap.add_argument("--utts-per-gpu", type=int, default=None)
     ap.add_argument("--tokens", type=int, default=None)
     ap.add_argument("--vocab", type=int, default=None)
@@ -102,8 +489,24 @@ def main():
     ap.add_argument("--side-layout", default="balanced", choices=["balanced", "strided", "high"])
     ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--only-main", action="store_true",
+                    help="skip configs_measured (the other BASELINE configs) and the fp32 "
+                         "projection timing")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only start the ranks and all-reduce a one (tests the launcher)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if not args.launch_check:
+            import torch  # device_count() does not initialise the GPU
+
+            have = torch.cuda.device_count()
+            if have < args.gpus:
+                log(f"bench: --gpus {args.gpus} but only {have} GPU(s) visible")
+                return 2
+        return self_launch(args.gpus, sys.argv[1:])
+    if args.launch_check:
+        return launch_check()
 
     import torch
     import torch.distributed as dist
@@ -117,6 +520,12 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        ranks_seen = dist.get_world_size()
+        one = torch.ones(1, device=dev)
+        dist.all_reduce(one)  # every rank is live on RCCL before the timed steps
+        assert int(one.item()) == ranks_seen == world
+    else:
+        ranks_seen = 1
 
     import mmb_lib
     import models
@@ -124,35 +533,38 @@ def main():
     import synth
 
     mmb_lib.require_gpu()
-    pom = args.workload == "pom"
-    dflt = (10_000, 1357, 7763) if pom else (1_000_000, 40, 400_000)
+    kind = args.workload
+    dflt = {"synthetic": (1_000_000, 40, 400_000), "pom": (10_000, 1357, 7763),
+            "ragged": (1_000_000, 64, 400_000)}[kind]
     U = args.utts_per_gpu or dflt[0]
     T = args.tokens or dflt[1]
     V = args.vocab or dflt[2]
     D = 300
     inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev,
-                                mean_len=370.0 if pom else None)
+                                mean_len=370.0 if kind == "pom" else None,
+                                poisson_len=40.0 if kind == "ragged" else None)
+    inp.pop("lengths", None)
+    ids = inp["ids"]
+    text_rows = None
+    if kind != "synthetic":
+        text_rows = (ids != 0).sum().item() / U + (ids == 0).any(1).float().mean().item()
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
 
     def allreduce(t):
-        if world > 1:
-            dist.all_reduce(t)
+        dist.all_reduce(t)
 
+    assert U * world >= D  # sklearn's direct (non-transposed) randomized-SVD branch
     step = P.FusedStep(inp, gen.networks(), allreduce=allreduce if world > 1 else None,
                        n_total=U * world, row0=rank * U, chunks=args.chunks,
                        side_cus=args.side_cus, side_layout=args.side_layout)
     torch.cuda.synchronize()
-
     for _ in range(args.warmup):
         step.run()
     torch.cuda.synchronize()
 
     # timed region: K steps, barrier + sync on both sides.  HIP events are
-    # recorded on the stream each phase is launched on (FusedStep.run trace):
-    # the stream kernel's chunks on the caller's stream, projection + Gram of
-    # each chunk on the side stream they overlap on.
-    assert U * world >= D  # sklearn's direct (non-transposed) randomized-SVD branch
+    # recorded on the stream each phase is launched on (FusedStep.run trace).
     traces = [dict() for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -168,97 +580,92 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    if int(step.flag.item()) != 0:
-        raise RuntimeError("id range flag set")
+    step.check()  # ids in range, no all-zero-weight utterance, finite PC
 
-    names = sorted({n for tr in traces for n in tr})
-    phase_ms = {n: sum(a.elapsed_time(b) for tr in traces for a, b in tr.get(n, ()))
-                / args.steps for n in names}
-    n_launch = sum(len(tr["mm2_stream"]) for tr in traces)
-    stream_launch_ms = phase_ms["mm2_stream"] * args.steps / n_launch
+    phase_ms = phase_times(traces, args.steps)
     ms_per_step = elapsed * 1e3 / args.steps
-    total_utts = U * world * args.steps
-    value = total_utts / elapsed
+    value = U * world * args.steps / elapsed
+    if rank != 0:
+        dist.destroy_process_group()
+        return 0
 
-    if rank == 0:
-        kb = stream_kernel_bytes(T, D, 300, 300)
-        utts_per_launch = U / len(step.bounds)
-        achieved = kb * utts_per_launch / (stream_launch_ms / 1e3) / 1e9
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("utts_per_launch") == utts_per_launch and tj.get("tokens") == T:
-                traffic = tj.get("mm2_stream_hbm_bytes_per_launch")
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
-                           else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)"),
-                "algorithmic_bytes_per_utt": kb, "utts_per_launch": utts_per_launch,
-                "avg_launch_ms": round(stream_launch_ms, 4)}
-        # MFMA-bound kernels of the step, from their HIP-event phase times:
-        # the projection as 3 f16 GEMMs [U, kp] x [kp, ldw] (hi/lo split; its
-        # phase includes the fused PC-removal tail), the Gram as the 16x16
-        # upper-triangle tiles it computes in fp64
-        mfma = {}
-        kp, ldw = step.proj.kp, step.proj.ldw
-        proj_ms = phase_ms.get("mm2_project+pc_remove", phase_ms.get("mm2_project+gram"))
-        if proj_ms and step.s_half:
-            tf = 3 * 2 * kp * ldw * U / (proj_ms / 1e3) / 1e12
-            mfma["mm2_project_x3b"] = {"bound": "mfma", "achieved": round(tf, 1),
-                                       "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                                       "frac": round(tf / F16_MFMA_PEAK_TFS, 4),
-                                       "flop_per_utt": 3 * 2 * kp * ldw,
-                                       "includes": "fused PC-removal tail"}
-        if "gram" in phase_ms:
-            nt = (D + 15) // 16
-            gflop = nt * (nt + 1) // 2 * 16 * 16 * 2 * U
-            tf = gflop / (phase_ms["gram"] / 1e3) / 1e12
-            mfma["gram_tri (fp64)"] = {"bound": "mfma", "achieved": round(tf, 2),
-                                       "peak": F64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                                       "frac": round(tf / F64_MFMA_PEAK_TFS, 4),
-                                       "flop_per_utt": gflop // U}
-        pb = path_bytes(T, D, 300, 300)
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
+    utts_per_launch = U // len(step.bounds) if len(step.bounds) > 1 else U
+    kb = stream_kernel_bytes(T, D, 300, 300, text_rows=text_rows)
+    kname = ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
+             else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)")
+    roof = stream_roofline(phase_ms, traces, args.steps, kb, utts_per_launch, kname, kind, T)
+    pb = path_bytes(T, D, 300, 300, text_rows=text_rows)
+    mfma = mfma_rooflines(step, phase_ms, U, D)
+    wl = {"synthetic": "configs[3]: synthetic utterances x 40 tokens/frames x 3 modalities x "
+                       "300d, V = 400k, Zipf(1.1) ids, SIF(+PC removal) + closed-form MMB2",
+          "pom": "configs[2]: POM-shaped (V=7763, w0=1.0, transcripts padded to 1357, ~370 "
+                 "tokens, aligned frames) x 3 modalities x 300d, SIF(+PC removal) + MMB2",
+          "ragged": "configs[3] ragged: Poisson(40) lengths in [1, 64], padded with id 0 / -10 "
+                    "frames, 3 x 300d, V = 400k, SIF(+PC removal) + MMB2"}[kind]
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "utterance-embeds/s",
+        "n_gpus": world,
+        "ranks_seen": ranks_seen,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": DTYPE,
+        "data": "synthetic (seeded, generated in HBM; no dataset or checkpoint)",
+        "config": {"workload": wl, "utts_per_gpu": U, "tokens": T, "vocab": V,
+                   "dims": [D, 300, 300],
+                   "parallelism": f"dp{world} (utterance shards) + RCCL all-reduce of the "
+                                  f"300x300 fp64 Gram"},
+        "roofline": roof,
+        "path_roofline": {"bytes_per_utt": round(pb, 1),
+                          "achieved": round(pb * U / (ms_per_step / 1e3) / 1e9, 1),
+                          "unit": "GB/s per GPU", "peak": HBM_PEAK_GBS,
+                          "frac": round(pb * U / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
+        "mfma_rooflines": mfma,
+        "chunks": len(step.bounds),
+    }
+    if world > 1:
+        out["phase_ms"].setdefault("allreduce", None)
+    cpu = None
+    extras = world == 1 and not args.only_main and kind == "synthetic"
+    if extras:
+        out["projection_fp32_mfma"] = time_fp32_projection(P, step)
+    sample = None
+    if not args.no_cpu_baseline and world == 1:
+        n_cpu = args.cpu_sample if T <= 64 else max(1, args.cpu_sample * 40 // T)
+        sample = host_sample(inp, n_cpu)
+    gen_cpu = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None)
+    gen_cpu.load_state_dict({k: v.cpu() for k, v in gen.state_dict().items()})
+    del step, inp, ids
+    torch.cuda.empty_cache()
+    if extras:
+        cm = {}
+        for name, fn in (("ragged", lambda: ragged_config(P, models, synth, dev, 5, 2, U)),
+                         ("pom", lambda: pom_config(P, models, synth, dev, 5, 2)),
+                         ("regressor", lambda: regressor_config(dev))):
             try:
-                n_cpu = args.cpu_sample if not pom else max(1, args.cpu_sample * 40 // T)
-                cpu = cpu_baseline(inp, gen.cpu(), n_cpu)
-            except Exception as exc:  # keep the GPU line even if the host leg fails
-                log(f"cpu baseline failed: {exc!r}")
-        out = {
-            "metric": "utterance-embeds/sec (MMB2, 3 modalities, 300d) at 1/2/4/8 MI355X",
-            "value": round(value, 1),
-            "unit": "utterance-embeds/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded, generated in HBM; no dataset or checkpoint)",
-            "config": {"workload": ("configs[2]: POM-shaped (V=7763, w0=1.0, transcripts padded "
-                                    "to 1357, ~370 tokens, aligned frames) x 3 modalities x 300d, "
-                                    "SIF(+PC removal) + closed-form MMB2" if pom else
-                                    "configs[3]: synthetic utterances x 40 tokens/frames x 3 "
-                                    "modalities x 300d, SIF(+PC removal) + closed-form MMB2"),
-                       "utts_per_gpu": U, "tokens": T, "vocab": V, "dims": [D, 300, 300],
-                       "parallelism": f"dp{world} (utterance shards) + RCCL all-reduce of the "
-                                      f"300x300 fp64 Gram"},
-            "roofline": roof,
-            "path_roofline": {"bytes_per_utt": pb, "achieved": round(pb * U * world / (ms_per_step / 1e3) / world / 1e9, 1),
-                              "unit": "GB/s per GPU", "peak": HBM_PEAK_GBS},
-            "phase_ms": {k: round(v, 4) for k, v in phase_ms.items()},
-            "mfma_rooflines": mfma,
-            "chunks": len(step.bounds),
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
+                cm[name] = fn()
+            except Exception as exc:  # keep the headline line even if an extra leg fails
+                log(f"configs_measured.{name} failed: {exc!r}")
+                cm[name] = {"error": repr(exc)}
+            torch.cuda.empty_cache()
+        out["configs_measured"] = cm
+    if sample is not None:
+        try:
+            cpu = cpu_baseline(sample, gen_cpu, sample[2].shape[0])
+        except Exception as exc:  # keep the GPU line even if the host leg fails
+            log(f"cpu baseline failed: {exc!r}")
+    out["cpu_baseline"] = cpu
+    print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -18,7 +18,8 @@
  *     positive hipError_t from the launch;
  *   - `flag` (nullable) is an int32 device word OR-ed with MMB_FLAG_* bits by
  *     kernels that meet out-of-range ids (the shim raises IndexError, like
- *     numpy would in the reference).
+ *     numpy would in the reference) or all-zero-weight utterances (the shim
+ *     raises ValueError where the reference's PC step would).
  */
 #ifndef MMB_H_
 #define MMB_H_
@@ -33,6 +34,9 @@ extern "C" {
 #define MMB_OK 0
 #define MMB_EINVAL (-1)
 #define MMB_FLAG_ID_RANGE 1
+/* an utterance whose SIF weights are all 0 (its a2 row is 0/0 = NaN, like
+ * numpy's; the reference's TruncatedSVD then raises ValueError on the split) */
+#define MMB_FLAG_ZERO_WEIGHTS 2
 
 /* Library version (major*10000 + minor*100 + patch). */
 int mmb_version(void);
@@ -104,6 +108,19 @@ int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n
  * replaces: sif_functions.remove_pc /root/reference/sif_functions.py:69-81 */
 int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int d, const double* pc,
                   int npc, float* out32, double* out64, hipStream_t stream);
+
+/* float64 X (the numpy drop-ins' general input, when it is not
+ * f32-representable): the same Gram (fp64 MFMA, 64x64 blocks), start block
+ * X^T Omega and f64 removal reading f64 rows, so compute_pc / remove_pc do not
+ * round X to f32 first.  ws as for mmb_gram_workspace_bytes(n, d).
+ * replaces: sif_functions.compute_pc / remove_pc on float64 input
+ *   /root/reference/sif_functions.py:58-81                                   */
+int mmb_gram_f64(const double* x, int64_t n, int d, double* g, int accumulate, void* ws,
+                 hipStream_t stream);
+int mmb_xt_omega_f64(const double* x, int64_t n, int d, const double* omega, int k, double* z0,
+                     hipStream_t stream);
+int mmb_pc_remove_f64(const double* x, int64_t n, int d, const double* pc, int npc,
+                      double* out64, hipStream_t stream);
 
 /* Streams restricted to a subset of the CUs (hipExtStreamCreateWithCUMask):
  * bit i of cu_mask[i / 32] enables CU i.  Used to run the HBM-bound stream

@@ -33,11 +33,17 @@ __device__ __forceinline__ float load_x(const float* __restrict__ num, const flo
   const float v = num[row * D + col];
   return cnt ? v / cnt[row] : v;  // x = num / count_nonzero(w), f32 (sif_functions.py:55)
 }
+// float64 rows (the numpy drop-in's general f64 X, sif_functions.py:58-81): no count
+__device__ __forceinline__ double load_x(const double* __restrict__ num, const float* __restrict__,
+                                         int64_t row, int col, int D) {
+  return col < D ? num[row * D + col] : 0.0;
+}
 
 // One workgroup: a 64x64 block (bp,bq), bp<=bq, of G over one chunk of rows.
 // fp64 MFMA 16x16x4: lane l holds A[l&15][l>>4] and B[l>>4][l&15]; with
 // A = X^T and B = X both fragments are 16 consecutive columns of 4 rows of X.
-__global__ __launch_bounds__(256) void gram_partial_kernel(const float* __restrict__ num,
+template <typename TX>
+__global__ __launch_bounds__(256) void gram_partial_kernel(const TX* __restrict__ num,
                                                            const float* __restrict__ cnt,
                                                            int64_t N, int D, int nb, int npairs,
                                                            int S, int64_t chunk, int xcd_map,
@@ -276,7 +282,8 @@ __global__ void gram_reduce_kernel(const double* __restrict__ part, int D, int n
   }
 }
 
-__global__ void xt_omega_kernel(const float* __restrict__ num, const float* __restrict__ cnt,
+template <typename TX>
+__global__ void xt_omega_kernel(const TX* __restrict__ num, const float* __restrict__ cnt,
                                 int64_t N, int D, const double* __restrict__ om, int k,
                                 double* __restrict__ z0) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1100,8 +1107,8 @@ inline size_t p16_lds_bytes(int d) {
 }
 
 // ------------------------------------------------------------------ pc_remove
-template <int VEC, int PER>
-__global__ __launch_bounds__(256) void pc_remove_kernel(const float* __restrict__ num,
+template <int VEC, int PER, typename TX = float>
+__global__ __launch_bounds__(256) void pc_remove_kernel(const TX* __restrict__ num,
                                                         const float* __restrict__ cnt, int64_t N,
                                                         int D, const double* __restrict__ pc,
                                                         int npc, float* __restrict__ out32,
@@ -1119,7 +1126,7 @@ __global__ __launch_bounds__(256) void pc_remove_kernel(const float* __restrict_
 #pragma unroll
     for (int m = 0; m < PER; ++m) {
       const int u = lane + kWave * m;
-      float v[VEC];
+      TX v[VEC];
       if (u < U) {
         if constexpr (VEC == 4) {
           const float4 q = *reinterpret_cast<const float4*>(num + row * D + u * 4);
@@ -1129,7 +1136,7 @@ __global__ __launch_bounds__(256) void pc_remove_kernel(const float* __restrict_
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) v[e] = 0.f;
+        for (int e = 0; e < VEC; ++e) v[e] = TX(0);
       }
 #pragma unroll
       for (int e = 0; e < VEC; ++e) x[m][e] = static_cast<double>(cnt ? v[e] / sc : v[e]);
@@ -1184,12 +1191,12 @@ __global__ __launch_bounds__(256) void pc_remove_kernel(const float* __restrict_
   }
 }
 
-template <int VEC, int PER>
-static int launch_remove(const float* num, const float* cnt, int64_t n, int d, const double* pc,
+template <int VEC, int PER, typename TX = float>
+static int launch_remove(const TX* num, const float* cnt, int64_t n, int d, const double* pc,
                          int npc, float* out32, double* out64, hipStream_t stream) {
   const int64_t waves = ceil_div(n, 1);
   const int grid = static_cast<int>(std::min<int64_t>(ceil_div(waves, 4), 256 * 8));
-  pc_remove_kernel<VEC, PER><<<grid, 256, sizeof(double) * npc * d, stream>>>(num, cnt, n, d, pc, npc, out32, out64);
+  pc_remove_kernel<VEC, PER, TX><<<grid, 256, sizeof(double) * npc * d, stream>>>(num, cnt, n, d, pc, npc, out32, out64);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1280,7 +1287,7 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
     return MMB_OK;
   }
   const GramPlan p = gram_plan(n, d);
-  gram_partial_kernel<<<p.npairs * p.S, 256, 0, stream>>>(num, cnt, n, d, p.nb, p.npairs, p.S,
+  gram_partial_kernel<float><<<p.npairs * p.S, 256, 0, stream>>>(num, cnt, n, d, p.nb, p.npairs, p.S,
                                                          p.chunk, p.xcd, part);
   MMB_LAUNCH_CHECK();
   gram_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, p.nb, p.npairs, p.S, accumulate, g);
@@ -1313,7 +1320,7 @@ extern "C" int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate,
 extern "C" int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d,
                             const double* omega, int k, double* z0, hipStream_t stream) {
   MMB_REQUIRE(num && omega && z0 && n >= 0 && d > 0 && k > 0);
-  xt_omega_kernel<<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
+  xt_omega_kernel<float><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1359,5 +1366,46 @@ extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int 
     if (per <= 4) return launch_remove<1, 4>(num, cnt, n, d, pc, npc, out32, out64, stream);
     if (per <= 8) return launch_remove<1, 8>(num, cnt, n, d, pc, npc, out32, out64, stream);
   }
+  return MMB_EINVAL;
+}
+
+// ------------------------------------------------------------------ float64 X
+// The numpy drop-ins (compute_pc / remove_pc) take any X; the reference runs
+// randomized SVD and the removal on it in f64 (sif_functions.py:58-81).  X
+// that is not f32-representable takes these entry points instead of being
+// rounded: the generic 64x64-block fp64-MFMA Gram, X^T Omega, and the f64
+// removal, all reading the f64 rows.
+extern "C" int mmb_gram_f64(const double* x, int64_t n, int d, double* g, int accumulate, void* ws,
+                            hipStream_t stream) {
+  MMB_REQUIRE(x && g && ws && n >= 0 && d > 0);
+  const GramPlan p = gram_plan(n, d);
+  const int64_t total = static_cast<int64_t>(d) * d;
+  double* part = static_cast<double*>(ws);
+  gram_partial_kernel<double><<<p.npairs * p.S, 256, 0, stream>>>(x, nullptr, n, d, p.nb, p.npairs,
+                                                                  p.S, p.chunk, p.xcd, part);
+  MMB_LAUNCH_CHECK();
+  gram_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, p.nb, p.npairs, p.S, accumulate, g);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_xt_omega_f64(const double* x, int64_t n, int d, const double* omega, int k,
+                                double* z0, hipStream_t stream) {
+  MMB_REQUIRE(x && omega && z0 && n >= 0 && d > 0 && k > 0);
+  xt_omega_kernel<double><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(
+      x, nullptr, n, d, omega, k, z0);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_pc_remove_f64(const double* x, int64_t n, int d, const double* pc, int npc,
+                                 double* out64, hipStream_t stream) {
+  MMB_REQUIRE(x && pc && out64 && n >= 0 && d > 0 && npc >= 1);
+  MMB_REQUIRE(static_cast<size_t>(npc) * d * sizeof(double) <= 64 * 1024);
+  if (n == 0) return MMB_OK;
+  const int per = static_cast<int>(ceil_div(d, kWave));
+  if (per <= 2) return launch_remove<1, 2, double>(x, nullptr, n, d, pc, npc, nullptr, out64, stream);
+  if (per <= 4) return launch_remove<1, 4, double>(x, nullptr, n, d, pc, npc, nullptr, out64, stream);
+  if (per <= 8) return launch_remove<1, 8, double>(x, nullptr, n, d, pc, npc, nullptr, out64, stream);
   return MMB_EINVAL;
 }

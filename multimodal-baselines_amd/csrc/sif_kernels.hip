@@ -263,6 +263,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       }
     }
     if (tid == 0) {
+      if (cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
       if constexpr (MM2) {
         a.aux_out[i] = cnt;         // planar [3][N]: row 0 doubles as the SIF count
         a.aux_out[a.N + i] = sw;
@@ -418,6 +419,9 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
     }
     const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
     const float sw = wave_sum(w);
+    // every weight 0: x is 0/0 = NaN (numpy's answer); the reference's
+    // TruncatedSVD then rejects the split -- report it through the flag word
+    if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
 
     float4 num[CT], sx[CT], sxx[CT], sa[CA], saa[CA], sv[CV], svv[CV];
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);

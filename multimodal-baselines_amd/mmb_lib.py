@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmmb.so")
 
 MMB_FLAG_ID_RANGE = 1
+MMB_FLAG_ZERO_WEIGHTS = 2
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -40,6 +41,9 @@ SIGNATURES = {
     "mmb_xt_omega": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
     "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "mmb_pc_remove": (_I, [_P, _P, _L, _I, _P, _I, _P, _P, _P]),
+    "mmb_gram_f64": (_I, [_P, _L, _I, _P, _I, _P, _P]),
+    "mmb_xt_omega_f64": (_I, [_P, _L, _I, _P, _I, _P, _P]),
+    "mmb_pc_remove_f64": (_I, [_P, _L, _I, _P, _I, _P, _P]),
     "mmb_host_randn": (_I, [ctypes.c_uint32, _L, _P]),
     "mmb_cu_count": (_I, [_I, _P]),
     "mmb_stream_create_cu_mask": (_I, [_P, _I, _P]),

@@ -51,9 +51,28 @@ def narrow_ids(ids: torch.Tensor) -> torch.Tensor:
     return ids.to(torch.int32).contiguous()
 
 
-def check_flag(flag: torch.Tensor, V: int):
-    if int(flag.item()) & L.MMB_FLAG_ID_RANGE:
+MAX_NPC = 16 - N_OVERSAMPLES  # the device solver keeps the k = npc + 10 block in 16 columns
+
+
+def check_npc(npc: int):
+    if not 1 <= npc <= MAX_NPC:
+        raise ValueError(f"npc={npc}: the device PC solver supports 1 <= npc <= {MAX_NPC} "
+                         f"(randomized-SVD block npc + {N_OVERSAMPLES} <= 16 columns)")
+
+
+def check_flag(flag: torch.Tensor, V: int, zero_weights: bool = False):
+    """Raise like the reference for what the kernels reported in `flag`:
+    IndexError for an id >= V (numpy fancy indexing); with `zero_weights`,
+    ValueError for an utterance whose weights are all 0 -- its a2 row is
+    0/0 = NaN (sif_functions.py:55) and the reference's TruncatedSVD rejects
+    the split (sklearn check_array: "Input X contains NaN")."""
+    f = int(flag.item())
+    if f & L.MMB_FLAG_ID_RANGE:
         raise IndexError(f"token id out of bounds for a vocabulary of size {V}")
+    if zero_weights and f & L.MMB_FLAG_ZERO_WEIGHTS:
+        raise ValueError("Input X contains NaN: an utterance whose SIF weights are all 0 has a "
+                         "0/0 weighted average (sif_functions.py:55), which the reference's "
+                         "TruncatedSVD rejects (sif_functions.py:65-67)")
 
 
 # ------------------------------------------------------------------ a1
@@ -124,6 +143,7 @@ def pc_start_block(n_total: int, d: int, npc: int, device, num=None, cnt=None, r
                    n_total_rows_omega: int | None = None):
     """Z0 of sklearn's randomized SVD.  Direct branch: Omega [d,k].  Transposed
     branch (n_total < d): X^T Omega_n for this shard's rows [row0, row0+n)."""
+    check_npc(npc)
     k = npc + N_OVERSAMPLES
     if n_total >= d:
         return omega(d, k, device), False
@@ -153,6 +173,33 @@ def remove_pc(num, cnt, pc: torch.Tensor, out_dtype=torch.float32, out=None) -> 
     return out
 
 
+# ------------------------------------------------------------------ a3/a4 on float64 X
+def pc_f64(x64: torch.Tensor, npc: int) -> torch.Tensor:
+    """PC of a float64 X [n, d] that is not f32-representable (the numpy
+    drop-ins' general input): Gram, start block and solve all read f64 rows."""
+    check_npc(npc)
+    n, d = x64.shape
+    k = npc + N_OVERSAMPLES
+    G = torch.empty((d, d), dtype=torch.float64, device=x64.device)
+    ws = GramWorkspace(n, d, x64.device)
+    L.call("mmb_gram_f64", L.ptr(x64), n, d, L.ptr(G), 0, L.ptr(ws.buf), L.stream_ptr())
+    if n >= d:
+        z0, transposed = omega(d, k, x64.device), False
+    else:
+        z0, transposed = torch.empty((d, k), dtype=torch.float64, device=x64.device), True
+        L.call("mmb_xt_omega_f64", L.ptr(x64), n, d, L.ptr(omega(n, k, x64.device)), k,
+               L.ptr(z0), L.stream_ptr())
+    return pc_solve(G, z0, npc, transposed)
+
+
+def remove_pc_f64(x64: torch.Tensor, pc: torch.Tensor) -> torch.Tensor:
+    n, d = x64.shape
+    out = torch.empty((n, d), dtype=torch.float64, device=x64.device)
+    L.call("mmb_pc_remove_f64", L.ptr(x64), n, d, L.ptr(pc), pc.shape[0], L.ptr(out),
+           L.stream_ptr())
+    return out
+
+
 class DeviceOps:
     """The libmmb kernels global_pc() composes (tests substitute CPU doubles)."""
 
@@ -173,6 +220,7 @@ def global_pc(num, cnt, npc: int, n_total: int, row0: int = 0, allreduce=None, o
     deterministic solve, so the PC is identical everywhere with no broadcast.
     """
     n, d = num.shape
+    check_npc(npc)
     k = npc + N_OVERSAMPLES
     G = ops.gram(num, cnt, G, ws)
     if n_total >= d:
@@ -192,14 +240,26 @@ def sif_embeddings(table, ids, wtab32=None, w=None, npc: int = 1, out_dtype=torc
     """a1-a5 fused on device: weighted average, Gram (+ optional all-reduce
     across ranks), randomized-SVD PC, removal.  Returns (emb [N,D], pc)."""
     ids32 = narrow_ids(ids)
-    flag = torch.zeros(1, dtype=torch.int32, device=table.device) if check_ids else None
+    flag = torch.zeros(1, dtype=torch.int32, device=table.device)
     num, cnt = weighted_sum(table, ids32, w=w, wtab32=wtab32, flag=flag)
     n_total = num.shape[0] if n_total is None else n_total
     pc = global_pc(num, cnt, npc, n_total, row0, allreduce)
     out = remove_pc(num, cnt, pc, out_dtype)
-    if check_ids:
-        check_flag(flag, table.shape[0])
+    if not check_ids:  # the id-range bit is then not the caller's concern
+        flag.bitwise_and_(~L.MMB_FLAG_ID_RANGE)
+    check_flag(flag, table.shape[0], zero_weights=True)
+    check_pc_finite(pc)
     return out, pc
+
+
+def check_pc_finite(pc: torch.Tensor):
+    """A NaN row on ANY rank reaches every rank's PC through the Gram
+    all-reduce: checking the PC makes every rank raise, not only the one that
+    holds the row."""
+    if not bool(torch.isfinite(pc).all()):
+        raise ValueError("Input X contains NaN or infinity: the split's Gram is not finite "
+                         "(an all-zero-weight utterance on some rank, or non-finite inputs), "
+                         "which the reference's TruncatedSVD rejects (sif_functions.py:65-67)")
 
 
 # ------------------------------------------------------------------ a7 / a8
@@ -412,6 +472,7 @@ class FusedStep:
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
+        check_npc(npc)
         self.npc = npc
         self.allreduce = allreduce
         self.n_total = self.n if n_total is None else n_total
@@ -443,6 +504,18 @@ class FusedStep:
             main_set = [c for c in range(n_cu) if c not in set(side_set)]
             self._cu_streams = [L.CUStream(main_set, dev), L.CUStream(side_set, dev)]
             self.main, self.side = self._cu_streams[0].torch, self._cu_streams[1].torch
+
+    def check(self):
+        """Raise what the reference would have raised for the last step(s):
+        IndexError for a token id >= V, ValueError for an utterance whose SIF
+        weights are all 0 (the PC step of the split is then undefined).  Reads
+        the flag word (one device sync); the flag accumulates until `reset()`."""
+        check_flag(self.flag, self.V, zero_weights=True)
+        if getattr(self, "pc", None) is not None:
+            check_pc_finite(self.pc)
+
+    def reset(self):
+        self.flag.zero_()
 
     def aux_of(self, c: int) -> torch.Tensor:
         r0, r1 = self.bounds[c]

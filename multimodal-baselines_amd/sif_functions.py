@@ -11,8 +11,12 @@ arithmetic runs on the GPU through libmmb (no CPU fallback):
 * SIF_embedding         -> all of it fused on device, one upload/download (:84-96)
 
 Numerics: rows are reduced in fp32 like the reference's f32 sgemv (an f64 word
-table is rounded to f32 first); X enters the PC step as fp32 values (exactly
-what get_weighted_average produces), the Gram and the solve are fp64.
+table is rounded to f32 first).  compute_pc / remove_pc take X as given: when X
+is f32-representable (what get_weighted_average produces) it enters the f32-row
+kernels exactly; any other float64 X takes the f64-row kernels (mmb_gram_f64,
+mmb_pc_remove_f64), so it is never rounded.  The Gram, the solve and the
+removal are fp64.  Non-finite X raises ValueError like sklearn's check_array in
+the reference's TruncatedSVD.
 """
 from __future__ import annotations
 
@@ -77,11 +81,22 @@ def get_weighted_average(We, x, w):
 
 
 def _x_device(X, dev):
+    """X on the device: f32 rows when X is f32-representable, else f64 rows."""
     X = np.asarray(X)
-    return torch.as_tensor(np.ascontiguousarray(X.astype(np.float32))).to(dev)
+    if X.ndim != 2:
+        raise ValueError(f"Expected 2D array, got {X.ndim}D array instead")
+    if X.dtype.kind == "f" and not np.isfinite(X).all():
+        raise ValueError("Input X contains NaN." if np.isnan(X).any() else
+                         f"Input X contains infinity or a value too large for {X.dtype!r}.")
+    x32 = X.astype(np.float32)
+    if X.dtype == np.float32 or np.array_equal(x32.astype(X.dtype), X):
+        return torch.as_tensor(np.ascontiguousarray(x32)).to(dev)
+    return torch.as_tensor(np.ascontiguousarray(X.astype(np.float64))).to(dev)
 
 
 def _pc_device(x, npc):
+    if x.dtype == torch.float64:
+        return P.pc_f64(x, npc)
     G = P.gram(x, None)
     z0, transposed = P.pc_start_block(x.shape[0], x.shape[1], npc, x.device, x, None)
     return P.pc_solve(G, z0, npc, transposed)
@@ -97,6 +112,8 @@ def remove_pc(X, npc=1):
     """XX = X - X pc^T pc, float64."""
     x = _x_device(X, _dev())
     pc = _pc_device(x, npc)
+    if x.dtype == torch.float64:
+        return P.remove_pc_f64(x, pc).cpu().numpy()
     return P.remove_pc(x, None, pc, torch.float64).cpu().numpy()
 
 

@@ -79,12 +79,17 @@ def frames(N: int, T: int, F: int, seed: int = 0, pad_frac: float = 0.0) -> np.n
 # ---------------------------------------------------------------- device side
 def device_workload(N: int, T: int, V: int, D: int = 300, A: int = 300, Vd: int = 300,
                     seed: int = 0, device="cuda", s: float = 1.1, w0: float = 1.0,
-                    mean_len: float | None = None):
+                    mean_len: float | None = None, poisson_len: float | None = None):
     """Config-3 workload generated directly in device memory (torch RNG).
 
     Returns dict of device tensors: table [V,D] f32, wtab [V] f32 (the f32
     rounding of the f64 SIF weights, as `simplesif.py:315` does), ids [N,T]
     int32, audio [N,T,A] f32, visual [N,T,Vd] f32.
+
+    Ragged variants (pad tokens id 0, pad frames -10, utils.py:188-189):
+    `mean_len` -- POM-like lengths ~ N(mean, mean/1.5) clipped to [1, T];
+    `poisson_len` -- SURVEY §8d's second configs[3] run, Poisson(mean) lengths
+    clipped to [1, T] (T = 64 there).  The result then also holds `lengths` [N].
     """
     import torch
 
@@ -109,17 +114,26 @@ def device_workload(N: int, T: int, V: int, D: int = 300, A: int = 300, Vd: int 
     visual = torch.empty(N, T, Vd, device=device, dtype=torch.float32)
     audio.uniform_(-1.0, 1.0, generator=gen)
     visual.uniform_(-1.0, 1.0, generator=gen)
+    out = {"table": table, "wtab": wtab, "ids": ids, "audio": audio, "visual": visual}
+    lens = None
     if mean_len is not None:
         # ragged transcripts padded to T (POM: 370 / 325 mean non-pad ids of 1089 /
         # 1357): lengths ~ N(mean, mean/1.5) clipped to [1, T]; pad
         # tokens are id 0 (weight w0, counted like the reference) and pad frames -10
         lens = (torch.randn(N, generator=gen, device=device) * (mean_len / 1.5) + mean_len)
         lens = lens.round().clamp_(1, T).to(torch.int64)
-        pad = torch.arange(T, device=device)[None, :] >= lens[:, None]
-        ids.masked_fill_(pad, 0)
-        audio.masked_fill_(pad[:, :, None], -10.0)
-        visual.masked_fill_(pad[:, :, None], -10.0)
-    return {"table": table, "wtab": wtab, "ids": ids, "audio": audio, "visual": visual}
+    elif poisson_len is not None:
+        rate = torch.full((N,), float(poisson_len), device=device)
+        lens = torch.poisson(rate, generator=gen).clamp_(1, T).to(torch.int64)
+    if lens is not None:
+        for o in range(0, N, 1 << 16):  # bounded temporaries
+            sl = slice(o, min(N, o + (1 << 16)))
+            pad = torch.arange(T, device=device)[None, :] >= lens[sl, None]
+            ids[sl].masked_fill_(pad, 0)
+            audio[sl].masked_fill_(pad[:, :, None], -10.0)
+            visual[sl].masked_fill_(pad[:, :, None], -10.0)
+        out["lengths"] = lens
+    return out
 
 
 # ---------------------------------------------------------------- CLI datasets

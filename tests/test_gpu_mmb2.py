@@ -262,12 +262,12 @@ def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
     assert M.row_rel_err(s4.cpu().numpy(), s1.cpu().numpy()) < 1e-6
 
 
-def test_zero_weight_rows_sif_nan_mmb2_finite(gpu):
+def test_zero_weight_rows_sif_raises_mmb2_finite(gpu):
     """A row whose SIF weights are all zero: its a2 row is 0/0 = NaN (numpy,
-    sif_functions.py:55; the reference's TruncatedSVD then rejects the split,
-    here the NaN reaches the Gram and every SIF row), while its MMB2
-    embedding is finite -- the text term is 0 (sif2.py:196-201) -- and every
-    MMB2 row matches the oracle."""
+    sif_functions.py:55) and the reference's TruncatedSVD rejects the split
+    with a ValueError -- FusedStep.check() raises the same -- while its MMB2
+    embedding is finite (the text term is 0, sif2.py:196-201) and every MMB2
+    row matches the oracle."""
     from oracle import sif_oracle as O
 
     N, T, A, Vd, V = 600, 40, 300, 300, 5000
@@ -285,6 +285,8 @@ def test_zero_weight_rows_sif_nan_mmb2_finite(gpu):
               "audio": torch.tensor(audio, device=gpu), "visual": torch.tensor(visual, device=gpu)}
     step = P.FusedStep(inputs, gen.to(gpu).networks())
     sif_out, mm2_out = [t.cpu().numpy() for t in step.run()]
+    with pytest.raises(ValueError, match="NaN"):
+        step.check()
     x = step.x.cpu().numpy()
     assert np.isnan(x[7]).all() and np.isfinite(np.delete(x, 7, 0)).all()
     sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
@@ -333,3 +335,114 @@ def test_non_default_kernel_variants_agree(gpu, tmp_path, env):
     # order (the 32x32x16 kernel's tail reduces with shuffles, not DPP)
     assert M.row_rel_err(z["sif"], s.cpu().numpy()) < 1e-6
     assert M.row_rel_err(z["mmb2"], m.cpu().numpy()) < TOL
+
+
+def _pom_case(golden, case, n, A, Vd, seed):
+    """Real POM transcript ids (pom_valid_ids 1089 / pom_test_ids 1357 wide,
+    interior id-0 OOV tokens, trailing id-0 padding) + the real POM weights
+    (w[0] = 1.0) from the g1 fixtures, the seeded V = 7763 table, and
+    word-aligned U(-1, 1) frames set to -10 after each transcript's last token
+    (the normalised pad value, utils.py:188-189)."""
+    z = golden(case)
+    ids = z["ids"][:n]
+    N, T = ids.shape
+    E = synth.word_table(int(z["V"]), 300, seed=int(z["table_seed"]))
+    last = np.where(ids != 0, np.arange(T)[None, :], -1).max(1)
+    pad = np.arange(T)[None, :] > last[:, None]
+    audio = synth.frames(N, T, A, seed=seed)
+    visual = synth.frames(N, T, Vd, seed=seed + 1)
+    audio[pad] = -10.0
+    visual[pad] = -10.0
+    return E, z["weights"], ids, audio, visual
+
+
+@pytest.mark.parametrize("case,n,A,Vd", [("g1_pom_valid", 32, 300, 300),
+                                         ("g1_pom_test", 24, 300, 300),
+                                         ("g1_pom_test", 48, 46, 37)])
+def test_fused_step_pom_length_vs_oracle(gpu, golden, case, n, A, Vd):
+    """BASELINE configs[2]: the bench step (SIF + PC removal + MMB2) at POM
+    transcript length (T = 1089 / 1357 > the 512-token LDS chunk of the
+    workgroup stream kernel, so the chunk loop wraps 3 times), against the
+    oracle; 46 / 37-wide frames take the scalar-load variants."""
+    E, wt, ids, audio, visual = _pom_case(golden, case, n, A, Vd, seed=40)
+    N, T = ids.shape
+    assert T > 1024
+    torch.manual_seed(5)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None)
+    inputs = {"table": torch.tensor(E, device=gpu),
+              "wtab": torch.tensor(wt, device=gpu, dtype=torch.float32),
+              "ids": torch.as_tensor(ids, dtype=torch.int32, device=gpu),
+              "audio": torch.tensor(audio, device=gpu), "visual": torch.tensor(visual, device=gpu)}
+    step = P.FusedStep(inputs, gen.to(gpu).networks())
+    sif_out, mm2_out = step.run()
+    step.check()
+    ref_sif = O.get_sentence_embeddings(E, wt, ids)
+    assert M.row_rel_err(sif_out.cpu().numpy(), ref_sif) < TOL
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    text = E[ids]
+    ref_mm2 = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                                 M.params_from_module(gen.cpu()), sw, text)
+    assert M.row_rel_err(mm2_out.cpu().numpy(), ref_mm2) < TOL
+
+
+@pytest.mark.parametrize("case,n,t_frames", [("g1_pom_test", 16, None), ("g1_pom_valid", 16, 160)])
+def test_gpu2_drop_in_pom_length(gpu, golden, case, n, t_frames):
+    """The sif2 drop-in at POM length through the --time_test call shape
+    (simplesif.py:820-875): dense text / frames at T = 1357, and the POM form
+    where the weighted text term runs over the unaligned transcript (L = 1089
+    ids) while the frames are word-aligned with their own T = 160."""
+    E, wt, ids, audio, visual = _pom_case(golden, case, n, 300, 300, seed=50)
+    N, L_ = ids.shape
+    T = t_frames or L_
+    torch.manual_seed(6)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None)
+    if t_frames:
+        rng = np.random.default_rng(7)
+        text = (E[rng.integers(1, E.shape[0], (N, T))]).astype(np.float32)
+        audio, visual = audio[:, :T].copy(), visual[:, :T].copy()
+    else:
+        text = E[ids]
+    emb = E[ids]
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    t_ = lambda a: torch.tensor(a, device=gpu)
+    au, vi, tx = t_(audio), t_(visual), t_(text)
+    data = {"text": tx, "audio": au, "visual": vi, "audiovisual": torch.cat([au, vi], -1),
+            "textaudio": torch.cat([tx, au], -1), "textvisual": torch.cat([tx, vi], -1),
+            "textaudiovisual": torch.cat([tx, au, vi], -1)}
+    masks = {k: None for k in data}
+    g = gen.to(gpu)
+    nets = {k: (g.embed2out[k]["mu"], g.embed2out[k]["log_sigma"]) for k in sif2.KEYS}
+    with torch.no_grad():
+        cs = sif2.estimate_embedding_overall_gpu2(data, masks, nets, t_(sw), t_(emb))
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                            M.params_from_module(gen.cpu()), sw, emb)
+    assert M.row_rel_err(cs.cpu().numpy(), ref) < TOL
+
+
+def test_gpu2_rejects_combinations_that_are_not_concatenations(gpu, golden):
+    """The kernel streams text / audio / visual once; a combination tensor that
+    is not their torch.cat (wrong width, wrong frames, or other contents)
+    would give a different answer than the reference, so it raises."""
+    z = golden("g4_mmb2_mosi")
+    gen, E, ids, audio, visual, weights = _inputs(z, gpu)
+    t_ = lambda a: torch.tensor(a, device=gpu)
+    text, au, vi = t_(E[ids]), t_(audio), t_(visual)
+    base = {"text": text, "audio": au, "visual": vi, "audiovisual": torch.cat([au, vi], -1),
+            "textaudio": torch.cat([text, au], -1), "textvisual": torch.cat([text, vi], -1),
+            "textaudiovisual": torch.cat([text, au, vi], -1)}
+    masks = {k: None for k in base}
+    g = gen.to(gpu)
+    nets = {k: (g.embed2out[k]["mu"], g.embed2out[k]["log_sigma"]) for k in sif2.KEYS}
+    sw = t_(np.where(ids >= 0, weights.astype(np.float32)[ids], 0).astype(np.float32))
+    bad_width = dict(base, textvisual=torch.cat([text, vi[..., :-1]], -1))
+    with pytest.raises(ValueError, match="textvisual.*features"):
+        sif2.estimate_embedding_overall_gpu2(bad_width, masks, nets, sw, text)
+    bad_frames = dict(base, audiovisual=base["audiovisual"][:, :-1])
+    with pytest.raises(ValueError, match="audiovisual"):
+        sif2.estimate_embedding_overall_gpu2(bad_frames, masks, nets, sw, text)
+    other = dict(base, textaudio=torch.cat([text * 2, au], -1))
+    with pytest.raises(ValueError, match="textaudio.*not data\\['text'\\]"):
+        sif2.estimate_embedding_overall_gpu2(other, masks, nets, sw, text)
+    with torch.no_grad():
+        ok = sif2.estimate_embedding_overall_gpu2(base, masks, nets, sw, text)
+    assert M.row_rel_err(ok.cpu().numpy(), z["cs_f64"]) < TOL

@@ -125,3 +125,49 @@ def test_train_for_latents_matches_reference_run(gpu, golden):
     assert abs(results["mae"] - after["mae"]) < 1e-4
     assert abs(results["corr"] - after["corr"]) < 1e-4
     assert results["accuracy"] == after["accuracy"]
+
+
+@pytest.mark.parametrize("case", ["g5_full", "g5_full_es"])
+def test_full_size_run_matches_reference(gpu, tmp_path, case, capsys):
+    """BASELINE configs[4]: MOSI-sized splits (1284 / 229 / 686), H = 100, 400
+    epochs, the reference's own recorded runs (tests/golden/make_goldens_regressor.py).
+    g5_full_es also takes the early-stopping branch end to end: two best-model
+    reloads with lr decay, then the early stop at epoch 330, and the
+    reference's quirk of evaluating the un-reloaded model afterwards
+    (sentiment_model.py:132-160, 243-250).  Tolerances: the GPU sums the
+    mini-batch reductions in another order than torch's CPU kernels, so the
+    fp32 trajectories drift apart slowly over 16k SGD steps."""
+    from test_regressor_oracle import full_case
+
+    args, lat, lab, z, meta = full_case(case)
+    captured = {}
+    orig = SM.train_sentiment
+
+    def spy(*a, **k):
+        tl, vl = orig(*a, **k)
+        captured["train"], captured["valid"] = tl, vl
+        captured["model"] = {kk: v.detach().cpu().numpy() for kk, v in a[1].state_dict().items()}
+        return tl, vl
+
+    SM.train_sentiment = spy
+    try:
+        torch.manual_seed(int(z["seed"]))
+        results = SM.train_sentiment_for_latents(args, tuple(torch.tensor(l) for l in lat),
+                                                 tuple(lab), gpu, model_save_path=str(tmp_path))
+    finally:
+        SM.train_sentiment = orig
+    out = capsys.readouterr().out
+    assert out.count("reloading model and decaying") == meta["events"]["reloads"]
+    assert ("early stopping..." in out) == meta["events"]["early_stop"]
+    assert sorted(os.listdir(tmp_path)) == meta["files"]
+    assert len(captured["train"]) == len(z["train_losses"])
+    assert len(captured["valid"]) == len(z["valid_losses"])
+    np.testing.assert_allclose(captured["train"], z["train_losses"], rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(captured["valid"], z["valid_losses"], rtol=2e-3, atol=1e-5)
+    for k, v in captured["model"].items():
+        ref = z["final_" + k.replace(".", "_")]
+        assert np.abs(v - ref).max() < 5e-3 * max(1.0, np.abs(ref).max()), k
+    after = meta["after"]
+    assert abs(results["mae"] - after["mae"]) < 2e-3
+    assert abs(results["corr"] - after["corr"]) < 2e-3
+    assert abs(results["accuracy"] - after["accuracy"]) <= 2.0 / len(lab[2]) + 1e-12

@@ -195,3 +195,119 @@ def test_two_phase_gram_equals_one_shot_and_fp64(gpu):
     with pytest.raises(L.MMBError):  # a chunk larger than the plan is rejected
         L.call("mmb_gram_part", L.ptr(x), None, x.shape[0], n_plan, d, 0, L.ptr(ws.buf),
                L.stream_ptr())
+
+
+def test_compute_pc_float64_input_is_not_rounded(gpu, golden):
+    """A float64 X that is not f32-representable takes the f64-row kernels
+    (mmb_gram_f64 / mmb_xt_omega_f64 / mmb_pc_remove_f64): the PC and the
+    removal match the reference's f64 randomized SVD to f64 rounding, where
+    rounding X to f32 first would be ~1e-7 off.  Both sklearn branches."""
+    for case in ("g2_mosi", "g1_pom_valid"):
+        z = golden(case)
+        rng = np.random.default_rng(3)
+        X = z["emb"].astype(np.float64) * (1.0 + 1e-6 * rng.standard_normal(z["emb"].shape))
+        assert not np.array_equal(X.astype(np.float32).astype(np.float64), X)
+        ref_pc = O.compute_pc(X, 1)
+        pc = SF.compute_pc(X, 1)
+        assert np.abs(pc - ref_pc).max() < 1e-12
+        out = SF.remove_pc(X, 1)
+        assert M.row_rel_err(out, O.remove_pc(X, 1)) < 1e-12
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 10, 11, 12])
+def test_compute_pc_tiny_splits(gpu, n):
+    """Splits smaller than the randomized-SVD block (n < npc + 10 = 11): the
+    block is rank-deficient; the device solver must still give sklearn's PC."""
+    rng = np.random.default_rng(n)
+    g = rng.standard_normal(300)
+    X = (0.4 * rng.standard_normal((n, 300)) + 0.3 * g).astype(np.float32).astype(np.float64)
+    ref = O.compute_pc(X, 1)
+    pc = SF.compute_pc(X, 1)
+    assert np.isfinite(pc).all()
+    assert np.abs(pc - ref).max() < 1e-8
+
+
+def test_npc_limit_raises_value_error(gpu, golden):
+    z = golden("g2_mosi")
+    with pytest.raises(ValueError, match="npc"):
+        SF.compute_pc(z["emb"].astype(np.float64), 7)
+    assert SF.compute_pc(z["emb"].astype(np.float64), 6).shape == (6, 300)
+
+
+def test_zero_weight_utterance_raises_like_reference(gpu):
+    """An utterance whose SIF weights are all 0 makes the reference's
+    TruncatedSVD raise ValueError (NaN row); so does the device path, while the
+    plain weighted average keeps numpy's NaN row."""
+    V = 500
+    E = synth.word_table(V, 300, seed=3)
+    wt = synth.sif_weights(V, w0=0.0)
+    ids = synth.token_ids(400, 12, V, seed=4, ragged=True)
+    ids[5, :] = 0
+    with pytest.raises(ValueError, match="NaN"):
+        sif.get_sentence_embeddings(E, wt, ids)
+    w = O.seq2weight(ids, np.ones(ids.shape), wt)
+    with pytest.raises(ValueError, match="NaN"):
+        SF.compute_pc(SF.get_weighted_average(E, ids, w))
+
+
+@pytest.mark.parametrize("n_total,shards", [(5000, 4), (250, 2), (1200, 3)])
+def test_fused_step_sharded_with_fake_allreduce(gpu, n_total, shards):
+    """The multi-GPU bench step, all ranks on one device: every shard runs the
+    product FusedStep(n_total=..., row0=..., allreduce=fake) where `fake`
+    adds the OTHER shards' Grams (and X^T Omega blocks in the transposed
+    branch, n_total < 300) exactly where RCCL's all_reduce would.  The PC must
+    equal the unsharded step's to 1e-10, the SIF rows to the removal's dot
+    order, and the MMB2 rows bit for bit (they never cross shards)."""
+    import distributed as D
+
+    V = 8000
+    inp = synth.device_workload(n_total, 40, V, seed=13, device=gpu)
+    torch.manual_seed(0)
+    import models
+
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    whole = P.FusedStep(inp, gen.networks())
+    s_ref, m_ref = [t.clone() for t in whole.run()]
+    pc_ref = whole.pc.clone()
+
+    def shard(r):
+        row0, n = D.shard_range(n_total, shards, r)
+        sl = {k: (v[row0:row0 + n] if k in ("ids", "audio", "visual") else v)
+              for k, v in inp.items()}
+        return row0, n, sl
+
+    # pass 1: every shard's local contributions, in all_reduce call order
+    local = []
+    for r in range(shards):
+        row0, n, sl = shard(r)
+        got = []
+        step = P.FusedStep(sl, gen.networks(), n_total=n_total, row0=row0,
+                           allreduce=lambda t, got=got: got.append(t.clone()))
+        step.run()
+        local.append(got)
+    n_calls = 2 if n_total < 300 else 1
+    assert all(len(g) == n_calls for g in local)
+
+    # pass 2: the fake all-reduce adds the other shards' tensors in rank order
+    sif_parts, mm2_parts = [], []
+    for r in range(shards):
+        row0, n, sl = shard(r)
+        calls = iter(range(n_calls))
+
+        def fake(t, r=r, calls=calls):
+            c = next(calls)
+            tot = torch.zeros_like(t)
+            for q in range(shards):
+                tot += t if q == r else local[q][c]
+            t.copy_(tot)
+
+        step = P.FusedStep(sl, gen.networks(), n_total=n_total, row0=row0, allreduce=fake)
+        trace = {}
+        s, m = step.run(trace=trace)
+        assert "allreduce" in trace
+        assert (step.pc - pc_ref).abs().max().item() < 1e-10
+        step.check()
+        sif_parts.append(s.clone())
+        mm2_parts.append(m.clone())
+    assert torch.equal(torch.cat(mm2_parts), m_ref)
+    assert M.row_rel_err(torch.cat(sif_parts).cpu().numpy(), s_ref.cpu().numpy()) < 1e-6

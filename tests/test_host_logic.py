@@ -77,3 +77,72 @@ def test_side_cu_sets_are_balanced_and_disjoint():
         assert set(collections.Counter(c // 32 for c in s).values()) == {side // 8}
         assert len(P.side_cu_set(256, side, "high")) == side
         assert len(P.side_cu_set(256, side, "strided")) == side
+
+
+def _mm_data(n=4, t=6, d=8, a=5, vd=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    tx, au, vi = (torch.randn(n, t, f, generator=g) for f in (d, a, vd))
+    return {"text": tx, "audio": au, "visual": vi, "audiovisual": torch.cat([au, vi], -1),
+            "textaudio": torch.cat([tx, au], -1), "textvisual": torch.cat([tx, vi], -1),
+            "textaudiovisual": torch.cat([tx, au, vi], -1)}
+
+
+def test_gpu2_combination_check_accepts_concatenations_and_names_the_bad_key():
+    """sif2.check_combinations (host side of the gpu2 drop-in): concatenations
+    pass; a wrong width, a wrong frame count, or other contents raise a
+    ValueError naming the key (simplesif.py:825-830 builds them with torch.cat)."""
+    import sif2
+
+    d = _mm_data()
+    sif2.check_combinations(d)
+    nan = _mm_data()
+    nan["audio"][0, 0, 0] = float("nan")
+    nan["audiovisual"] = torch.cat([nan["audio"], nan["visual"]], -1)
+    nan["textaudio"] = torch.cat([nan["text"], nan["audio"]], -1)
+    nan["textaudiovisual"] = torch.cat([nan["text"], nan["audio"], nan["visual"]], -1)
+    sif2.check_combinations(nan)  # NaN frames are still the same concatenation
+    bad = dict(d, textaudiovisual=d["textaudiovisual"][..., :-1])
+    with pytest.raises(ValueError, match="textaudiovisual.*8 \\+ 5 \\+ 3"):
+        sif2.check_combinations(bad)
+    bad = dict(d, textvisual=d["textvisual"][:, :-1])
+    with pytest.raises(ValueError, match="textvisual"):
+        sif2.check_combinations(bad)
+    swapped = dict(d, audiovisual=torch.cat([d["visual"], d["audio"]], -1))
+    with pytest.raises(ValueError, match="audiovisual"):
+        sif2.check_combinations(swapped)
+    sif2.CHECK_CONCATENATIONS = False
+    try:
+        sif2.check_combinations(dict(d, textaudio=d["textaudio"] * 2))  # widths only
+    finally:
+        sif2.CHECK_CONCATENATIONS = True
+
+
+def test_npc_limit_is_a_clear_value_error():
+    import pipeline as P
+
+    for npc in range(1, 7):
+        P.check_npc(npc)
+    for npc in (0, 7, 20):
+        with pytest.raises(ValueError, match="npc"):
+            P.check_npc(npc)
+
+
+def test_tiny_splits_pc_restatement_matches_sklearn():
+    """The device solver's math (Gram-only randomized SVD, pc_from_gram via
+    CPUOps) equals scikit-learn's TruncatedSVD also for splits smaller than
+    the npc + 10 block (the rank-deficient LU branch)."""
+    from sklearn.decomposition import TruncatedSVD
+
+    import pipeline as P
+    from oracle import sif_oracle as O
+
+    for n in (1, 2, 5, 10, 11):
+        rng = np.random.default_rng(n)
+        g = rng.standard_normal(300)
+        X = (0.4 * rng.standard_normal((n, 300)) + 0.3 * g).astype(np.float32)
+        svd = TruncatedSVD(n_components=1, n_iter=7, random_state=0)
+        with np.errstate(all="ignore"):
+            ref = svd.fit(X.astype(np.float64)).components_
+        pc = P.global_pc(torch.from_numpy(X), None, 1, n, 0, None, ops=O.CPUOps).numpy()
+        assert np.abs(pc - ref).max() < 1e-12
+        assert np.abs(O.compute_pc(X.astype(np.float64), 1) - ref).max() < 1e-14
