@@ -35,31 +35,50 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = "/root/reference"
 SIZES = (1284, 229, 686)
-# (fixture, early_stopping, seed, label noise): with noise 1.5 the ES run reloads
-# the best model twice (lr decayed each time) and then stops early at epoch 330
-CASES = (("g5_full", False, 4242, 0.9), ("g5_full_es", True, 4343, 1.5))
+# (fixture, early_stopping, seed, label noise, validation labels flipped).
+# g5_full_es flips the validation labels' sign: every SGD step that fits the
+# training split moves the validation loss up, so after the first validation
+# none is better -- 10 bad validations (epoch 100) reload the epoch-0
+# checkpoint with lr * 0.5, again at epoch 200, and the third trial stops at
+# epoch 300.  The margins between validations are wide, so these events do
+# not depend on rounding (the plain run's loss curve does, see ENVELOPE).
+CASES = (("g5_full", False, 4242, 0.9, False), ("g5_full_es", True, 4343, 0.9, True))
 
 
-def latents_and_labels(seed: int, sizes=SIZES, noise: float = 0.9):
+def latents_and_labels(seed: int, sizes=SIZES, noise: float = 0.9, flip_valid: bool = False):
     """Seeded MOSI-shaped latents (unit-norm-ish rows like SIF output) and
-    labels in [-3, 3] (MOSI's range) that a 300->100->1 net can fit but,
-    with label noise, overfits -- so validation loss turns up and the
-    early-stopping branch is exercised."""
+    labels in [-3, 3] (MOSI's range) that a 300->100->1 net can fit, with
+    label noise (it overfits)."""
     rng = np.random.default_rng(seed)
     lat = [(rng.standard_normal((n, 300)) / np.sqrt(300)).astype(np.float32) for n in sizes]
     wproj = rng.standard_normal(300).astype(np.float32) * np.float32(2.0)
     wq = rng.standard_normal(300).astype(np.float32) * np.float32(2.0)
     labels = [np.clip(l @ wproj + np.abs(l @ wq) - 1.0 + noise * rng.standard_normal(l.shape[0]),
                       -3, 3).astype(np.float32) for l in lat]
+    if flip_valid:
+        labels[1] = -labels[1]
     return lat, labels
+
+
+# The loss curve of 16,400 fp32 SGD steps on an L1 loss is sensitive to
+# rounding: every residual that crosses 0 flips its gradient.  Each fixture
+# therefore also records the SAME reference function run (a) in float64 and
+# (b) in float32 on latents nudged by one ulp -- two rounding-level
+# perturbations of the reference itself.  Their distance from the recorded
+# run is the envelope a different-but-correct fp32 implementation (the GPU's
+# summation order) is held to after the first epochs.
+ENVELOPE = ("f64", "ulp")
 
 
 def checksum(a) -> float:
     return float(np.asarray(a, dtype=np.float64).sum())
 
 
-def run_reference(R_sm, args, lat, labels, seed, save_dir):
+def run_reference(R_sm, args, lat, labels, seed, save_dir, dtype=None):
     import torch
+
+    if dtype is not None:
+        torch.set_default_dtype(dtype)
 
     captured, metrics = {}, []
     orig, orig_fl = R_sm.train_sentiment, R_sm.full_loss
@@ -86,6 +105,7 @@ def run_reference(R_sm, args, lat, labels, seed, save_dir):
                                               model_save_path=save_dir)
     finally:
         R_sm.train_sentiment, R_sm.full_loss = orig, orig_fl
+        torch.set_default_dtype(torch.float32)
     log = buf.getvalue().splitlines()
     events = {"reloads": sum("reloading model and decaying" in s for s in log),
               "early_stop": any(s.strip() == "early stopping..." for s in log),
@@ -98,8 +118,10 @@ def main():
     sys.modules.setdefault("h5py", types.ModuleType("h5py"))
     import sentiment_model as R_sm  # noqa: E402
 
-    for name, es, seed, noise in CASES:
-        lat, labels = latents_and_labels(seed, noise=noise)
+    import torch
+
+    for name, es, seed, noise, flip in CASES:
+        lat, labels = latents_and_labels(seed, noise=noise, flip_valid=flip)
         args = {"sentiment_hidden_size": 100, "n_sentiment_epochs": 400, "sentiment_lr": 0.1,
                 "early_stopping": es, "dataset": "mosi", "lr_decay": 0.5}
         with tempfile.TemporaryDirectory() as d:
@@ -111,6 +133,21 @@ def main():
                 with open(os.path.join(d, f)) as fh:
                     text[f] = fh.read()
         print(name, events, "epochs run:", len(cap["train"]), "validations:", len(cap["valid"]))
+        env = {}
+        for kind in ENVELOPE:
+            if kind == "f64":
+                lat_k, dt = [l.astype(np.float64) for l in lat], torch.float64
+            else:
+                lat_k, dt = [np.nextafter(l, np.float32(np.inf)) for l in lat], None
+            with tempfile.TemporaryDirectory() as d:
+                c2, m2, e2 = run_reference(R_sm, args, lat_k, labels, seed, d, dtype=dt)
+            env[kind] = {"train_losses": c2["train"], "valid_losses": c2["valid"],
+                         "after": m2[1], "events": e2}
+            tl = np.array(c2["train"])
+            n = min(len(tl), len(cap["train"]))
+            print("  envelope", kind, e2, "max rel train-loss dev",
+                  float(np.max(np.abs(tl[:n] - cap["train"][:n]) / np.array(cap["train"][:n]))),
+                  "mae", m2[1]["mae"], "vs", metrics[1]["mae"])
         np.savez_compressed(
             os.path.join(HERE, name + ".npz"), seed=np.int64(seed),
             lat_checksums=np.array([checksum(l) for l in lat]),
@@ -118,8 +155,9 @@ def main():
             train_losses=np.array(cap["train"]), valid_losses=np.array(cap["valid"]),
             **{"final_" + k.replace(".", "_"): v.numpy() for k, v in cap["model"].items()})
         with open(os.path.join(HERE, name + ".json"), "w") as f:
-            json.dump({"args": args, "noise": noise, "before": metrics[0], "after": metrics[1], "events": events,
-                       "files": files, "text_files": text}, f, indent=1, sort_keys=True)
+            json.dump({"args": args, "noise": noise, "flip_valid": flip, "before": metrics[0],
+                       "after": metrics[1], "events": events, "files": files,
+                       "text_files": text, "envelope": env}, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -127,16 +127,28 @@ def test_train_for_latents_matches_reference_run(gpu, golden):
     assert results["accuracy"] == after["accuracy"]
 
 
+def _rel_dev(a, ref):
+    n = min(len(a), len(ref))
+    a, ref = np.asarray(a[:n], np.float64), np.asarray(ref[:n], np.float64)
+    return float(np.max(np.abs(a - ref) / np.abs(ref)))
+
+
 @pytest.mark.parametrize("case", ["g5_full", "g5_full_es"])
 def test_full_size_run_matches_reference(gpu, tmp_path, case, capsys):
     """BASELINE configs[4]: MOSI-sized splits (1284 / 229 / 686), H = 100, 400
-    epochs, the reference's own recorded runs (tests/golden/make_goldens_regressor.py).
-    g5_full_es also takes the early-stopping branch end to end: two best-model
-    reloads with lr decay, then the early stop at epoch 330, and the
-    reference's quirk of evaluating the un-reloaded model afterwards
-    (sentiment_model.py:132-160, 243-250).  Tolerances: the GPU sums the
-    mini-batch reductions in another order than torch's CPU kernels, so the
-    fp32 trajectories drift apart slowly over 16k SGD steps."""
+    epochs against the reference's own recorded runs
+    (tests/golden/make_goldens_regressor.py).  g5_full_es takes the
+    early-stopping branch end to end: reloads of the best checkpoint with lr
+    decay at epochs 100 and 200, the early stop at 300, and the reference's
+    quirk of evaluating the un-reloaded model afterwards
+    (sentiment_model.py:132-160, 243-250).
+
+    Bars.  16,400 fp32 SGD steps on an L1 loss amplify rounding: the
+    REFERENCE ITSELF, run in float64 or on latents nudged by one ulp, leaves
+    its recorded loss curve by up to ~20 % after epoch ~30 (the fixture's
+    `envelope`).  So: the first 20 epochs within 1e-4; the early-stopping
+    events, epoch count and files exactly; the loss curves and final metrics
+    within 1.5x the reference's own rounding envelope."""
     from test_regressor_oracle import full_case
 
     args, lat, lab, z, meta = full_case(case)
@@ -157,17 +169,26 @@ def test_full_size_run_matches_reference(gpu, tmp_path, case, capsys):
     finally:
         SM.train_sentiment = orig
     out = capsys.readouterr().out
-    assert out.count("reloading model and decaying") == meta["events"]["reloads"]
-    assert ("early stopping..." in out) == meta["events"]["early_stop"]
+    ev = meta["events"]
+    assert out.count("reloading model and decaying") == ev["reloads"]
+    assert ("early stopping..." in out) == ev["early_stop"]
     assert sorted(os.listdir(tmp_path)) == meta["files"]
-    assert len(captured["train"]) == len(z["train_losses"])
-    assert len(captured["valid"]) == len(z["valid_losses"])
-    np.testing.assert_allclose(captured["train"], z["train_losses"], rtol=2e-3, atol=1e-5)
-    np.testing.assert_allclose(captured["valid"], z["valid_losses"], rtol=2e-3, atol=1e-5)
-    for k, v in captured["model"].items():
-        ref = z["final_" + k.replace(".", "_")]
-        assert np.abs(v - ref).max() < 5e-3 * max(1.0, np.abs(ref).max()), k
+    tl, vl = captured["train"], captured["valid"]
+    assert len(tl) == len(z["train_losses"]) and len(vl) == len(z["valid_losses"])
+    np.testing.assert_allclose(tl[:20], z["train_losses"][:20], rtol=1e-4)
+    np.testing.assert_allclose(vl[:2], z["valid_losses"][:2], rtol=1e-4)
+    env = meta["envelope"]
+    for kind in env:  # the perturbed reference runs took the same branch decisions
+        assert env[kind]["events"]["reloads"] == ev["reloads"]
+    env_train = max(_rel_dev(e["train_losses"], z["train_losses"]) for e in env.values())
+    env_valid = max(_rel_dev(e["valid_losses"], z["valid_losses"]) for e in env.values())
+    assert _rel_dev(tl, z["train_losses"]) <= 1.5 * env_train + 1e-3
+    assert _rel_dev(vl, z["valid_losses"]) <= 1.5 * env_valid + 1e-3
     after = meta["after"]
-    assert abs(results["mae"] - after["mae"]) < 2e-3
-    assert abs(results["corr"] - after["corr"]) < 2e-3
-    assert abs(results["accuracy"] - after["accuracy"]) <= 2.0 / len(lab[2]) + 1e-12
+    for key in ("mae", "corr", "accuracy"):
+        band = max(abs(e["after"][key] - after[key]) for e in env.values())
+        assert abs(results[key] - after[key]) <= 1.5 * band + 0.01, (key, results[key], after[key], band)
+    if ev["early_stop"]:
+        # after each reload the epoch-0 checkpoint is back: the next validation
+        # is again above the first one, like the reference's
+        assert all(v > vl[0] for v in vl[1:])

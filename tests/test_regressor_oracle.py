@@ -4,7 +4,9 @@ Pins the oracle the GPU regressor tests and bench.py's regressor cpu_baseline
 rely on: the 20-epoch g5_senti_train run exactly, the full-size (1284 / 229 /
 686, 400 epochs) g5_full run over its first 20 epochs, and the full-size
 early-stopping run g5_full_es end to end (two best-model reloads with lr
-decay, then the early stop at epoch 330, sentiment_model.py:132-160).
+decay at epochs 100 and 200, then the early stop at epoch 300,
+sentiment_model.py:132-160) -- bit for bit: the oracle is the reference's
+loop in the same torch CPU arithmetic.
 """
 import importlib.util
 import json
@@ -34,7 +36,8 @@ def full_case(name):
     z = np.load(os.path.join(GOLDEN, name + ".npz"))
     with open(os.path.join(GOLDEN, name + ".json")) as f:
         meta = json.load(f)
-    lat, lab = g.latents_and_labels(int(z["seed"]), noise=meta["noise"])
+    lat, lab = g.latents_and_labels(int(z["seed"]), noise=meta["noise"],
+                                    flip_valid=meta["flip_valid"])
     assert np.allclose([g.checksum(l) for l in lat], z["lat_checksums"], rtol=0, atol=1e-9)
     assert np.allclose([g.checksum(l) for l in lab], z["label_checksums"], rtol=0, atol=1e-9)
     return dict(meta["args"]), lat, lab, z, meta
