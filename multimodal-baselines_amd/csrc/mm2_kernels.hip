@@ -605,7 +605,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
   }
 }
 
-template <int CT, bool ROWEPI>
+template <int CT, bool ROWEPI, bool PIPE = false>
 __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
     const _Float16* __restrict__ img, const float* __restrict__ col_inv,
@@ -661,10 +661,6 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
 
   // 1 / row scale (a power of two: exact)
   if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
-  stage_b(0);
-  stage_a(0);
-  stage_a(1);
-  stage_a(2);
 
   f32x4 acc[4][CT];
 #pragma unroll
@@ -672,6 +668,83 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
 #pragma unroll
     for (int t = 0; t < CT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (PIPE) {
+    // Software-pipelined K loop: the fragments an MFMA consumes were read
+    // from LDS while the previous MFMAs ran.  B(c+1)'s fragments (a second
+    // register set) are read during chunk c's MFMAs; A(c)'s row tiles one
+    // tile ahead (A(c+1) tile 0 during chunk c's last tile).  One barrier per
+    // chunk, placed where chunk c+1 has landed (own copies by a counted
+    // vmcnt that leaves A(c+2) in flight, everyone's by the barrier) and
+    // every wave has finished reading B(c) and A(c-1) -- whose ring slots
+    // the copies issued right after it (B(c+2), A(c+3)) overwrite.  The
+    // MFMA pipe then idles only for the barrier skew, not for LDS latency.
+    stage_b(0);
+    stage_a(0);
+    stage_a(1);
+    stage_b(1);
+    stage_a(2);
+    // B(0), A(0) landed; A(1), B(1), A(2) may be in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * AQ + BQ) : "memory");
+    __builtin_amdgcn_s_barrier();
+    half8 bh0[CT], bl0[CT], bh1[CT], bl1[CT], ah0, al0, ah1, al1;
+    auto rd_b = [&](int c, half8 (&bh)[CT], half8 (&bl)[CT]) {
+      const _Float16* b = bring + (c & (kXBbuf - 1)) * BBUF;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        const int col = (wc * CT + t) * 16 + lc;
+        const int bo = col * kXK + ((lq ^ x3_swz(col)) * 8);
+        bh[t] = *reinterpret_cast<const half8*>(b + bo);
+        bl[t] = *reinterpret_cast<const half8*>(b + LDW * kXK + bo);
+      }
+    };
+    auto rd_a = [&](int c, int i, half8& ah, half8& al) {
+      const _Float16* a = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
+      const int row = wr * 64 + i * 16 + lc;
+      const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
+      ah = *reinterpret_cast<const half8*>(a + ao);
+      al = *reinterpret_cast<const half8*>(a + kXM * kXK + ao);
+    };
+    auto tile = [&](int i, const half8& ah, const half8& al, const half8 (&bh)[CT],
+                    const half8 (&bl)[CT]) {
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[t], acc[i][t], 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[t], acc[i][t], 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[t], acc[i][t], 0, 0, 0);
+      }
+    };
+    rd_b(0, bh0, bl0);
+    rd_a(0, 0, ah0, al0);
+    // chunk c with B(c) in (bh, bl), A(c) tile 0 in (ah0, al0); reads B(c+1)
+    // into (nbh, nbl) and leaves A(c+1) tile 0 in (ah0, al0)
+    auto chunk = [&](int c, half8 (&bh)[CT], half8 (&bl)[CT], half8 (&nbh)[CT],
+                     half8 (&nbl)[CT]) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AQ) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      stage_b(c + 2);
+      stage_a(c + 3);
+      rd_b(c + 1, nbh, nbl);
+      rd_a(c, 1, ah1, al1);
+      tile(0, ah0, al0, bh, bl);
+      rd_a(c, 2, ah0, al0);
+      tile(1, ah1, al1, bh, bl);
+      rd_a(c, 3, ah1, al1);
+      tile(2, ah0, al0, bh, bl);
+      rd_a(c + 1, 0, ah0, al0);
+      tile(3, ah1, al1, bh, bl);
+    };
+#pragma unroll 1
+    for (int c = 0; c + 1 < nch; c += 2) {
+      chunk(c, bh0, bl0, bh1, bl1);
+      chunk(c + 1, bh1, bl1, bh0, bl0);
+    }
+    if (nch & 1) chunk(nch - 1, bh0, bl0, bh1, bl1);
+  } else {
+  stage_b(0);
+  stage_a(0);
+  stage_a(1);
+  stage_a(2);
   for (int c = 0; c < nch; ++c) {
     // chunk c landed: this wave's copies of B(c) and A(c) retired (only the
     // newest A chunk, AQ copies, may still be in flight; in the first
@@ -714,6 +787,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
         acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh[t], acc[i][t], 0, 0, 0);
       }
   }
+  }  // PIPE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -963,7 +1037,8 @@ constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(
 
 // Projection kernel variant: 0 = 32x32x16 MFMA tiles (wave = 32 rows x 32 CT
 // columns), 1 = 16x16x32 tiles (wave = 64 rows x 16 CT columns: 18 instead of
-// 24 fragment reads per chunk).  MMB_PROJ_VARIANT overrides (read once).
+// 24 fragment reads per chunk), 2 = the 16x16x32 kernel with the
+// software-pipelined K loop.  MMB_PROJ_VARIANT overrides (read once).
 // Row-wise projection epilogue (1, default) or the MFMA-tile-layout one (0);
 // MMB_PROJ_ROWEPI overrides (read once).
 static bool proj_row_epilogue() {
@@ -977,7 +1052,7 @@ static bool proj_row_epilogue() {
 static int proj_variant() {
   static const int v = [] {
     const char* e = getenv("MMB_PROJ_VARIANT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -996,7 +1071,7 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
-  if (proj_variant() == 1) {
+  if (proj_variant() >= 1) {
     constexpr size_t ldsb = x3b_lds_bytes<CT>();
     static_assert(ldsb <= 160 * 1024, "x3b chunk rings exceed LDS");
     static bool attr_b = false;
@@ -1005,6 +1080,10 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, false, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
       attr_b = true;
     }
     auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
@@ -1012,7 +1091,14 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
     // unit), whole float4 units, 16-byte aligned rows
     const bool rowepi = CT == 5 && d >= 256 && d % 4 == 0 && a16(num) && a16(out) &&
                         (sif == nullptr || a16(sif)) && proj_row_epilogue();
-    if (rowepi) {
+    const bool pipe = proj_variant() == 2;
+    if (rowepi && pipe) {
+      mm2_project_x3b_kernel<CT, true, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
+                                                                          n, kp, d, out, pc, sif);
+    } else if (pipe) {
+      mm2_project_x3b_kernel<CT, false, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
+                                                                           n, kp, d, out, pc, sif);
+    } else if (rowepi) {
       mm2_project_x3b_kernel<CT, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp,
                                                                     d, out, pc, sif);
     } else {

@@ -311,11 +311,13 @@ np.savez(sys.argv[1], sif=s.cpu().numpy(), mmb2=m.cpu().numpy())
 
 
 @pytest.mark.parametrize("env", [{"MMB_PROJ_VARIANT": "0", "MMB_STREAM_POLICY": "0"},
+                                 {"MMB_PROJ_VARIANT": "1"},
                                  {"MMB_STREAM_POLICY": "7", "MMB_STREAM_GRID_MULT": "8"},
                                  {"MMB_PROJ_ROWEPI": "0"}])
 def test_non_default_kernel_variants_agree(gpu, tmp_path, env):
     """The measured-and-kept-selectable variants (32x32x16 projection tiles,
-    every stream-kernel load/store policy, grid size; read once per process,
+    the 16x16x32 kernel without the pipelined K loop, every stream-kernel
+    load/store policy, grid size; read once per process,
     so run in a child process) give the default path's rows: SIF to the
     removal's dot order, MMB2 within the 1e-5 bar."""
     import os

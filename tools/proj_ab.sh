@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# A/B of the projection kernel variants (MMB_PROJ_VARIANT 0 = 32x32x16 tiles,
+# A/B of the projection kernel variants (MMB_PROJ_VARIANT 0 = 32x32x16 tiles, 2 = pipelined 16x16x32,
 # 1 = 16x16x32 tiles): the
 # MMB2 GPU parity tests under variant $V (default 1), then the kernel
 # microbench of each listed variant, twice, and the bench under each.
