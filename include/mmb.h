@@ -223,6 +223,20 @@ int mmb_mlp_forward(const float* latents, const int64_t* idx, int64_t b, int d, 
                     const float* w1, const float* b1, const float* w2, const float* b2,
                     float* y_out, hipStream_t stream);
 
+/* Differentiable forward / backward of the same model, for the e2e joint
+ * objective whose regressor term backpropagates into the latents
+ * (simplesif.py:776-790, autograd of sentiment_model.py:36-41):
+ *   forward_train: y [b,o] and the post-ReLU hidden activations hid [b,h];
+ *   backward: dh_ws [b,h] scratch, dx [b,d] (nullable), dw1 [h,d], db1 [h],
+ *   dw2 [o,h], db2 [o] (each nullable) for upstream gradient dy [b,o].
+ * Parameter gradients reduce over the rows in a fixed order.                 */
+int mmb_mlp_forward_train(const float* x, int64_t b, int d, int h, int o, const float* w1,
+                          const float* b1, const float* w2, const float* b2, float* y_out,
+                          float* hid_out, hipStream_t stream);
+int mmb_mlp_backward(const float* x, const float* hid, int64_t b, int d, int h, int o,
+                     const float* w1, const float* w2, const float* dy, float* dh_ws, float* dx,
+                     float* dw1, float* db1, float* dw2, float* db2, hipStream_t stream);
+
 /* L1 loss sum for prediction rows vs labels (per-batch means written to
  * batch_loss): the evaluation loops of sentiment_model.py:60-74,117-125.
  * Batches are consecutive slices of `perm` of size batch (last one ragged). */

@@ -276,6 +276,139 @@ __global__ __launch_bounds__(256) void mlp_eval_kernel(const float* __restrict__
   if (tid == 0 && batch_loss) batch_loss[blockIdx.x] = (s_red[0] + s_red[1] + s_red[2] + s_red[3]) / static_cast<float>(Bc * O);
 }
 
+// ---------------------------------------------------------------- autograd pieces
+// The differentiable forward / backward the e2e joint objective needs
+// (simplesif.py:776-790: the regressor's L1 term backpropagates into the
+// latents and the regressor's parameters).  Rows are independent in the
+// forward and in dX; the parameter gradients reduce over the batch in a
+// fixed row order (deterministic).
+constexpr int kMlpRows = 8;  // rows per block of the row kernels
+
+// hid[b][h] = relu(b1[h] + x[b] . w1[h]),  y[b][o] = b2[o] + hid[b] . w2[o].
+// Block = kMlpRows rows staged in LDS; thread = hidden unit h, walking its own
+// w1 row (each 64-byte line reused over 16 k-steps from L1) with the block's
+// rows' x broadcast from LDS: one w1 load serves kMlpRows FMAs.
+__global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restrict__ x, int64_t B,
+                                                           int D, int H, int O,
+                                                           const float* __restrict__ w1,
+                                                           const float* __restrict__ b1,
+                                                           const float* __restrict__ w2,
+                                                           const float* __restrict__ b2,
+                                                           float* __restrict__ y,
+                                                           float* __restrict__ hid) {
+  extern __shared__ float sm[];
+  float* sx = sm;                      // [kMlpRows][D]
+  float* sh = sx + kMlpRows * D;       // [kMlpRows][H]
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kMlpRows;
+  const int nr = static_cast<int>(min<int64_t>(kMlpRows, B - r0));
+  for (int e = threadIdx.x; e < kMlpRows * D; e += blockDim.x) {
+    const int r = e / D;
+    sx[e] = r < nr ? x[(r0 + r) * D + e % D] : 0.f;
+  }
+  __syncthreads();
+  for (int h = threadIdx.x; h < H; h += blockDim.x) {
+    const float* wr = w1 + static_cast<int64_t>(h) * D;
+    float p[kMlpRows];
+#pragma unroll
+    for (int r = 0; r < kMlpRows; ++r) p[r] = b1[h];
+#pragma unroll 4
+    for (int d = 0; d < D; ++d) {
+      const float w = wr[d];
+#pragma unroll
+      for (int r = 0; r < kMlpRows; ++r) p[r] = fmaf(w, sx[r * D + d], p[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < kMlpRows; ++r) {
+      const float v = p[r] > 0.f ? p[r] : 0.f;
+      sh[r * H + h] = v;
+      if (r < nr) hid[(r0 + r) * H + h] = v;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nr * O; e += blockDim.x) {
+    const int o = e % O, r = e / O;
+    float out = b2[o];
+    for (int h = 0; h < H; ++h) out = fmaf(w2[o * H + h], sh[r * H + h], out);
+    y[(r0 + r) * O + o] = out;
+  }
+}
+
+// dh[b][h] = [hid > 0] * sum_o dy[b][o] w2[o][h];  dx[b][d] = sum_h dh[b][h] w1[h][d]
+// (thread = column d: w1[h][d] coalesced over the block, dh broadcast from LDS)
+__global__ __launch_bounds__(256) void mlp_bwd_rows_kernel(const float* __restrict__ hid, int64_t B,
+                                                           int D, int H, int O,
+                                                           const float* __restrict__ w1,
+                                                           const float* __restrict__ w2,
+                                                           const float* __restrict__ dy,
+                                                           float* __restrict__ dh,
+                                                           float* __restrict__ dx) {
+  extern __shared__ float sm[];
+  float* sdh = sm;  // [kMlpRows][H]
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kMlpRows;
+  const int nr = static_cast<int>(min<int64_t>(kMlpRows, B - r0));
+  for (int e = threadIdx.x; e < kMlpRows * H; e += blockDim.x) {
+    const int h = e % H, r = e / H;
+    float g = 0.f;
+    if (r < nr && hid[(r0 + r) * H + h] > 0.f)
+      for (int o = 0; o < O; ++o) g = fmaf(dy[(r0 + r) * O + o], w2[o * H + h], g);
+    sdh[e] = g;
+    if (r < nr) dh[(r0 + r) * H + h] = g;
+  }
+  __syncthreads();
+  if (dx == nullptr) return;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float g[kMlpRows];
+#pragma unroll
+    for (int r = 0; r < kMlpRows; ++r) g[r] = 0.f;
+#pragma unroll 4
+    for (int h = 0; h < H; ++h) {
+      const float w = w1[static_cast<int64_t>(h) * D + d];
+#pragma unroll
+      for (int r = 0; r < kMlpRows; ++r) g[r] = fmaf(sdh[r * H + h], w, g[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < kMlpRows; ++r)
+      if (r < nr) dx[(r0 + r) * D + d] = g[r];
+  }
+}
+
+// block h < H: dw1[h][:] = sum_b dh[b][h] x[b][:], db1[h] = sum_b dh[b][h],
+// dw2[:, h] = sum_b dy[b][:] hid[b][h];  block H: db2 = sum_b dy[b][:]
+__global__ __launch_bounds__(256) void mlp_bwd_params_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ hid,
+                                                             const float* __restrict__ dh,
+                                                             const float* __restrict__ dy,
+                                                             int64_t B, int D, int H, int O,
+                                                             float* __restrict__ dw1,
+                                                             float* __restrict__ db1,
+                                                             float* __restrict__ dw2,
+                                                             float* __restrict__ db2) {
+  const int h = blockIdx.x;
+  if (h == H) {
+    for (int o = threadIdx.x; o < O; o += blockDim.x) {
+      float g = 0.f;
+      for (int64_t b = 0; b < B; ++b) g += dy[b * O + o];
+      if (db2) db2[o] = g;
+    }
+    return;
+  }
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float g = 0.f;
+    for (int64_t b = 0; b < B; ++b) g = fmaf(dh[b * H + h], x[b * D + d], g);
+    if (dw1) dw1[static_cast<int64_t>(h) * D + d] = g;
+  }
+  if (threadIdx.x == 0 && db1) {
+    float g = 0.f;
+    for (int64_t b = 0; b < B; ++b) g += dh[b * H + h];
+    db1[h] = g;
+  }
+  for (int o = threadIdx.x; o < O; o += blockDim.x) {
+    float g = 0.f;
+    for (int64_t b = 0; b < B; ++b) g = fmaf(dy[b * O + o], hid[b * H + h], g);
+    if (dw2) dw2[o * H + h] = g;
+  }
+}
+
 static int launch_train(const MlpArgs& a, size_t lds, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
@@ -347,4 +480,37 @@ extern "C" int mmb_mlp_train(const float* latents, const float* labels, const in
                                       o + 2 * kBatchMax * o + kMaxWaves);
   MMB_REQUIRE(lds <= 160 * 1024);
   return launch_train(a, lds, stream);
+}
+
+extern "C" int mmb_mlp_forward_train(const float* x, int64_t b, int d, int h, int o,
+                                     const float* w1, const float* b1, const float* w2,
+                                     const float* b2, float* y_out, float* hid_out,
+                                     hipStream_t stream) {
+  MMB_REQUIRE(x && w1 && b1 && w2 && b2 && y_out && hid_out && b >= 0 && d > 0 && h > 0 && o > 0);
+  if (b == 0) return MMB_OK;
+  const size_t lds = sizeof(float) * kMlpRows * (d + h);
+  MMB_REQUIRE(lds <= 64 * 1024);
+  mlp_fwd_rows_kernel<<<static_cast<int>(ceil_div(b, kMlpRows)), 256, lds, stream>>>(
+      x, b, d, h, o, w1, b1, w2, b2, y_out, hid_out);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_mlp_backward(const float* x, const float* hid, int64_t b, int d, int h, int o,
+                                const float* w1, const float* w2, const float* dy, float* dh_ws,
+                                float* dx, float* dw1, float* db1, float* dw2, float* db2,
+                                hipStream_t stream) {
+  MMB_REQUIRE(x && hid && w1 && w2 && dy && dh_ws && b >= 0 && d > 0 && h > 0 && o > 0);
+  if (b == 0) return MMB_OK;
+  const size_t lds = sizeof(float) * kMlpRows * h;
+  MMB_REQUIRE(lds <= 64 * 1024);
+  mlp_bwd_rows_kernel<<<static_cast<int>(ceil_div(b, kMlpRows)), 256, lds, stream>>>(
+      hid, b, d, h, o, w1, w2, dy, dh_ws, dx);
+  MMB_LAUNCH_CHECK();
+  if (dw1 || db1 || dw2 || db2) {
+    mlp_bwd_params_kernel<<<h + 1, 256, 0, stream>>>(x, hid, dh_ws, dy, b, d, h, o, dw1, db1, dw2,
+                                                     db2);
+    MMB_LAUNCH_CHECK();
+  }
+  return MMB_OK;
 }

@@ -97,6 +97,16 @@ def _combine(args, log_probs: dict, word_log_prob):
     return sum(log_probs.values()) + word_log_prob
 
 
+def combine_weighted(args, log_probs: dict, word_log_prob):
+    """_combine's weighting without its host-side inf check (the caller
+    checks, e.g. once per captured step: simplesif.check_step)."""
+    if "word_loss_weight" in args:
+        word_weight = args["word_loss_weight"]
+        other_weight = (1. - word_weight) / len(log_probs)
+        return sum(log_probs.values()) * other_weight + word_weight * word_log_prob
+    return sum(log_probs.values()) + word_log_prob
+
+
 def get_log_prob_matrix(args, latents, out, data, masks, word_log_prob_fn,
                         device=torch.device("cpu"), verbose=False):
     """losses.py:216-274: word model + one Gaussian per generator output key."""

@@ -60,6 +60,8 @@ SIGNATURES = {
     "mmb_mm2_project_x3_rmpc": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P, _P, _P]),
     "mmb_mlp_forward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_eval": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_mlp_forward_train": (_I, [_P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_mlp_backward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_workspace_bytes": (_S, [_I, _I]),
     "mmb_mlp_train": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_word_pad": (_I, [_I]),

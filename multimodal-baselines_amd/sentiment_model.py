@@ -3,8 +3,9 @@
 Same classes and functions, same arguments, same printed/saved artefacts.
 The arithmetic runs on the GPU through libmmb:
 
-* SentimentModel.forward          -> mmb_mlp_forward (no-grad calls; while autograd
-  records — the e2e joint objective — torch's device GEMMs carry the graph)
+* SentimentModel.forward          -> mmb_mlp_forward (no-grad calls); while autograd
+  records (the e2e joint objective, simplesif.py:776-790) -> the autograd
+  Function _Regressor: mmb_mlp_forward_train / mmb_mlp_backward
 * predict_sentiment / validation  -> mmb_mlp_eval (per-batch L1 means + predictions)
 * train_sentiment inner loop      -> mmb_mlp_train: every mini-batch step of a
   block of epochs (forward, L1 backward, SGD) in ONE single-workgroup launch,
@@ -27,7 +28,6 @@ import json
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 import torch.optim as optim
 from torch.utils.data import DataLoader, Dataset
 
@@ -66,6 +66,41 @@ def _params(model):
     return ps
 
 
+class _Regressor(torch.autograd.Function):
+    """y = relu(x W1^T + b1) W2^T + b2 with a hand-written backward
+    (libmmb mmb_mlp_forward_train / mmb_mlp_backward): gradients to the
+    inputs (the latents, in the e2e loop) and to every parameter."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x = x.detach().contiguous()
+        b, d = x.shape
+        h, o = w1.shape[0], w2.shape[0]
+        y = torch.empty((b, o), dtype=torch.float32, device=x.device)
+        hid = torch.empty((b, h), dtype=torch.float32, device=x.device)
+        L.call("mmb_mlp_forward_train", L.ptr(x), b, d, h, o, L.ptr(w1.detach()),
+               L.ptr(b1.detach()), L.ptr(w2.detach()), L.ptr(b2.detach()), L.ptr(y), L.ptr(hid),
+               L.stream_ptr())
+        ctx.save_for_backward(x, hid, w1, w2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, hid, w1, w2 = ctx.saved_tensors
+        b, d = x.shape
+        h, o = w1.shape[0], w2.shape[0]
+        need = ctx.needs_input_grad
+        e = lambda *shape: torch.empty(shape, dtype=torch.float32, device=x.device)
+        dx = e(b, d) if need[0] else None
+        dw1, db1 = (e(h, d) if need[1] else None), (e(h) if need[2] else None)
+        dw2, db2 = (e(o, h) if need[3] else None), (e(o) if need[4] else None)
+        dh = e(b, h)
+        L.call("mmb_mlp_backward", L.ptr(x), L.ptr(hid), b, d, h, o, L.ptr(w1.detach()),
+               L.ptr(w2.detach()), L.ptr(dy.float().contiguous()), L.ptr(dh), L.ptr(dx),
+               L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(db2), L.stream_ptr())
+        return dx, dw1, db1, dw2, db2
+
+
 class SentimentModel(nn.Module):
     """sentiment_model.py:29-41: squeeze(out(relu(hidden1(x))))."""
 
@@ -80,11 +115,12 @@ class SentimentModel(nn.Module):
             raise L.MMBError("SentimentModel runs on the GPU (libmmb); move it with .to('cuda')")
         if torch.is_grad_enabled() and (inputs.requires_grad or
                                         any(p.requires_grad for p in self.parameters())):
-            # differentiable forward (the e2e joint objective, simplesif.py:776-790):
-            # torch's GEMMs on the device carry the autograd graph
+            # differentiable forward (the e2e joint objective, simplesif.py:776-790)
             w1, b1, w2, b2 = _params(self)
-            x = F.linear(F.relu(F.linear(inputs.to(dev, torch.float32), w1, b1)), w2, b2)
-            return x.squeeze()
+            x = inputs.to(dev, torch.float32)
+            lead = x.shape[:-1]
+            y = _Regressor.apply(x.reshape(-1, x.shape[-1]), w1, b1, w2, b2)
+            return y.reshape(*lead, w2.shape[0]).squeeze()
         home = inputs.device
         x = inputs.detach().to(dev, torch.float32)
         lead = x.shape[:-1]

@@ -43,7 +43,7 @@ from torch.utils.data import DataLoader
 
 import latent as LT
 import mmb_lib as L
-from losses import _combine
+from losses import _combine, combine_weighted
 from models import AudioVisualGeneratorMultimodal
 from sentiment_model import SentimentData, SentimentModel, train_sentiment_for_latents
 from sif import get_sentence_embeddings, load_weights
@@ -140,19 +140,115 @@ class Objective:
             visual=LT.gauss_stats(torch.as_tensor(visual, device=dev, dtype=torch.float32),
                                   torch.as_tensor(visual_mask, device=dev, dtype=torch.float32)))
 
-    def log_prob(self, latents, out, j):
-        """get_log_prob_matrix(...) [B] for batch rows j of the split."""
+    def parts(self, latents, out, j):
+        """(word log-prob [B], Gaussian log-probs [K, B], keys) for batch rows j
+        (device work only: no host sync, so it can be captured in a graph)."""
         j = j.to(self.ids.device)
         word = LT.word_log_prob(latents, self.table, self.w[j], self.m[j], WORD_A, ids=self.ids[j])
-        wmin = word.detach().min().abs()
         keys = list(out.keys())
         lp = LT.gauss_log_prob(self.stats, keys, [out[k]["mu"] for k in keys],
                                [out[k]["sigma"] for k in keys], idx=j)
+        return word, lp, keys
+
+    def log_prob(self, latents, out, j):
+        """get_log_prob_matrix(...) [B] for batch rows j of the split."""
+        word, lp, keys = self.parts(latents, out, j)
+        wmin = word.detach().min().abs()
         if float(wmin) == np.inf:  # simplesif.py:517-523
             print("word inf")
             print(latents.size())
             sys.exit()
         return _combine(self.args, {k: lp[i] for i, k in enumerate(keys)}, word)
+
+    def log_prob_nocheck(self, latents, out, j):
+        """log_prob without the host-side inf checks, plus the values those
+        checks read: (log-prob [B], [word min |.|, per-key min |.| ...])."""
+        word, lp, keys = self.parts(latents, out, j)
+        mins = torch.cat([word.detach().min().abs().view(1), lp.detach().amin(dim=1).abs()])
+        return combine_weighted(self.args, {k: lp[i] for i, k in enumerate(keys)}, word), mins
+
+
+def check_step(out, mins_all, latents_size):
+    """The reference's per-step host checks, in its order, from one device
+    read: sigma < 1e-7 prints (simplesif.py:82-84 / 724-726), a word
+    log-prob of inf exits (simplesif.py:517-523), a Gaussian one of inf
+    exits (losses.py:258-264).  mins_all = [loss, sigma mins (K), word min,
+    Gaussian mins (K)]; returns the loss."""
+    v = mins_all.cpu().numpy()
+    K = len(out)
+    for (modality, d), m in zip(out.items(), v[1:1 + K]):
+        if float(m) < 1e-7:
+            print(d, "boo!")
+    if float(v[1 + K]) == np.inf:
+        print("word inf")
+        print(latents_size)
+        sys.exit()
+    bad = False
+    for k, m in zip(out.keys(), v[2 + K:]):
+        if float(m) == np.inf:
+            print(k, "inf")
+            bad = True
+    if bad:
+        sys.exit()
+    return float(v[0])
+
+
+USE_GRAPHS = os.environ.get("MMB_STEP_GRAPHS", "1") != "0"
+
+
+class StepGraphs:
+    """One optimisation step's device work -- generator forward, objective,
+    regressor, backward -- captured as a HIP graph per batch size and
+    replayed, so the ~100 small launches of a step cost one graph launch.
+
+    `body(j)` (j: a device index tensor) must do device work only and return
+    (out dict, tensor of the values the host checks read).  The optimiser step
+    stays eager (torch.optim, the reference's arithmetic), as do the host
+    checks, which read the step's values once per step like the reference's
+    float() calls.  Gradients: a replay overwrites the gradient buffers its
+    capture allocated (what zero_grad + backward produce); after a replay the
+    parameters' .grad are pointed at that graph's buffers.  Capture needs
+    warm-up passes; module buffers (BatchNorm running statistics) are
+    restored after them, so the first real step sees the same state as the
+    reference's."""
+
+    def __init__(self, body, modules, params, device):
+        self.body, self.modules, self.params, self.dev = body, modules, list(params), device
+        self.graphs = {}
+
+    def _capture(self, b):
+        dev = self.dev
+        j = torch.zeros(b, dtype=torch.int64, device=dev)
+        bufs = [x for m in self.modules for x in m.buffers()]
+        saved = [x.clone() for x in bufs]
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                for p in self.params:
+                    p.grad = None
+                self.body(j)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        with torch.no_grad():
+            for x, v in zip(bufs, saved):
+                x.copy_(v)
+        for p in self.params:
+            p.grad = None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            outs = self.body(j)
+        self.graphs[b] = (g, j, outs, [p.grad for p in self.params])
+
+    def __call__(self, j_host):
+        b = len(j_host)
+        if b not in self.graphs:
+            self._capture(b)
+        g, j, outs, grads = self.graphs[b]
+        j.copy_(j_host)
+        g.replay()
+        for p, gr in zip(self.params, grads):
+            p.grad = gr
+        return outs
 
 
 def _sigma_check(out):
@@ -179,11 +275,27 @@ def optimize_latents(args, train: bool, gen_model, embed_arr, dataloader, n_epoc
     start_time = time.time()
     losses = []
     all_valid_losses = []
+    graphs = None
+    if USE_GRAPHS:
+        def body(j):
+            out = gen_model(embeddings[j])
+            sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
+            lp, mins = objective.log_prob_nocheck(embeddings[j], out, j)
+            avg_log_prob = (-lp).mean()
+            avg_log_prob.backward()
+            return out, torch.cat([avg_log_prob.detach().view(1), sig, mins])
+
+        graphs = StepGraphs(body, [gen_model], grad_params, device)
     for i in range(n_epochs):
         epoch_loss = 0.
         iters = 0
         for j in _index_batches(dataloader):
             iters += 1
+            if graphs is not None:
+                out, vals = graphs(j)
+                epoch_loss += check_step(out, vals, embeddings[:len(j)].size())
+                optimizer.step()
+                continue
             optimizer.zero_grad()
             out = gen_model(embeddings[j])
             _sigma_check(out)
@@ -406,10 +518,35 @@ def main(argv=None):
         train_losses = []
         all_valid_losses = []
         N_EPOCHS = args["n_epochs"]
+        graphs = None
+        if USE_GRAPHS:
+            senti_labels = senti_train_data.sentiment
+            lw = args["likelihood_weight"]
+
+            def body(j):
+                out = gen_model(train_embed[j])
+                sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
+                lp, mins = train_obj.log_prob_nocheck(train_embed[j], out, j)
+                senti_loss = loss_function(senti_model(train_embed[j]), senti_labels[j])
+                if sentiment_train_idxes is not None:
+                    senti_loss = senti_loss * senti_mask[j]
+                senti_loss = senti_loss.mean(dim=-1)
+                loss = lw * (-lp) + (1 - lw) * senti_loss
+                lm = loss.mean()
+                lm.backward()
+                return out, torch.cat([lm.detach().view(1), sig, mins])
+
+            graphs = StepGraphs(body, [gen_model, senti_model], grad_params, device)
         for i in range(N_EPOCHS):
             epoch_loss = 0.
             iters = 0
             for j in _index_batches(dataloader):
+                if graphs is not None:
+                    iters += 1
+                    out, vals = graphs(j)
+                    epoch_loss += check_step(out, vals, train_embed[:len(j)].size())
+                    optimizer.step()
+                    continue
                 _, s_data = senti_train_data[j]
                 iters += 1
                 optimizer.zero_grad()

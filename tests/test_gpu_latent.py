@@ -178,10 +178,15 @@ def loss_values(text):
     return np.array(vals)
 
 
+@pytest.mark.parametrize("graphs", [True, False], ids=["graph_steps", "eager_steps"])
 @pytest.mark.parametrize("variant", list(VARIANTS))
-def test_cli_matches_reference_run(gpu, tmp_path, monkeypatch, variant):
+def test_cli_matches_reference_run(gpu, tmp_path, monkeypatch, variant, graphs):
+    """simplesif.main() against the reference CLI's own run; the optimisation
+    steps captured as HIP graphs (the default, simplesif.StepGraphs) and
+    launched eagerly."""
     import simplesif
 
+    monkeypatch.setattr(simplesif, "USE_GRAPHS", graphs)
     ref = json.load(open(os.path.join(GOLDEN, f"g9_cli_{variant}.json")))
     arr = np.load(os.path.join(GOLDEN, f"g9_cli_{variant}.npz"))
     dd = ref["data"]

@@ -192,3 +192,31 @@ def test_full_size_run_matches_reference(gpu, tmp_path, case, capsys):
         # after each reload the epoch-0 checkpoint is back: the next validation
         # is again above the first one, like the reference's
         assert all(v > vl[0] for v in vl[1:])
+
+
+@pytest.mark.parametrize("b,h,o", [(64, 100, 1), (4, 150, 1), (33, 100, 7)])
+def test_differentiable_forward_backward_vs_torch(gpu, b, h, o):
+    """The e2e objective's regressor term under autograd goes through
+    mmb_mlp_forward_train / mmb_mlp_backward: outputs and the gradients to the
+    inputs and every parameter equal torch autograd of the reference module
+    (sentiment_model.py:36-41) on the same device, within fp32 sum order."""
+    torch.manual_seed(b + h + o)
+    m = SM.SentimentModel(300, h, o).to(gpu)
+    ref = torch.nn.Sequential(torch.nn.Linear(300, h), torch.nn.ReLU(), torch.nn.Linear(h, o)).to(gpu)
+    with torch.no_grad():
+        ref[0].weight.copy_(m.hidden1.weight); ref[0].bias.copy_(m.hidden1.bias)
+        ref[2].weight.copy_(m.out.weight); ref[2].bias.copy_(m.out.bias)
+    x = torch.randn(b, 300, device=gpu, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    y = m(x)
+    yr = ref(x2).squeeze()
+    assert y.shape == yr.shape
+    np.testing.assert_allclose(y.detach().cpu().numpy(), yr.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    pairs = [(x.grad, x2.grad), (m.hidden1.weight.grad, ref[0].weight.grad),
+             (m.hidden1.bias.grad, ref[0].bias.grad), (m.out.weight.grad, ref[2].weight.grad),
+             (m.out.bias.grad, ref[2].bias.grad)]
+    for got, want in pairs:
+        np.testing.assert_allclose(got.cpu().numpy(), want.cpu().numpy(), rtol=1e-4, atol=1e-5)
