@@ -266,6 +266,34 @@ def time_fp32_projection(P, step, reps=3):
             "note": "mmb_mm2_project: fp32-input MFMA (exact f32 products), no fused removal"}
 
 
+def stream_uniform_ids(P, step, kbytes, reps=3):
+    """The stream kernel on the same workload with UNIFORM token ids over
+    [1, V): every text row a likely L2 / Infinity-Cache miss, so the
+    algorithmic-bytes roofline no longer counts Zipf cache hits."""
+    import torch
+
+    inp = step.inp
+    ids_u = torch.randint(1, step.V, step.ids.shape, dtype=torch.int32, device=step.ids.device)
+    run = lambda: P.mm2_stream(step.n, step.t, step.d, step.a, step.vd, inp["audio"], inp["visual"],
+                               ids32=ids_u, table=step.table, wtab32=inp["wtab"], s_half=True,
+                               out=(step.x, step.s, step.aux))
+    run()
+    evs = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        run()
+        b.record()
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    ms = sum(a.elapsed_time(b) for a, b in evs) / reps
+    ach = kbytes * step.n / (ms / 1e3) / 1e9
+    del ids_u
+    return {"avg_launch_ms": round(ms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "note": "same frames and table, token ids uniform over [1, V) instead of Zipf(1.1)"}
+
+
 def ragged_config(P, models, synth, dev, steps, warmup, U):
     """SURVEY §8d's second configs[3] run: Poisson(40) lengths clipped to
     [1, 64], padded with id 0 (weight 1.0) and -10 frames, T = 64."""
@@ -635,6 +663,7 @@ def main():
     extras = world == 1 and not args.only_main and kind == "synthetic"
     if extras:
         out["projection_fp32_mfma"] = time_fp32_projection(P, step)
+        out["stream_uniform_ids"] = stream_uniform_ids(P, step, kb)
     sample = None
     if not args.no_cpu_baseline and world == 1:
         n_cpu = args.cpu_sample if T <= 64 else max(1, args.cpu_sample * 40 // T)

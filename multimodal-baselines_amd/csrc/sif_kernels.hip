@@ -105,12 +105,24 @@ __device__ __forceinline__ void stage_token(const StreamArgs& a, int64_t i, int 
   }
 }
 
+// Token staging of the workgroup kernel.  In gather mode the tokens whose
+// row is table row 0 (id 0: the reference's pad / OOV index, ~72 % of a POM
+// transcript) are not staged: they are counted (c0) and their weights summed
+// (w0), and row 0 enters the sums once at the end as w0 * E0, c0 * E0,
+// c0 * E0^2 -- one load instead of c0.  The other tokens are compacted in
+// token order (wave ballots + a fixed-order prefix over the waves), so the
+// text loop runs over rows that carry new bytes only.  Out-of-range ids
+// (flagged) are dropped: they contribute nothing (sif_functions.py:8-15).
+constexpr int kStageIters = (kTokChunk + kNT - 1) / kNT;
+
 template <bool MM2, int VT, int VA, int VV>
 __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
   __shared__ int64_t s_off[kTokChunk];
   __shared__ float s_w[kTokChunk];
   __shared__ float s_red[(MM2 ? 4 : 1) * kRedFloats];
   __shared__ float s_cnt[kNT / kWave], s_sw[kNT / kWave];
+  __shared__ float s_c0[kNT / kWave], s_w0[kNT / kWave];
+  __shared__ int s_keep[kStageIters][kNT / kWave];
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), wave = tid / kWave;
@@ -128,22 +140,50 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
   const float* esrc = a.ids ? a.table : a.emb_dense;
   const bool split_emb = MM2 && (esrc != tsrc);
 
+  const bool gather = a.ids != nullptr;
   for (int64_t i = blockIdx.x; i < a.N; i += gridDim.x) {
     float num[VT], sx[VT], sxx[VT];
 #pragma unroll
     for (int e = 0; e < VT; ++e) num[e] = sx[e] = sxx[e] = 0.f;
-    float cntp = 0.f, swp = 0.f;
+    float cntp = 0.f, swp = 0.f, c0p = 0.f, w0p = 0.f;
 
     for (int t0 = 0; t0 < a.L; t0 += kTokChunk) {
       const int tl = min(kTokChunk, a.L - t0);
-      for (int t = tid; t < tl; t += kNT) {
-        int64_t off;
-        float w;
-        stage_token(a, i, t0 + t, off, w);
-        s_off[t] = off;
-        s_w[t] = w;
-        cntp += (w != 0.f) ? 1.f : 0.f;
-        swp += w;
+      int64_t off_k[kStageIters];
+      float w_k[kStageIters];
+      int rank_k[kStageIters];
+      bool keep_k[kStageIters];
+#pragma unroll
+      for (int k = 0; k < kStageIters; ++k) {
+        const int t = tid + k * kNT;
+        int64_t off = -1;
+        float w = 0.f;
+        if (t < tl) {
+          stage_token(a, i, t0 + t, off, w);
+          cntp += (w != 0.f) ? 1.f : 0.f;
+          swp += w;
+          if (gather && off == 0) {
+            c0p += 1.f;
+            w0p += w;
+          }
+        }
+        const bool keep = t < tl && (gather ? off > 0 : true);
+        const unsigned long long bal = __ballot(keep);
+        rank_k[k] = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) s_keep[k][wave] = __popcll(bal);
+        off_k[k] = off;
+        w_k[k] = w;
+        keep_k[k] = keep;
+      }
+      __syncthreads();
+      int nkeep = 0;
+#pragma unroll
+      for (int k = 0; k < kStageIters; ++k) {
+        for (int v = 0; v < kNT / kWave; ++v) {
+          if (keep_k[k] && v == wave) s_off[nkeep + rank_k[k]] = off_k[k];
+          if (keep_k[k] && v == wave) s_w[nkeep + rank_k[k]] = w_k[k];
+          nkeep += s_keep[k][v];
+        }
       }
       __syncthreads();
       if (actT) {
@@ -152,7 +192,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         // loads in flight together (a `continue` per token would wait on
         // each load right after its branch)
 #pragma unroll 4
-        for (int t = rT; t < tl; t += RT) {
+        for (int t = rT; t < nkeep; t += RT) {
           const float w = s_w[t];
           const int64_t off = s_off[t];
           const bool ok = off >= 0;
@@ -217,12 +257,17 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       }
     }
 
-    // count_nonzero(w) and sum(w): wave shuffle then fixed-order wave sum
+    // count_nonzero(w) and sum(w) (and the row-0 token count / weight sum):
+    // wave shuffle then fixed-order wave sum
     cntp = wave_sum(cntp);
     swp = wave_sum(swp);
+    c0p = wave_sum(c0p);
+    w0p = wave_sum(w0p);
     if (lane == 0) {
       s_cnt[wave] = cntp;
       s_sw[wave] = swp;
+      s_c0[wave] = c0p;
+      s_w0[wave] = w0p;
     }
     // round 1: text accumulators
     if (actT) {
@@ -237,22 +282,29 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       }
     }
     __syncthreads();
-    float cnt = 0.f, sw = 0.f;
+    float cnt = 0.f, sw = 0.f, c0 = 0.f, w0 = 0.f;
 #pragma unroll
     for (int w = 0; w < kNT / kWave; ++w) {
       cnt += s_cnt[w];
       sw += s_sw[w];
+      c0 += s_c0[w];
+      w0 += s_w0[w];
     }
     float smax = 0.f;  // max |sum| of this thread's part of the row (MMB2)
     for (int f = tid; f < a.D; f += kNT) {
       float n_ = 0.f;
       for (int r = 0; r < RT; ++r) n_ += s_red[r * a.D + f];
+      // row 0 once for its c0 tokens (gather mode; c0 = 0 otherwise)
+      const float e0 = (c0 > 0.f) ? a.table[f] : 0.f;
+      n_ = fmaf(w0, e0, n_);
       if constexpr (MM2) {
         float x1 = 0.f, x2 = 0.f;
         for (int r = 0; r < RT; ++r) {
           x1 += s_red[kRedFloats + r * a.D + f];
           x2 += s_red[2 * kRedFloats + r * a.D + f];
         }
+        x1 = fmaf(c0, e0, x1);
+        x2 = fmaf(c0 * e0, e0, x2);
         a.num_out[i * a.D + f] = n_ / cnt;  // x = the a2 row (sif_functions.py:55)
         a.s_out[i * a.Kp + f] = x1;
         a.s_out[i * a.Kp + a.D + f] = x2;
