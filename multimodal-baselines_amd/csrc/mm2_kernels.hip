@@ -309,9 +309,16 @@ constexpr int kXAbuf = 4; // A chunk ring (3 chunks in flight from HBM)
 constexpr int kXBbuf = 2; // B chunk ring (1 chunk in flight from L2)
 
 // 16-byte slot swizzle of a 64-byte LDS row (4 slots of 8 halves): row r
-// keeps data slot j at position j ^ swz(r), which spreads the 16 rows one
-// ds_read_b128 lane group touches over all 64 banks
-__host__ __device__ constexpr int x3_swz(int r) { return (r >> 2) & 3; }
+// keeps data slot j at position j ^ swz(r).  A 64-byte row puts slot
+// position p of row r on bank set 4 (r mod 4) + p, so a ds_read_b128 lane
+// group (16 lanes: {0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same +32)
+// is conflict-free iff its 16 (row mod 4, position) pairs differ.  For the
+// 16x16x32 fragment reads (lane l: row 16 t + (l & 15), data slot l >> 4)
+// the groups read rows {0-3, 12-15} at one slot and rows {4-11} at the
+// next: swz over the four 4-row groups of a 16-row tile = 0, 2, 3, 1 makes
+// every group conflict-free (the former (r >> 2) & 3 left them 2-way:
+// SQ_LDS_BANK_CONFLICT = 48 % of the kernel's LDS cycles, r02 counters).
+__host__ __device__ constexpr int x3_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
 // Weight split, written in the projection kernel's B chunk image order so the
 // kernel stages B with straight 16-byte global->LDS copies:
@@ -605,6 +612,143 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
   }
 }
 
+// Row-wise epilogue (D % 4 == 0, 16-byte aligned rows, 256 <= D < 320) of
+// the fp16x3 projection kernels: the raw accumulators of 64 rows at a time
+// go through the idle LDS rings (row stride 324 floats: the 4 row groups of
+// an MFMA store land on disjoint banks), then each wave finishes 8 whole rows
+// with 16-byte loads / stores: lane l owns columns 4l.. and 256 + 4l.. .  One
+// read of x serves the weighted text sum and the fused PC removal.  M rows
+// per workgroup; each wave row block (wr) holds NI 16-row tiles; a wave
+// finishes Q rows at a time (all their loads first).
+template <int CT, int NI, int Q = 4>
+__device__ __forceinline__ void x3_row_epilogue(f32x4 (&acc)[NI][CT], float* sacc, const float* s_rs,
+                                                int M, int wr, int wc, int lq, int lc, int wave,
+                                                int lane, int64_t n0, int64_t N, int D,
+                                                const float* __restrict__ num,
+                                                const float* __restrict__ aux,
+                                                const float* __restrict__ col_inv,
+                                                const float* __restrict__ c0,
+                                                const double* __restrict__ pc,
+                                                float* __restrict__ out, float* __restrict__ sif) {
+  constexpr int LDW = 64 * CT;
+  constexpr int kRS = 324;
+  const int U = D >> 2;                 // float4 units of a row
+  const bool u1 = lane + 64 < U;        // second unit (columns 256 + 4l..)
+  const int c0a = 4 * lane, c1a = 256 + 4 * min(lane, 15);  // acc columns (LDW <= 320)
+  const int c0x = 4 * min(lane, U - 1), c1x = 4 * min(lane + 64, U - 1);
+  float4 ci0, ci1, ca0, ca1;
+  {
+    const int cA = min(c0a, LDW - 4), cB = c1a;
+    ci0 = make_float4(col_inv[cA], col_inv[cA + 1], col_inv[cA + 2], col_inv[cA + 3]);
+    ca0 = make_float4(c0[cA], c0[cA + 1], c0[cA + 2], c0[cA + 3]);
+    ci1 = make_float4(col_inv[cB], col_inv[cB + 1], col_inv[cB + 2], col_inv[cB + 3]);
+    ca1 = make_float4(c0[cB], c0[cB + 1], c0[cB + 2], c0[cB + 3]);
+  }
+  double pv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pv[e] = 0.0;
+  if (pc) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pv[e] = lane < U ? pc[c0x + e] : 0.0;
+      pv[4 + e] = u1 ? pc[c1x + e] : 0.0;
+    }
+  }
+  const int lane_tot = (D - 256) >> 2, e_tot = (D - 256) & 3;  // column D in unit 1
+#pragma unroll 1
+  for (int p = 0; p < M / 64; ++p) {
+    __syncthreads();  // the rings' last reads / the previous pass's rows
+    // the wave row block holding rows [64 p, 64 p + 64): its tiles i with
+    // 16 i in that range, i.e. i / 4 == ip
+    const int ip = ((p * 64) % (NI * 16)) / 64;
+    if (wr == (p * 64) / (NI * 16)) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        if (i / 4 == ip)
+#pragma unroll
+          for (int t = 0; t < CT; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              sacc[((i % 4) * 16 + lq * 4 + j) * kRS + (wc * CT + t) * 16 + lc] = acc[i][t][j];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int h = 0; h < 8 / Q; ++h) {
+      // Q rows of this wave: all loads first
+      float4 xa[Q], xb[Q], aa[Q], ab[Q];
+      float cn[Q], tw[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int rl = p * 64 + wave * 8 + h * Q + q;
+        const int64_t rowc = min(n0 + rl, N - 1);
+        xa[q] = *reinterpret_cast<const float4*>(num + rowc * D + c0x);
+        xb[q] = *reinterpret_cast<const float4*>(num + rowc * D + c1x);
+        cn[q] = aux[rowc];
+        tw[q] = aux[N + rowc];
+        const float* sr = sacc + (rl - p * 64) * kRS;
+        aa[q] = *reinterpret_cast<const float4*>(sr + c0a);
+        ab[q] = *reinterpret_cast<const float4*>(sr + c1a);
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int rl = p * 64 + wave * 8 + h * Q + q;
+        const int64_t row = n0 + rl;
+        const float irs = s_rs[rl];
+        // y = unscaled product + (weighted text sum x * count, or the total
+        // weight sum_t w at column D) + c0 -- the tile epilogue's order
+        const float av[8] = {aa[q].x, aa[q].y, aa[q].z, aa[q].w, ab[q].x, ab[q].y, ab[q].z, ab[q].w};
+        const float civ[8] = {ci0.x, ci0.y, ci0.z, ci0.w, ci1.x, ci1.y, ci1.z, ci1.w};
+        const float cav[8] = {ca0.x, ca0.y, ca0.z, ca0.w, ca1.x, ca1.y, ca1.z, ca1.w};
+        const float xv[8] = {xa[q].x, xa[q].y, xa[q].z, xa[q].w, xb[q].x, xb[q].y, xb[q].z, xb[q].w};
+        float y[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int col = (e < 4 ? c0a : 256 + 4 * lane) + (e & 3);
+          const bool in = e < 4 ? lane < U : u1;
+          const float add = (in && col < D) ? text_sum(xv[e], cn[q]) : (col == D ? tw[q] : 0.f);
+          y[e] = av[e] * (civ[e] * irs) + add + cav[e];
+        }
+        // the total (column D) from its lane; cs = y / total
+        const float ysel = e_tot == 0 ? y[4] : e_tot == 1 ? y[5] : e_tot == 2 ? y[6] : y[7];
+        const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ysel), lane_tot));
+        const float rt = 1.f / tot;
+        float ss = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool in = e < 4 ? lane < U : u1;
+          y[e] *= rt;
+          if (in) ss = fmaf(y[e], y[e], ss);
+        }
+        const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
+        double dot = 0.0;
+        if (pc) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot = fma(static_cast<double>(xv[e]), pv[e], dot);
+          dot = wave_sum_dpp(dot);
+        }
+        if (row < N) {
+          float* orow = out + row * D;
+          if (lane < U)
+            *reinterpret_cast<float4*>(orow + c0x) =
+                make_float4(y[0] * inv, y[1] * inv, y[2] * inv, y[3] * inv);
+          if (u1)
+            *reinterpret_cast<float4*>(orow + c1x) =
+                make_float4(y[4] * inv, y[5] * inv, y[6] * inv, y[7] * inv);
+          if (pc) {
+            float* srow = sif + row * D;
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              o[e] = static_cast<float>(static_cast<double>(xv[e]) - dot * pv[e]);
+            if (lane < U) *reinterpret_cast<float4*>(srow + c0x) = make_float4(o[0], o[1], o[2], o[3]);
+            if (u1) *reinterpret_cast<float4*>(srow + c1x) = make_float4(o[4], o[5], o[6], o[7]);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int CT, bool ROWEPI, bool PIPE = false>
 __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
@@ -792,125 +936,8 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   __syncthreads();
 
   if constexpr (ROWEPI) {
-    // Row-wise epilogue (D % 4 == 0, 16-byte aligned rows): the raw
-    // accumulators of 64 rows at a time go through the idle LDS rings
-    // (row stride 324 floats: the 4 row groups of an MFMA store land on
-    // disjoint banks), then each wave finishes 8 whole rows with 16-byte
-    // loads / stores: lane l owns columns 4l.. and 256 + 4l.. .  One read of
-    // x serves the weighted text sum and the fused PC removal.
-    constexpr int kRS = 324;
-    float* sacc = reinterpret_cast<float*>(lds);
-    const int U = D >> 2;                 // float4 units of a row
-    const bool u1 = lane + 64 < U;        // second unit (columns 256 + 4l..)
-    const int c0a = 4 * lane, c1a = 256 + 4 * min(lane, 15);  // acc columns (LDW <= 320)
-    const int c0x = 4 * min(lane, U - 1), c1x = 4 * min(lane + 64, U - 1);
-    float4 ci0, ci1, ca0, ca1;
-    {
-      const int cA = min(c0a, LDW - 4), cB = c1a;
-      ci0 = make_float4(col_inv[cA], col_inv[cA + 1], col_inv[cA + 2], col_inv[cA + 3]);
-      ca0 = make_float4(c0[cA], c0[cA + 1], c0[cA + 2], c0[cA + 3]);
-      ci1 = make_float4(col_inv[cB], col_inv[cB + 1], col_inv[cB + 2], col_inv[cB + 3]);
-      ca1 = make_float4(c0[cB], c0[cB + 1], c0[cB + 2], c0[cB + 3]);
-    }
-    double pv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pv[e] = 0.0;
-    if (pc) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        pv[e] = lane < U ? pc[c0x + e] : 0.0;
-        pv[4 + e] = u1 ? pc[c1x + e] : 0.0;
-      }
-    }
-    const int lane_tot = (D - 256) >> 2, e_tot = (D - 256) & 3;  // column D in unit 1
-#pragma unroll 1
-    for (int p = 0; p < 2; ++p) {
-      __syncthreads();  // the rings' last reads / the previous pass's rows
-      if (wr == p) {
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2)
-#pragma unroll
-          for (int t = 0; t < CT; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              sacc[(i2 * 16 + lq * 4 + j) * kRS + (wc * CT + t) * 16 + lc] = acc[i2][t][j];
-      }
-      __syncthreads();
-#pragma unroll 1
-      for (int h = 0; h < 2; ++h) {
-        // 4 rows of this wave: all loads first
-        float4 xa[4], xb[4], aa[4], ab[4];
-        float cn[4], tw[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rl = p * 64 + wave * 8 + h * 4 + q;
-          const int64_t rowc = min(n0 + rl, N - 1);
-          xa[q] = *reinterpret_cast<const float4*>(num + rowc * D + c0x);
-          xb[q] = *reinterpret_cast<const float4*>(num + rowc * D + c1x);
-          cn[q] = aux[rowc];
-          tw[q] = aux[N + rowc];
-          const float* sr = sacc + (rl - p * 64) * kRS;
-          aa[q] = *reinterpret_cast<const float4*>(sr + c0a);
-          ab[q] = *reinterpret_cast<const float4*>(sr + c1a);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rl = p * 64 + wave * 8 + h * 4 + q;
-          const int64_t row = n0 + rl;
-          const float irs = s_rs[rl];
-          // y = unscaled product + (weighted text sum x * count, or the total
-          // weight sum_t w at column D) + c0 -- the tile epilogue's order
-          const float av[8] = {aa[q].x, aa[q].y, aa[q].z, aa[q].w, ab[q].x, ab[q].y, ab[q].z, ab[q].w};
-          const float civ[8] = {ci0.x, ci0.y, ci0.z, ci0.w, ci1.x, ci1.y, ci1.z, ci1.w};
-          const float cav[8] = {ca0.x, ca0.y, ca0.z, ca0.w, ca1.x, ca1.y, ca1.z, ca1.w};
-          const float xv[8] = {xa[q].x, xa[q].y, xa[q].z, xa[q].w, xb[q].x, xb[q].y, xb[q].z, xb[q].w};
-          float y[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int col = (e < 4 ? c0a : 256 + 4 * lane) + (e & 3);
-            const bool in = e < 4 ? lane < U : u1;
-            const float add = (in && col < D) ? text_sum(xv[e], cn[q]) : (col == D ? tw[q] : 0.f);
-            y[e] = av[e] * (civ[e] * irs) + add + cav[e];
-          }
-          // the total (column D) from its lane; cs = y / total
-          const float ysel = e_tot == 0 ? y[4] : e_tot == 1 ? y[5] : e_tot == 2 ? y[6] : y[7];
-          const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ysel), lane_tot));
-          const float rt = 1.f / tot;
-          float ss = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bool in = e < 4 ? lane < U : u1;
-            y[e] *= rt;
-            if (in) ss = fmaf(y[e], y[e], ss);
-          }
-          const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
-          double dot = 0.0;
-          if (pc) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) dot = fma(static_cast<double>(xv[e]), pv[e], dot);
-            dot = wave_sum_dpp(dot);
-          }
-          if (row < N) {
-            float* orow = out + row * D;
-            if (lane < U)
-              *reinterpret_cast<float4*>(orow + c0x) =
-                  make_float4(y[0] * inv, y[1] * inv, y[2] * inv, y[3] * inv);
-            if (u1)
-              *reinterpret_cast<float4*>(orow + c1x) =
-                  make_float4(y[4] * inv, y[5] * inv, y[6] * inv, y[7] * inv);
-            if (pc) {
-              float* srow = sif + row * D;
-              float o[8];
-#pragma unroll
-              for (int e = 0; e < 8; ++e)
-                o[e] = static_cast<float>(static_cast<double>(xv[e]) - dot * pv[e]);
-              if (lane < U) *reinterpret_cast<float4*>(srow + c0x) = make_float4(o[0], o[1], o[2], o[3]);
-              if (u1) *reinterpret_cast<float4*>(srow + c1x) = make_float4(o[4], o[5], o[6], o[7]);
-            }
-          }
-        }
-      }
-    }
+    x3_row_epilogue<CT, 4>(acc, reinterpret_cast<float*>(lds), s_rs, kXM, wr, wc, lq, lc, wave, lane,
+                           n0, N, D, num, aux, col_inv, c0, pc, out, sif);
     return;
   }
   // epilogue (as mm2_project_kernel): unscale, add weighted text sum + c0,
