@@ -620,8 +620,12 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
 // read of x serves the weighted text sum and the fused PC removal.  M rows
 // per workgroup; each wave row block (wr) holds NI 16-row tiles; a wave
 // finishes Q rows at a time (all their loads first).
-template <int CT, int NI, int Q = 4>
-__device__ __forceinline__ void x3_row_epilogue(f32x4 (&acc)[NI][CT], float* sacc, const float* s_rs,
+// LAYOUT 0: waves (wr, wc) = 2 x 4, a wave holds rows wr*64 + 16 i, columns
+// (wc*CT + t)*16 (acc[NI][CT]); LAYOUT 1: waves 4 x 2, rows wr*32 + 16 i,
+// columns (wc*NT + t)*16 (acc[2][NT], NT = 10); LAYOUT 2: waves 4 x 2 of a
+// 256-row tile, rows wr*64 + 16 i (acc[4][NT]).
+template <int CT, int NI, int Q = 4, int LAYOUT = 0, int NT = CT>
+__device__ __forceinline__ void x3_row_epilogue(f32x4 (&acc)[NI][NT], float* sacc, const float* s_rs,
                                                 int M, int wr, int wc, int lq, int lc, int wave,
                                                 int lane, int64_t n0, int64_t N, int D,
                                                 const float* __restrict__ num,
@@ -660,16 +664,38 @@ __device__ __forceinline__ void x3_row_epilogue(f32x4 (&acc)[NI][CT], float* sac
     __syncthreads();  // the rings' last reads / the previous pass's rows
     // the wave row block holding rows [64 p, 64 p + 64): its tiles i with
     // 16 i in that range, i.e. i / 4 == ip
-    const int ip = ((p * 64) % (NI * 16)) / 64;
-    if (wr == (p * 64) / (NI * 16)) {
+    if constexpr (LAYOUT == 0) {
+      const int ip = ((p * 64) % (NI * 16)) / 64;
+      if (wr == (p * 64) / (NI * 16)) {
 #pragma unroll
-      for (int i = 0; i < NI; ++i)
-        if (i / 4 == ip)
+        for (int i = 0; i < NI; ++i)
+          if (i / 4 == ip)
 #pragma unroll
-          for (int t = 0; t < CT; ++t)
+            for (int t = 0; t < CT; ++t)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                sacc[((i % 4) * 16 + lq * 4 + j) * kRS + (wc * CT + t) * 16 + lc] = acc[i][t][j];
+      }
+    } else if constexpr (LAYOUT == 2) {
+      if (wr == p) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              sacc[((i % 4) * 16 + lq * 4 + j) * kRS + (wc * CT + t) * 16 + lc] = acc[i][t][j];
+              sacc[(i * 16 + lq * 4 + j) * kRS + (wc * NT + t) * 16 + lc] = acc[i][t][j];
+      }
+    } else {
+      if ((wr >> 1) == p) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              sacc[((wr & 1) * 32 + i * 16 + lq * 4 + j) * kRS + (wc * NT + t) * 16 + lc] = acc[i][t][j];
+      }
     }
     __syncthreads();
 #pragma unroll 1
@@ -749,7 +775,11 @@ __device__ __forceinline__ void x3_row_epilogue(f32x4 (&acc)[NI][CT], float* sac
   }
 }
 
-template <int CT, bool ROWEPI, bool PIPE = false>
+// DIAG (timing-only builds, wrong outputs; MMB_PROJ_DIAG): bit 0 skips the
+// epilogue (accumulators kept live), bit 1 stages A chunk 0 every time
+// (L2-resident A), bit 2 B chunk 0 every time, bit 3 drops the MFMAs (the
+// fragment reads kept live)
+template <int CT, bool ROWEPI, bool PIPE = false, int DIAG = 0>
 __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
     const _Float16* __restrict__ img, const float* __restrict__ col_inv,
@@ -789,14 +819,16 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
   }
   auto stage_a = [&](int c) {
-    const int cc = min(c, nch - 1);
+    if ((DIAG & 64) && c >= 3) return;
+    const int cc = (DIAG & 2) ? 0 : min(c, nch - 1);
     _Float16* dst = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
 #pragma unroll
     for (int q = 0; q < AQ; ++q)
       glds16(asrc[q] + cc * kXK, dst + (q * kXT + wave * 64) * 8);
   };
   auto stage_b = [&](int c) {
-    const int cc = min(c, nch - 1);
+    if ((DIAG & 32) && c >= 2) return;
+    const int cc = (DIAG & 4) ? 0 : min(c, nch - 1);
     const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
     _Float16* dst = bring + (c & (kXBbuf - 1)) * BBUF;
 #pragma unroll
@@ -831,7 +863,18 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * AQ + BQ) : "memory");
     __builtin_amdgcn_s_barrier();
     half8 bh0[CT], bl0[CT], bh1[CT], bl1[CT], ah0, al0, ah1, al1;
+    if constexpr ((DIAG & 16) != 0) {
+      const half8 z = {};
+      ah0 = al0 = ah1 = al1 = z;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) bh0[t] = bl0[t] = bh1[t] = bl1[t] = z;
+    }
     auto rd_b = [&](int c, half8 (&bh)[CT], half8 (&bl)[CT]) {
+      if constexpr ((DIAG & 16) != 0) {
+#pragma unroll
+        for (int t = 0; t < CT; ++t) asm volatile("" : "+v"(bh[t]), "+v"(bl[t]));
+        return;
+      }
       const _Float16* b = bring + (c & (kXBbuf - 1)) * BBUF;
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
@@ -842,6 +885,10 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
       }
     };
     auto rd_a = [&](int c, int i, half8& ah, half8& al) {
+      if constexpr ((DIAG & 16) != 0) {
+        asm volatile("" : "+v"(ah), "+v"(al));
+        return;
+      }
       const _Float16* a = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
       const int row = wr * 64 + i * 16 + lc;
       const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
@@ -850,6 +897,12 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     };
     auto tile = [&](int i, const half8& ah, const half8& al, const half8 (&bh)[CT],
                     const half8 (&bl)[CT]) {
+      if constexpr ((DIAG & 8) != 0) {
+        asm volatile("" ::"v"(ah), "v"(al));
+#pragma unroll
+        for (int t = 0; t < CT; ++t) asm volatile("" ::"v"(bh[t]), "v"(bl[t]));
+        return;
+      }
 #pragma unroll
       for (int t = 0; t < CT; ++t) {
         acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[t], acc[i][t], 0, 0, 0);
@@ -934,6 +987,13 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   }  // PIPE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) asm volatile("" ::"v"(acc[i][t]));
+    return;
+  }
 
   if constexpr (ROWEPI) {
     x3_row_epilogue<CT, 4>(acc, reinterpret_cast<float*>(lds), s_rs, kXM, wr, wc, lq, lc, wave, lane,
@@ -1059,6 +1119,263 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   }
 }
 
+
+// Variant 3 (r02): A (the row sums) straight from HBM into registers, B (the
+// weight image) through a 3-slot LDS ring.  The K-loop ablation of the
+// variant-2 kernel (tools/proj_diag.py, r02d) showed its staging latency-bound:
+// the A and B LDS-DMA copies alone took 2.26 ms of its 3.57, A's 7.3 GB only
+// two chunks ahead because the 2 x 40 KB B ring + 4 x 16 KB A ring fill the
+// LDS.  Here the waves are 4 (rows) x 2 (columns), a wave 32 rows x 160
+// columns (2 x 10 tiles of v_mfma_f32_16x16x32_f16): its A fragments are its
+// own rows (16 bytes per lane per plane and row tile, shared by the two
+// column waves through L2), loaded AD chunks ahead into rotating register
+// buffers by inline-asm loads (hidden from hipcc's vmcnt bookkeeping so the
+// LDS-DMA stream of B is never drained), and the whole 120 KB ring holds B,
+// two chunks ahead.  One barrier per chunk: B(c) landed for every wave, and
+// every wave's reads of the slot B(c+2) overwrites are done.
+//   issue order per chunk c: B(c+2) (5 copies per thread), A(c+AD) (4 loads)
+constexpr int kX3cBslots = 3;
+template <int CT>
+constexpr size_t x3c_lds_bytes() {
+  return kX3cBslots * x3_bbuf_halves<CT>() * sizeof(_Float16) + kXM * sizeof(float);
+}
+
+__device__ __forceinline__ void gload16_asm(half8& v, const _Float16* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+}
+
+template <int AD, int DIAG = 0>
+__global__ __launch_bounds__(kXT) void mm2_project_x3c_kernel(
+    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
+    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
+    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
+    const double* __restrict__ pc, float* __restrict__ sif) {
+  static_assert(AD == 3, "vmcnt counts below are written for AD = 3");
+  constexpr int CT = 5, NT = 10;
+  constexpr int BBUF = x3_bbuf_halves<CT>();
+  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 5 copies per thread per B chunk
+  static_assert(BQ == 5, "staging split");
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  _Float16* bring = lds;
+  float* s_rs = reinterpret_cast<float*>(lds + kX3cBslots * BBUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lq = lane >> 4, lc = lane & 15;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
+  const int nch = Kp / kXK;
+
+  // lane's A fragment rows (rows past N re-read row N-1, never stored):
+  // row tile i -> row wr*32 + 16 i + lc, k offset 8 lq of each chunk
+  const _Float16* arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t r = min(n0 + wr * 32 + i * 16 + lc, N - 1);
+    arow[i] = S + r * 2 * Kp + lq * 8;
+  }
+  auto load_a = [&](int c, half8 (&h)[2], half8 (&l)[2]) {
+    const int cc = (DIAG & 2) ? 0 : min(c, nch - 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      gload16_asm(h[i], arow[i] + cc * kXK);
+      gload16_asm(l[i], arow[i] + Kp + cc * kXK);
+    }
+  };
+  auto stage_b = [&](int c) {
+    const int cc = min(c, nch - 1);
+    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
+    _Float16* dst = bring + (c % kX3cBslots) * BBUF;
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, dst + (q * kXT + wave * 64) * 8);
+  };
+
+  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
+
+  f32x4 acc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  half8 a0h[2], a0l[2], a1h[2], a1l[2], a2h[2], a2l[2], a3h[2], a3l[2];
+  stage_b(0);
+  stage_b(1);
+  load_a(0, a0h, a0l);
+  load_a(1, a1h, a1l);
+  load_a(2, a2h, a2l);
+
+  // chunk c: B(c) in ring slot c % 3, A(c) in (ah, al); A(c + 3) is loaded
+  // into (nh, nl), the buffer chunk c - 1 consumed
+  auto chunk = [&](int c, half8 (&ah)[2], half8 (&al)[2], half8 (&nh)[2], half8 (&nl)[2]) {
+    // B(c) and A(c) landed for this wave: ops issued after them are at most
+    // A(c+2) + B(c+1), A(c+3)... = 13 (chunk 0: A1, A2 = 8)
+    if (c == 0) {
+      asm volatile("s_waitcnt vmcnt(8)" : "+v"(ah[0]), "+v"(ah[1]), "+v"(al[0]), "+v"(al[1])::"memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(13)" : "+v"(ah[0]), "+v"(ah[1]), "+v"(al[0]), "+v"(al[1])::"memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    stage_b(c + 2);
+    load_a(c + 3, nh, nl);
+    const _Float16* b = bring + (c % kX3cBslots) * BBUF;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = (wc * NT + t) * 16 + lc;
+      const int bo = col * kXK + ((lq ^ x3_swz(col)) * 8);
+      const half8 bh = *reinterpret_cast<const half8*>(b + bo);
+      const half8 bl = *reinterpret_cast<const half8*>(b + (64 * CT) * kXK + bo);
+      if constexpr ((DIAG & 8) != 0) {
+        asm volatile("" ::"v"(bh), "v"(bl), "v"(ah[0]), "v"(al[0]), "v"(ah[1]), "v"(al[1]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][t], 0, 0, 0);
+        }
+      }
+    }
+  };
+#pragma unroll 1
+  for (int c = 0; c < nch; c += 4) {
+    chunk(c, a0h, a0l, a3h, a3l);
+    if (c + 1 < nch) chunk(c + 1, a1h, a1l, a0h, a0l);
+    if (c + 2 < nch) chunk(c + 2, a2h, a2l, a1h, a1l);
+    if (c + 3 < nch) chunk(c + 3, a3h, a3l, a2h, a2l);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) asm volatile("" ::"v"(acc[i][t]));
+    return;
+  }
+  x3_row_epilogue<CT, 2, 4, 1, NT>(acc, reinterpret_cast<float*>(lds), s_rs, kXM, wr, wc, lq, lc, wave,
+                                   lane, n0, N, D, num, aux, col_inv, c0, pc, out, sif);
+}
+
+
+// Variant 4 (r02): 256-row tiles.  The weight image is staged once per 256
+// rows instead of per 128 (the K-loop ablation, r02d: the B copies cost as
+// much as streaming A from HBM); A (32 KB) and B (40 KB) chunks in 2-slot
+// rings (144 KB), one chunk ahead; 8 waves as 4 (rows) x 2 (columns), a wave
+// 64 rows x 160 columns (4 x 10 tiles of v_mfma_f32_16x16x32_f16, 160
+// accumulator registers).  The row-wise epilogue in four 64-row passes.
+constexpr int kX4M = 256;
+template <int CT>
+constexpr size_t x3d_lds_bytes() {
+  return 2 * (x3_bbuf_halves<CT>() + 2 * kX4M * kXK) * sizeof(_Float16) + kX4M * sizeof(float);
+}
+
+template <int DIAG = 0>
+__global__ __launch_bounds__(kXT) void mm2_project_x3d_kernel(
+    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
+    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
+    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
+    const double* __restrict__ pc, float* __restrict__ sif) {
+  constexpr int CT = 5, NT = 10, NI = 4, M = kX4M;
+  constexpr int BBUF = x3_bbuf_halves<CT>();
+  constexpr int ABUF = 2 * M * kXK;
+  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 5
+  constexpr int AQ = ABUF * 2 / 16 / kXT;  // 4
+  static_assert(BQ == 5 && AQ == 4, "staging split");
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  _Float16* bring = lds;
+  _Float16* aring = lds + 2 * BBUF;
+  float* s_rs = reinterpret_cast<float*>(aring + 2 * ABUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lq = lane >> 4, lc = lane & 15;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * M;
+  const int nch = Kp / kXK;
+
+  // A piece g = q * 512 + tid: plane g >> 10, row (g >> 2) & 255, LDS slot
+  // position g & 3 <- data slot (g & 3) ^ swz(row)
+  const _Float16* asrc[AQ];
+#pragma unroll
+  for (int q = 0; q < AQ; ++q) {
+    const int g = q * kXT + tid;
+    const int plane = g >> 10, row = (g >> 2) & (M - 1);
+    const int64_t r = min(n0 + row, N - 1);
+    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
+  }
+  auto stage = [&](int c) {
+    const int cc = min(c, nch - 1);
+    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
+    _Float16* bd = bring + (c & 1) * BBUF;
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, bd + (q * kXT + wave * 64) * 8);
+    _Float16* ad = aring + (c & 1) * ABUF;
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) glds16(asrc[q] + cc * kXK, ad + (q * kXT + wave * 64) * 8);
+  };
+
+  if (tid < M) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
+
+  f32x4 acc[NI][NT];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed (this wave's copies, then everyone's by the barrier);
+    // the barrier also retires every read of the slots chunk c + 1 overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < nch) stage(c + 1);
+    const _Float16* a = aring + (c & 1) * ABUF;
+    const _Float16* b = bring + (c & 1) * BBUF;
+    half8 ah[NI], al[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int row = wr * 64 + i * 16 + lc;
+      const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
+      ah[i] = *reinterpret_cast<const half8*>(a + ao);
+      al[i] = *reinterpret_cast<const half8*>(a + M * kXK + ao);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = (wc * NT + t) * 16 + lc;
+      const int bo = col * kXK + ((lq ^ x3_swz(col)) * 8);
+      const half8 bh = *reinterpret_cast<const half8*>(b + bo);
+      const half8 bl = *reinterpret_cast<const half8*>(b + (64 * CT) * kXK + bo);
+      if constexpr ((DIAG & 8) != 0) {
+        asm volatile("" ::"v"(bh), "v"(bl));
+      } else {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][t], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr ((DIAG & 8) != 0) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) asm volatile("" ::"v"(ah[i]), "v"(al[i]));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) asm volatile("" ::"v"(acc[i][t]));
+    return;
+  }
+  x3_row_epilogue<CT, NI, 1, 2, NT>(acc, reinterpret_cast<float*>(lds), s_rs, M, wr, wc, lq, lc, wave,
+                                    lane, n0, N, D, num, aux, col_inv, c0, pc, out, sif);
+}
+
 template <int CT>
 constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(float); }
 
@@ -1076,12 +1393,46 @@ static bool proj_row_epilogue() {
   return v;
 }
 
-static int proj_variant() {
-  static const int v = [] {
-    const char* e = getenv("MMB_PROJ_VARIANT");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
+static int proj_diag() {  // re-read per launch: timing sweeps flip it in one process
+  const char* e = getenv("MMB_PROJ_DIAG");
+  return e ? atoi(e) : 0;
+}
+
+static int proj_variant() {  // re-read per launch (in-process A/B sweeps)
+  const char* e = getenv("MMB_PROJ_VARIANT");
+  return e ? atoi(e) : 2;
+}
+
+template <int CT, int D_>
+static void launch_diag1(int grid, size_t ldsb, const _Float16* s, const float* num, const float* aux,
+                         const _Float16* img, const float* ci, const float* c0, int64_t n, int kp,
+                         int d, float* out, const double* pc, float* sif, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true, true, D_>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+    attr = true;
+  }
+  mm2_project_x3b_kernel<CT, true, true, D_><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp,
+                                                                         d, out, pc, sif);
+}
+
+// timing-only ablations of the default kernel (MMB_PROJ_DIAG; see the DIAG bits)
+template <int CT>
+static void launch_diag(int v, int grid, size_t ldsb, const _Float16* s, const float* num,
+                        const float* aux, const _Float16* img, const float* ci, const float* c0,
+                        int64_t n, int kp, int d, float* out, const double* pc, float* sif,
+                        hipStream_t stream) {
+#define MMB_DIAG_CASE(D_) \
+  case D_: launch_diag1<CT, D_>(grid, ldsb, s, num, aux, img, ci, c0, n, kp, d, out, pc, sif, stream); break;
+  switch (v) {
+    MMB_DIAG_CASE(1) MMB_DIAG_CASE(2) MMB_DIAG_CASE(3) MMB_DIAG_CASE(4) MMB_DIAG_CASE(8)
+    MMB_DIAG_CASE(9) MMB_DIAG_CASE(11) MMB_DIAG_CASE(13) MMB_DIAG_CASE(17) MMB_DIAG_CASE(25)
+    MMB_DIAG_CASE(33) MMB_DIAG_CASE(41) MMB_DIAG_CASE(65) MMB_DIAG_CASE(73) MMB_DIAG_CASE(97)
+    MMB_DIAG_CASE(105) MMB_DIAG_CASE(121) MMB_DIAG_CASE(113)
+    default: break;
+  }
+#undef MMB_DIAG_CASE
 }
 
 template <int CT>
@@ -1119,7 +1470,60 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
     const bool rowepi = CT == 5 && d >= 256 && d % 4 == 0 && a16(num) && a16(out) &&
                         (sif == nullptr || a16(sif)) && proj_row_epilogue();
     const bool pipe = proj_variant() == 2;
-    if (rowepi && pipe) {
+    if constexpr (CT == 5) {
+      if (rowepi && proj_variant() == 4) {
+        constexpr size_t ldsd = x3d_lds_bytes<CT>();
+        static_assert(ldsd <= 160 * 1024, "x3d rings exceed LDS");
+        static bool attr_d = false;
+        if (!attr_d) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3d_kernel<0>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsd));
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3d_kernel<1>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsd));
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3d_kernel<9>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsd));
+          attr_d = true;
+        }
+        const int g4 = static_cast<int>(ceil_div(n, kX4M));
+        const int dg = proj_diag();
+        if (dg == 1)
+          mm2_project_x3d_kernel<1><<<g4, kXT, ldsd, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        else if (dg == 9)
+          mm2_project_x3d_kernel<9><<<g4, kXT, ldsd, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        else
+          mm2_project_x3d_kernel<0><<<g4, kXT, ldsd, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        MMB_LAUNCH_CHECK();
+        return MMB_OK;
+      }
+      if (rowepi && proj_variant() == 3) {
+        constexpr size_t ldsc = x3c_lds_bytes<CT>();
+        static_assert(ldsc <= 160 * 1024, "x3c ring exceeds LDS");
+        static_assert(64 * 324 * sizeof(float) <= kX3cBslots * x3_bbuf_halves<CT>() * sizeof(_Float16),
+                      "row epilogue scratch exceeds the B ring");
+        static bool attr_c = false;
+        if (!attr_c) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3c_kernel<3>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsc));
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3c_kernel<3, 1>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsc));
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3c_kernel<3, 9>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsc));
+          attr_c = true;
+        }
+        const int dg = proj_diag();
+        if (dg == 1)
+          mm2_project_x3c_kernel<3, 1><<<grid, kXT, ldsc, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        else if (dg == 9)
+          mm2_project_x3c_kernel<3, 9><<<grid, kXT, ldsc, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        else
+          mm2_project_x3c_kernel<3><<<grid, kXT, ldsc, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        MMB_LAUNCH_CHECK();
+        return MMB_OK;
+      }
+    }
+    if (rowepi && pipe && proj_diag() != 0) {
+      if constexpr (CT == 5) launch_diag<CT>(proj_diag(), grid, ldsb, s, num, aux, img, ci, c0, n, kp, d, out, pc, sif, stream);
+    } else if (rowepi && pipe) {
       mm2_project_x3b_kernel<CT, true, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
                                                                           n, kp, d, out, pc, sif);
     } else if (pipe) {

@@ -262,6 +262,28 @@ def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
     assert M.row_rel_err(s4.cpu().numpy(), s1.cpu().numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("variant", ["3", "4"])
+@pytest.mark.parametrize("N", [700, 128, 129, 1000])
+def test_projection_variants_bit_identical(gpu, N, variant, monkeypatch):
+    """Variant 3 (A fragments straight from HBM into registers, B through a
+    3-slot LDS ring, 4 x 2 waves) and variant 4 (256-row tiles) sum every 16x16
+    tile in the same MFMA order as the default kernel and share its epilogue:
+    MMB2 and PC-removed rows bit-identical, ragged last tiles included."""
+    T, V = 40, 5000
+    inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=41, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks())
+    s1, m1 = [t.clone() for t in step.run()]
+    monkeypatch.setenv("MMB_PROJ_VARIANT", variant)
+    step.sif.zero_()
+    step.mmb2.zero_()
+    s3, m3 = step.run()
+    torch.cuda.synchronize()
+    assert torch.equal(m1, m3)
+    assert torch.equal(s1, s3)
+
+
 def test_zero_weight_rows_sif_raises_mmb2_finite(gpu):
     """A row whose SIF weights are all zero: its a2 row is 0/0 = NaN (numpy,
     sif_functions.py:55) and the reference's TruncatedSVD rejects the split
@@ -311,7 +333,8 @@ np.savez(sys.argv[1], sif=s.cpu().numpy(), mmb2=m.cpu().numpy())
 
 
 @pytest.mark.parametrize("env", [{"MMB_PROJ_VARIANT": "0", "MMB_STREAM_POLICY": "0"},
-                                 {"MMB_PROJ_VARIANT": "1"},
+                                 {"MMB_PROJ_VARIANT": "1"}, {"MMB_PROJ_VARIANT": "3"},
+                                 {"MMB_PROJ_VARIANT": "4"},
                                  {"MMB_STREAM_POLICY": "7", "MMB_STREAM_GRID_MULT": "8"},
                                  {"MMB_PROJ_ROWEPI": "0"}])
 def test_non_default_kernel_variants_agree(gpu, tmp_path, env):
