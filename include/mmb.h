@@ -84,6 +84,21 @@ int mmb_gram_part(const float* num, const float* cnt, int64_t n, int64_t n_plan,
 int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate, const void* ws,
                     hipStream_t stream);
 
+/* The same Gram on the int8 matrix pipe, for x rows (cnt = 1) whose column
+ * bounds colmax[j] = max_i |x[i,j]| (float bits) are known: every value as a
+ * 30-bit fixed-point integer of its column's power-of-two bound, cut into
+ * four int8 digits; digit-pair products of level <= 4 summed exactly (int32
+ * per 64-row step, then f64).  Not bit-equal to mmb_gram: ~1e-10 relative
+ * (the PC within 6e-11 of the reference's on the golden splits).  d % 4 == 0,
+ * d <= 304; ws as for mmb_gram_workspace_bytes(n, d).  mmb_colmax computes
+ * the bounds (accumulate = 0 zeroes colmax first).
+ * replaces: the X^T X inside sif_functions.compute_pc's TruncatedSVD
+ *   /root/reference/sif_functions.py:58-67                                   */
+int mmb_colmax(const float* x, int64_t n, int d, uint32_t* colmax, int accumulate,
+               hipStream_t stream);
+int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
+                int accumulate, void* ws, hipStream_t stream);
+
 /* z0[d,k] = X^T omega  (omega [n,k] float64) — start block of the transposed
  * randomized-SVD branch (n < d).                                             */
 int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d, const double* omega,
@@ -164,7 +179,14 @@ int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const floa
                    const float* text_dense, const float* emb_dense, const float* w_dense,
                    const float* audio, const float* visual, int64_t n, int t, int d, int a,
                    int vd, float* num_out, void* s_out, int s_half, float* aux_out,
-                   int32_t* flag, hipStream_t stream);
+                   int32_t* flag, uint32_t* colmax, void* colmax_ws, hipStream_t stream);
+
+/* colmax (nullable; d <= 640): the column bounds max_i |num[i,:]| of the a2
+ * rows as float bits, the input of mmb_gram_i8 -- a by-product of the stream
+ * kernel (per-wave running maxima into colmax_ws, then one fixed-order reduce
+ * launch) instead of a second pass over x.  colmax_ws: scratch of
+ * mmb_mm2_colmax_ws_bytes(d) bytes.                                          */
+size_t mmb_mm2_colmax_ws_bytes(int d);
 
 /* Padded width (row stride) of the per-utterance sums: roundup(2(d+a+vd), 32). */
 int mmb_mm2_k(int d, int a, int vd);

@@ -244,6 +244,254 @@ __global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict
   }
 }
 
+
+// ------------------------------------------------------------------ Gram i8
+// G = X^T X on the int8 matrix pipe (v_mfma_i32_16x16x64_i8: 64x the fp64
+// MFMA rate per operation), for the fused step's x rows.  Each value becomes
+// a 30-bit fixed-point integer of its column's power-of-two bound 2^e_j
+// (colmax: max |x| of the column):  v = rint(x 2^(30 - e_j)), |v| < 2^30,
+// cut into four balanced base-256 digits (the low three sign-extended bytes
+// in [-128, 127], the top one in [-64, 64]):  v = sum_a d_a 2^(8 (3 - a)).
+// G_ij = 2^(e_i + e_j - 60) sum_rows v_i v_j, keeping the digit pairs of
+// level a + b <= 4 (13 of 16; the dropped (2,3), (3,2), (3,3) weigh 2^8 and
+// 1 against the top pair's 2^48).  Per 64-row k-step the levels are summed
+// EXACTLY in three int32 accumulators, H = acc_0 2^8 + acc_1 (< 2^27),
+// M = acc_2 2^8 + acc_3 (< 2^30), L = acc_4, then added in f64 as
+// H 2^-20 + M 2^-36 + L 2^-44.  The only roundings are v's (2^-31 of the
+// column bound per value) and the f64 accumulation: G within 1e-10 of the
+// exact f64 Gram on the golden splits (7e-10 on heavy-tailed t(3) columns),
+// the PC within 6e-11 of the reference's (CPU restatement:
+// oracle.sif_oracle.sliced_gram; the digit format was chosen by measuring
+// it: base-128 digits of 33-bit values needed 22 pairs for the same error,
+// because values far below their column's bound live in the low digits).
+// Structure as gram_tri_kernel: a pair of workgroups per row range (same
+// XCD), each with half of the 16x16 tiles of the upper triangle; per 64-row
+// chunk every thread turns its (feature, 16-row) items into digit bytes in
+// LDS ([digit][feature][4 slots of 16 rows], the conflict-free slot swizzle
+// of the 16x16x32 f16 fragment reads, whose lane map this read shares), then
+// each wave runs 13 MFMAs per tile and the f64 update.
+constexpr int kGiNT = 512;
+constexpr int kGiRows = 64;
+constexpr int kGiF = 320;       // padded feature count (D <= 320)
+constexpr int kGiDig = 4;       // base-256 digits per value
+constexpr int kGiMaxTiles = 12; // tiles per wave (<= 96 per workgroup: d <= 304)
+constexpr int kGiItems = kGiF / 16 * 16 * 4;  // (feature, 16-row slot) items per chunk
+
+__host__ __device__ constexpr int gi_swz(int f) { return (0x78 >> (2 * ((f >> 2) & 3))) & 3; }
+
+using i32x4 = __attribute__((ext_vector_type(4))) int;
+
+__device__ __forceinline__ int gi_exp(unsigned bits) {
+  const float m = __uint_as_float(bits);
+  if (!(m > 0.f) || !isfinite(m)) return 0;
+  int e;
+  frexpf(m, &e);  // m = f 2^e, f in [0.5, 1): |x| <= m < 2^e
+  return e;
+}
+
+// the four digit bytes of v = rint(x 2^(30 - e)) (two's complement bytes of
+// the balanced digits, low digit first)
+__device__ __forceinline__ void gi_digits(float x, int e, int (&b)[kGiDig]) {
+  int v = static_cast<int>(rintf(ldexpf(x, 30 - e)));
+#pragma unroll
+  for (int a = 0; a < kGiDig - 1; ++a) {
+    const int d = __builtin_amdgcn_sbfe(v, 0, 8);  // sign-extended low byte
+    b[a] = v;                                        // its byte = d's byte
+    v = (v - d) >> 8;
+  }
+  b[kGiDig - 1] = v;
+}
+
+// bytes 0 of a, b, c, d -> one dword (row order a, b, c, d)
+__device__ __forceinline__ unsigned gi_pack4(int a, int b, int c, int d) {
+  const unsigned ab = __builtin_amdgcn_perm(static_cast<unsigned>(b), static_cast<unsigned>(a), 0x0c0c0400u);
+  const unsigned cd = __builtin_amdgcn_perm(static_cast<unsigned>(d), static_cast<unsigned>(c), 0x0c0c0400u);
+  return __builtin_amdgcn_perm(cd, ab, 0x05040100u);
+}
+
+__global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict__ x,
+                                                       const unsigned* __restrict__ colmax,
+                                                       int64_t N, int D, int nt, int R,
+                                                       int64_t chunk, int xcd_map,
+                                                       double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dig[];  // [4][kGiF][64]
+  const int T = nt * (nt + 1) / 2;
+  int half, range;
+  if (xcd_map) {
+    const int b = blockIdx.x;
+    half = (b >> 3) & 1;
+    range = (b & 7) + 8 * (b >> 4);
+  } else {
+    half = blockIdx.x & 1;
+    range = blockIdx.x >> 1;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t0 = half * ((T + 1) / 2), t1 = half ? T : (T + 1) / 2;
+  // this wave's tiles: a contiguous run of the triangle (row-major)
+  const int per = (t1 - t0 + (kGiNT / kWave) - 1) / (kGiNT / kWave);
+  const int q0 = t0 + wave * per;
+  int ti[kGiMaxTiles], tj[kGiMaxTiles];
+  int ntl = 0;
+#pragma unroll
+  for (int q = 0; q < kGiMaxTiles; ++q) {
+    ti[q] = tj[q] = 0;
+    if (q < per && q0 + q < t1) {
+      tri_tile(q0 + q, nt, ti[q], tj[q]);
+      ntl = q + 1;
+    }
+  }
+  double acc[kGiMaxTiles][4];
+#pragma unroll
+  for (int q = 0; q < kGiMaxTiles; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[q][e] = 0.0;
+
+  const int64_t r0 = range * chunk;
+  const int64_t r1 = min(N, r0 + chunk);
+  const int nchunks = static_cast<int>(r1 > r0 ? (r1 - r0 + kGiRows - 1) / kGiRows : 0);
+  const int nf = nt * 16;  // features turned into digits (zero past D)
+  const int nitems = nf * 4;
+  constexpr int kIt = (kGiItems + kGiNT - 1) / kGiNT;  // items per thread (<= 3)
+  // item it = f + nf * kq: feature f, rows 16 kq .. 16 kq + 15 of the chunk
+  int it_f[kIt], it_kq[kIt], it_e[kIt];
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int it = tid + kGiNT * u;
+    it_f[u] = it < nitems ? it % nf : 0;
+    it_kq[u] = it < nitems ? it / nf : 0;
+    it_e[u] = (it < nitems && it_f[u] < D) ? gi_exp(colmax[it_f[u]]) : 0;
+  }
+  // the range's rows through a buffer descriptor: rows past the range read 0
+  // (hardware range check), the per-row step is a scalar offset, and each
+  // item needs one 32-bit VGPR offset (64-bit addresses for the 48 prefetched
+  // values would not fit beside the f64 sums)
+  const int nrec = __builtin_amdgcn_readfirstlane(static_cast<int>((r1 > r0 ? r1 - r0 : 0) * D * 4));
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + r0 * D), 0, nrec, 0x00020000);
+  int it_off[kIt];
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int it = tid + kGiNT * u;
+    // padding features / missing items read past the record count: 0
+    it_off[u] = (it < nitems && it_f[u] < D) ? (it_kq[u] * 16 * D + it_f[u]) * 4 : 0x7ffffff0;
+  }
+  float xv[kIt][16];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
+#pragma unroll
+      for (int u = 0; u < kIt; ++u)
+        xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
+    }
+  };
+  auto slice = [&]() {
+#pragma unroll
+    for (int u = 0; u < kIt; ++u) {
+      const int it = tid + kGiNT * u;
+      if (it < nitems) {
+        unsigned w[kGiDig][4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          int b0[kGiDig], b1[kGiDig], b2[kGiDig], b3[kGiDig];
+          gi_digits(xv[u][4 * g + 0], it_e[u], b0);
+          gi_digits(xv[u][4 * g + 1], it_e[u], b1);
+          gi_digits(xv[u][4 * g + 2], it_e[u], b2);
+          gi_digits(xv[u][4 * g + 3], it_e[u], b3);
+          // plane a holds digit a from the top (b[kGiDig - 1 - a])
+#pragma unroll
+          for (int a = 0; a < kGiDig; ++a)
+            w[a][g] = gi_pack4(b0[kGiDig - 1 - a], b1[kGiDig - 1 - a], b2[kGiDig - 1 - a],
+                               b3[kGiDig - 1 - a]);
+        }
+        const int f = it_f[u], slot = it_kq[u] ^ gi_swz(f);
+#pragma unroll
+        for (int a = 0; a < kGiDig; ++a)
+          *reinterpret_cast<uint4*>(s_dig + ((a * kGiF + f) * 4 + slot) * 16) =
+              make_uint4(w[a][0], w[a][1], w[a][2], w[a][3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one item's digits live at a time
+    }
+  };
+
+  if (nchunks > 0) load(0);
+  for (int c = 0; c < nchunks; ++c) {
+    __syncthreads();  // every wave done reading the previous chunk's digits
+    slice();
+    if (c + 1 < nchunks) load(c + 1);
+    __syncthreads();
+    // lane l: feature (l & 15) of the tile's block, 16 rows of slot (l >> 4)
+    const int lf = lane & 15, lsl = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < kGiMaxTiles; ++q) {
+      if (q < ntl) {
+        const int fa = ti[q] * 16 + lf, fb = tj[q] * 16 + lf;
+        i32x4 A[kGiDig], B[kGiDig];
+#pragma unroll
+        for (int a = 0; a < kGiDig; ++a) {
+          A[a] = *reinterpret_cast<const i32x4*>(s_dig + ((a * kGiF + fa) * 4 + (lsl ^ gi_swz(fa))) * 16);
+          B[a] = *reinterpret_cast<const i32x4*>(s_dig + ((a * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
+        }
+        const i32x4 z = {0, 0, 0, 0};
+        i32x4 H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[0], z, 0, 0, 0);
+        H <<= 8;
+        H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[1], H, 0, 0, 0);
+        H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[0], H, 0, 0, 0);
+        i32x4 M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[2], z, 0, 0, 0);
+        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[1], M, 0, 0, 0);
+        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[0], M, 0, 0, 0);
+        M <<= 8;
+        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[3], M, 0, 0, 0);
+        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[2], M, 0, 0, 0);
+        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[1], M, 0, 0, 0);
+        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3], B[0], M, 0, 0, 0);
+        i32x4 Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[3], z, 0, 0, 0);
+        Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[2], Lo, 0, 0, 0);
+        Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3], B[1], Lo, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[q][e] = fma(static_cast<double>(H[e]), 0x1p-20, acc[q][e]);
+          acc[q][e] = fma(static_cast<double>(M[e]), 0x1p-36, acc[q][e]);
+          acc[q][e] = fma(static_cast<double>(Lo[e]), 0x1p-44, acc[q][e]);
+        }
+      }
+      // one tile's operands live at a time (12 tiles' f64 sums + the next
+      // chunk's x values already hold 144 registers)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // partials in gram_tri_kernel's layout, scaled by 2^(e_i + e_j) (exact):
+  // C/D map of the 16x16 integer MFMA: row 4 (lane >> 4) + e, column lane & 15
+  double* pr = part + static_cast<int64_t>(range) * T * 256;
+  const int lc = lane & 15, lr = 4 * (lane >> 4);
+#pragma unroll
+  for (int q = 0; q < kGiMaxTiles; ++q) {
+    if (q < ntl) {
+      const int fj = tj[q] * 16 + lc;
+      const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int fi = ti[q] * 16 + lr + e;
+        const int ei = fi < D ? gi_exp(colmax[fi]) : 0;
+        pr[static_cast<int64_t>(q0 + q) * 256 + (lr + e) * 16 + lc] = ldexp(acc[q][e], ei + ej);
+      }
+    }
+  }
+}
+
+// colmax[j] = max_i |x[i, j]| as float bits (atomicMax on the bits of a
+// non-negative float orders like the float); NaNs are skipped.
+__global__ void colmax_kernel(const float* __restrict__ x, int64_t N, int D, int64_t rows_per_block,
+                              unsigned* __restrict__ colmax) {
+  const int64_t r0 = blockIdx.x * rows_per_block;
+  const int64_t r1 = min(N, r0 + rows_per_block);
+  for (int j = threadIdx.x; j < D; j += blockDim.x) {
+    float m = 0.f;
+    for (int64_t r = r0; r < r1; ++r) m = fmaxf(m, fabsf(x[r * D + j]));
+    if (m > 0.f) atomicMax(colmax + j, __float_as_uint(m));
+  }
+}
+
 __global__ void gram_tri_reduce_kernel(const double* __restrict__ part, int D, int nt, int R,
                                        int accumulate, double* __restrict__ g) {
   const int T = nt * (nt + 1) / 2;
@@ -1260,6 +1508,17 @@ static bool gram2_ok(const float* num, int d) {
   return d % 4 == 0 && d <= 320 && (reinterpret_cast<uintptr_t>(num) & 15) == 0;
 }
 
+
+static size_t gram_i8_lds() {
+  const size_t lds = kGiDig * kGiF * kGiRows;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr = true;
+  }
+  return lds;
+}
 }  // namespace mmb
 
 using namespace mmb;
@@ -1291,6 +1550,40 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
                                                          p.chunk, p.xcd, part);
   MMB_LAUNCH_CHECK();
   gram_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, p.nb, p.npairs, p.S, accumulate, g);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+
+extern "C" int mmb_colmax(const float* x, int64_t n, int d, uint32_t* colmax, int accumulate,
+                          hipStream_t stream) {
+  MMB_REQUIRE(x && colmax && n >= 0 && d > 0);
+  if (!accumulate) {
+    const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  if (n == 0) return MMB_OK;
+  const int64_t rpb = 256;
+  const int64_t blocks = ceil_div(n, rpb);
+  colmax_kernel<<<static_cast<int>(blocks), d < 256 ? ((d + 63) / 64) * 64 : 256, 0, stream>>>(
+      x, n, d, rpb, colmax);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
+                           int accumulate, void* ws, hipStream_t stream) {
+  MMB_REQUIRE(x && colmax && g && ws && n >= 0 && d > 0 && d <= 304 && d % 4 == 0);
+  const Gram2Plan q = gram2_plan(n, d);
+  MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
+  // int32 level sums are per 64-row k-step, so any range length is safe
+  double* part = static_cast<double*>(ws);
+  gram_i8_kernel<<<2 * q.R, kGiNT, gram_i8_lds(), stream>>>(x, colmax, n, d, q.nt, q.R, q.chunk,
+                                                             q.xcd, part);
+  MMB_LAUNCH_CHECK();
+  const int64_t total = static_cast<int64_t>(d) * d;
+  gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, q.nt, q.R,
+                                                                                   accumulate, g);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

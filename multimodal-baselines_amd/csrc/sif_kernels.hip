@@ -39,6 +39,7 @@ struct StreamArgs {
   float* aux_out;
   int32_t* flag;
   int s_half;
+  float* cmax_part;  // per-wave (wave kernel) / per-workgroup running max |x| rows [P][D], or null
 };
 
 template <int VEC>
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
   const bool split_emb = MM2 && (esrc != tsrc);
 
   const bool gather = a.ids != nullptr;
+  float cmx0 = 0.f, cmx1 = 0.f;  // running max |x| of columns tid, tid + kNT (MMB2)
   for (int64_t i = blockIdx.x; i < a.N; i += gridDim.x) {
     float num[VT], sx[VT], sxx[VT];
 #pragma unroll
@@ -305,7 +307,9 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         }
         x1 = fmaf(c0, e0, x1);
         x2 = fmaf(c0 * e0, e0, x2);
-        a.num_out[i * a.D + f] = n_ / cnt;  // x = the a2 row (sif_functions.py:55)
+        const float xf = n_ / cnt;
+        a.num_out[i * a.D + f] = xf;  // x = the a2 row (sif_functions.py:55)
+        if (f < kNT) cmx0 = fmaxf(cmx0, fabsf(xf)); else cmx1 = fmaxf(cmx1, fabsf(xf));
         a.s_out[i * a.Kp + f] = x1;
         a.s_out[i * a.Kp + a.D + f] = x2;
         smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
@@ -376,6 +380,11 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       }
     }
     __syncthreads();
+  }
+  if (MM2 && a.cmax_part) {  // this workgroup's column bounds (mmb_gram_i8)
+    float* pr = a.cmax_part + static_cast<int64_t>(blockIdx.x) * a.D;
+    if (tid < a.D) pr[tid] = cmx0;
+    if (tid + kNT < a.D) pr[tid + kNT] = cmx1;
   }
 }
 
@@ -460,6 +469,9 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
   constexpr bool split_emb = MM2 && SPLIT;  // weighted sum over a different dense tensor
   const bool gather = a.ids != nullptr;
 
+  float4 cmx[CT];  // running max |x| of this lane's columns (MMB2, mmb_gram_i8)
+#pragma unroll
+  for (int c = 0; c < CT; ++c) cmx[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t i = wid; i < a.N; i += nw) {
     // stage: lane t <- token t (row id or -1, weight)
     int rid = -1;
@@ -584,7 +596,10 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       for (int c = 0; c < CT; ++c) {
         const int u = lane + kWave * c;
         if (u < UT) {
-          stnt4<NTS>(a.num_out + i * a.D + 4 * u, div4(num[c], cnt));  // x = the a2 row
+          const float4 xr = div4(num[c], cnt);
+          stnt4<NTS>(a.num_out + i * a.D + 4 * u, xr);  // x = the a2 row
+          cmx[c] = make_float4(fmaxf(cmx[c].x, fabsf(xr.x)), fmaxf(cmx[c].y, fabsf(xr.y)),
+                               fmaxf(cmx[c].z, fabsf(xr.z)), fmaxf(cmx[c].w, fabsf(xr.w)));
           put(4 * u, sx[c]);
           put(a.D + 4 * u, sxx[c]);
         }
@@ -630,6 +645,31 @@ __global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
       if (lane == 0 && a.cnt_out) a.cnt_out[i] = cnt;
     }
   }
+  if (MM2 && a.cmax_part) {  // this wave's column bounds (mmb_gram_i8)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int u = lane + kWave * c;
+      if (u < UT) st4(a.cmax_part + wid * a.D + 4 * u, cmx[c]);
+    }
+  }
+}
+
+// colmax[f] = max over the P partial rows (float bits; non-negative floats
+// order like their bits), fixed order.  16 row groups per column, LDS reduce.
+__global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __restrict__ part, int P,
+                                                            int D, unsigned* __restrict__ colmax) {
+  __shared__ float s_m[16][64];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + c;
+  float m = 0.f;
+  if (f < D)
+    for (int r = g; r < P; r += 16) m = fmaxf(m, part[static_cast<int64_t>(r) * D + f]);
+  s_m[g][c] = m;
+  __syncthreads();
+  if (g == 0 && f < D) {
+    for (int k = 1; k < 16; ++k) m = fmaxf(m, s_m[k][c]);
+    colmax[f] = __float_as_uint(m);
+  }
 }
 
 // Load/store policy of the MMB2 wave kernel: bit 0 = frame loads
@@ -669,11 +709,16 @@ static int stream_grid_mult() {
   return m;
 }
 
+// rows of the column-bound partials (one per wave / workgroup of a launch)
+constexpr int kCmaxRows = 8192;
+
 template <bool MM2, int CT, int CA, int CV>
-static int launch_wave(const StreamArgs& a, hipStream_t stream) {
+static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nullptr) {
   const int64_t blocks = ceil_div(a.N, 4);
-  const int grid_cap = stream_grid_mult() * stream_cu_count(stream);
+  int grid_cap = stream_grid_mult() * stream_cu_count(stream);
+  if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
+  if (parts) *parts = grid * 4;
   switch (MM2 ? stream_policy() & 7 : 0) {
     case 1: launch_wave_v<MM2, CT, CA, CV, 2, true, false>(a, grid, stream); break;
     case 2: launch_wave_v<MM2, CT, CA, CV, 2, false, true>(a, grid, stream); break;
@@ -740,8 +785,10 @@ int stream_cu_count(hipStream_t stream) {
 }
 
 template <bool MM2, int VT, int VA, int VV>
-static int launch_stream(const StreamArgs& a, hipStream_t stream) {
-  const int grid = stream_grid(a.N, 6, stream);
+static int launch_stream(const StreamArgs& a, hipStream_t stream, int* parts = nullptr) {
+  int grid = stream_grid(a.N, 6, stream);
+  if (a.cmax_part && grid > kCmaxRows) grid = kCmaxRows;
+  if (parts) *parts = grid;
   utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
@@ -843,21 +890,43 @@ __global__ __launch_bounds__(256) void split_rows_kernel(float* __restrict__ s,
   }
 }
 
+extern "C" size_t mmb_mm2_colmax_ws_bytes(int d) {
+  return static_cast<size_t>(kCmaxRows) * (d > 0 ? d : 0) * sizeof(float);
+}
+
 extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
                               const float* wtab32, const float* text_dense,
                               const float* emb_dense, const float* w_dense, const float* audio,
                               const float* visual, int64_t n, int t, int d, int a_, int vd,
                               float* num_out, void* s_out, int s_half, float* aux_out,
-                              int32_t* flag, hipStream_t stream) {
+                              int32_t* flag, uint32_t* colmax, void* colmax_ws,
+                              hipStream_t stream) {
   MMB_REQUIRE(n >= 0 && t > 0 && d > 0 && a_ > 0 && vd > 0);
+  MMB_REQUIRE(colmax == nullptr || (colmax_ws != nullptr && d <= 2 * kNT));
   MMB_REQUIRE(audio && visual && num_out && s_out && aux_out && (s_half == 0 || s_half == 1));
   if (ids) {
     MMB_REQUIRE(table && v > 0 && (wtab32 || w_dense));
   } else {
     MMB_REQUIRE(text_dense && emb_dense && w_dense);
   }
-  if (n == 0) return MMB_OK;
+  if (n == 0) {
+    if (colmax) {
+      const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return MMB_OK;
+  }
   StreamArgs s{};
+  s.cmax_part = colmax ? static_cast<float*>(colmax_ws) : nullptr;
+  int parts = 0;
+  // the column bounds: max over the launch's per-wave / per-workgroup rows
+  auto reduce_colmax = [&](int rc) {
+    if (rc != MMB_OK || !colmax) return rc;
+    colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(
+        static_cast<const float*>(colmax_ws), parts, d, colmax);
+    MMB_LAUNCH_CHECK();
+    return static_cast<int>(MMB_OK);
+  };
   s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.w_dense = w_dense;
   s.text_dense = text_dense; s.emb_dense = emb_dense; s.audio = audio; s.visual = visual;
   s.N = n; s.L = t; s.D = d; s.A = a_; s.Vd = vd; s.Kp = mmb_mm2_k(d, a_, vd);
@@ -870,14 +939,14 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
       aligned16(s_out)) {
     const int sel = (d > 256 ? 4 : 0) | (a_ > 256 ? 2 : 0) | (vd > 256 ? 1 : 0);
     switch (sel) {
-      case 7: return launch_wave<true, 2, 2, 2>(s, stream);
-      case 6: return launch_wave<true, 2, 2, 1>(s, stream);
-      case 5: return launch_wave<true, 2, 1, 2>(s, stream);
-      case 4: return launch_wave<true, 2, 1, 1>(s, stream);
-      case 3: return launch_wave<true, 1, 2, 2>(s, stream);
-      case 2: return launch_wave<true, 1, 2, 1>(s, stream);
-      case 1: return launch_wave<true, 1, 1, 2>(s, stream);
-      default: return launch_wave<true, 1, 1, 1>(s, stream);
+      case 7: return reduce_colmax(launch_wave<true, 2, 2, 2>(s, stream, &parts));
+      case 6: return reduce_colmax(launch_wave<true, 2, 2, 1>(s, stream, &parts));
+      case 5: return reduce_colmax(launch_wave<true, 2, 1, 2>(s, stream, &parts));
+      case 4: return reduce_colmax(launch_wave<true, 2, 1, 1>(s, stream, &parts));
+      case 3: return reduce_colmax(launch_wave<true, 1, 2, 2>(s, stream, &parts));
+      case 2: return reduce_colmax(launch_wave<true, 1, 2, 1>(s, stream, &parts));
+      case 1: return reduce_colmax(launch_wave<true, 1, 1, 2>(s, stream, &parts));
+      default: return reduce_colmax(launch_wave<true, 1, 1, 1>(s, stream, &parts));
     }
   }
   MMB_REQUIRE(d / (vt ? 4 : 1) <= kNT && a_ / (va ? 4 : 1) <= kNT && vd / (vv ? 4 : 1) <= kNT);
@@ -885,15 +954,16 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   const int sel = (vt ? 4 : 0) | (va ? 2 : 0) | (vv ? 1 : 0);
   int rc;
   switch (sel) {
-    case 7: rc = launch_stream<true, 4, 4, 4>(s, stream); break;
-    case 6: rc = launch_stream<true, 4, 4, 1>(s, stream); break;
-    case 5: rc = launch_stream<true, 4, 1, 4>(s, stream); break;
-    case 4: rc = launch_stream<true, 4, 1, 1>(s, stream); break;
-    case 3: rc = launch_stream<true, 1, 4, 4>(s, stream); break;
-    case 2: rc = launch_stream<true, 1, 4, 1>(s, stream); break;
-    case 1: rc = launch_stream<true, 1, 1, 4>(s, stream); break;
-    default: rc = launch_stream<true, 1, 1, 1>(s, stream); break;
+    case 7: rc = launch_stream<true, 4, 4, 4>(s, stream, &parts); break;
+    case 6: rc = launch_stream<true, 4, 4, 1>(s, stream, &parts); break;
+    case 5: rc = launch_stream<true, 4, 1, 4>(s, stream, &parts); break;
+    case 4: rc = launch_stream<true, 4, 1, 1>(s, stream, &parts); break;
+    case 3: rc = launch_stream<true, 1, 4, 4>(s, stream, &parts); break;
+    case 2: rc = launch_stream<true, 1, 4, 1>(s, stream, &parts); break;
+    case 1: rc = launch_stream<true, 1, 1, 4>(s, stream, &parts); break;
+    default: rc = launch_stream<true, 1, 1, 1>(s, stream, &parts); break;
   }
+  rc = reduce_colmax(rc);
   if (rc != MMB_OK || !s_half) return rc;
   split_rows_kernel<<<static_cast<unsigned>(n), 256, s.Kp * sizeof(float), stream>>>(
       s.s_out, aux_out + 2 * n, s.Kp);

@@ -37,6 +37,8 @@ SIGNATURES = {
     "mmb_gram_workspace_bytes": (_S, [_L, _I]),
     "mmb_gram": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
     "mmb_gram_part": (_I, [_P, _P, _L, _L, _I, _I, _P, _P]),
+    "mmb_colmax": (_I, [_P, _L, _I, _P, _I, _P]),
+    "mmb_gram_i8": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
     "mmb_gram_finish": (_I, [_L, _I, _P, _I, _P, _P]),
     "mmb_xt_omega": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
     "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
@@ -52,7 +54,8 @@ SIGNATURES = {
     "mmb_mm2_k": (_I, [_I, _I, _I]),
     "mmb_mm2_ldw": (_I, [_I]),
     "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _I,
-                            _P, _P, _P]),
+                            _P, _P, _P, _P, _P]),
+    "mmb_mm2_colmax_ws_bytes": (_S, [_I]),
     "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "mmb_mm2_split_bytes": (_S, [_I, _I, _I]),
     "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),

@@ -14,6 +14,8 @@ Data layout in HBM (one utterance per row, row-major, fp32 unless noted):
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -126,6 +128,30 @@ def gram(num: torch.Tensor, cnt: torch.Tensor | None, G: torch.Tensor | None = N
     if ws is None or not ws.fits(n, d):
         ws = GramWorkspace(n, d, num.device)
     L.call("mmb_gram", L.ptr(num), L.ptr(cnt), n, d, L.ptr(G), int(accumulate), L.ptr(ws.buf),
+           L.stream_ptr())
+    return G
+
+
+def colmax(x: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
+    """Column bounds max_i |x[i, j]| as float bits (int32 view of uint32) for
+    the int8 Gram (mmb_colmax)."""
+    n, d = x.shape
+    if out is None:
+        out = torch.empty((d,), dtype=torch.int32, device=x.device)
+    L.call("mmb_colmax", L.ptr(x), n, d, L.ptr(out), int(accumulate), L.stream_ptr())
+    return out
+
+
+def gram_i8(x: torch.Tensor, cmax: torch.Tensor, G: torch.Tensor | None = None,
+            accumulate: bool = False, ws: GramWorkspace | None = None) -> torch.Tensor:
+    """G = x^T x on the int8 matrix pipe (mmb_gram_i8): 33-bit fixed point per
+    column bound, ~1e-10 relative to the exact f64 Gram."""
+    n, d = x.shape
+    if G is None:
+        G = torch.empty((d, d), dtype=torch.float64, device=x.device)
+    if ws is None or not ws.fits(n, d):
+        ws = GramWorkspace(n, d, x.device)
+    L.call("mmb_gram_i8", L.ptr(x), L.ptr(cmax), n, d, L.ptr(G), int(accumulate), L.ptr(ws.buf),
            L.stream_ptr())
     return G
 
@@ -308,12 +334,14 @@ def ctypes_ptr_array(ptrs):
 
 def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=None,
                text_dense=None, emb_dense=None, w_dense=None, flag=None, out=None,
-               s_half: bool = True):
+               s_half: bool = True, colmax=None, colmax_ws=None):
     """a6-a8 frame sums.  Returns (x, s, aux): x [n, d] the a2 rows (weighted
     text sum / count_nonzero(w)), aux [3, n] (count, total weight, row scale).
     s_half=True (default) writes s as fp16 [n, 2*kp] (hi | lo planes of the
     row-scaled sums, the x3 projection's A operand); s_half=False writes fp32
-    [n, kp] for the fp32-MFMA projection."""
+    [n, kp] for the fp32-MFMA projection.  With `colmax` ([d] int32) and
+    `colmax_ws` (mmb_mm2_colmax_ws_bytes) the kernel also writes the column
+    bounds max_i |x[i, j]| (float bits) for mmb_gram_i8."""
     kp, _ = mm2_dims(d, a, vd)
     dev = audio.device
     if out is None:
@@ -326,7 +354,8 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
     V = table.shape[0] if table is not None else 0
     L.call("mmb_mm2_stream", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32), L.ptr(text_dense),
            L.ptr(emb_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
-           L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag), L.stream_ptr())
+           L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag), L.ptr(colmax),
+           L.ptr(colmax_ws), L.stream_ptr())
     return num, s, aux
 
 
@@ -455,7 +484,8 @@ class FusedStep:
 
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
-                 side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True):
+                 side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True,
+                 gram_kind: str | None = None):
         self.inp = inputs
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
@@ -491,6 +521,22 @@ class FusedStep:
         self.aux_flat = torch.empty((3 * self.n,), dtype=torch.float32, device=dev)
         self.gram_parts = len(self.bounds) > 1 and self.d % 4 == 0 and self.d <= 320
         self.fused_remove = fuse_remove and len(self.bounds) == 1 and npc == 1 and self.s_half
+        # Gram of the one-chunk step: "i8" (mmb_gram_i8, int8 digits of the
+        # column-bounded fixed-point x, ~1e-10 of exact; the bounds come from
+        # the stream kernel) or "f64" (mmb_gram, exact f64 products).
+        # MMB_GRAM overrides the default (A/B runs).
+        if gram_kind is None:
+            gram_kind = os.environ.get("MMB_GRAM", "i8")
+        if gram_kind not in ("i8", "f64"):
+            raise ValueError(f"gram_kind must be 'i8' or 'f64', not {gram_kind!r}")
+        self.gram_i8 = (gram_kind == "i8" and len(self.bounds) == 1 and self.d % 4 == 0
+                        and self.d <= 304)
+        if self.gram_i8:
+            self.colmax = torch.zeros((self.d,), dtype=torch.int32, device=dev)
+            nb = L.query("mmb_mm2_colmax_ws_bytes", self.d)
+            self.colmax_ws = torch.empty((nb + 15) // 16 * 16, dtype=torch.uint8, device=dev)
+        else:
+            self.colmax = self.colmax_ws = None
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
         self.main = None
@@ -534,7 +580,8 @@ class FusedStep:
         mm2_stream(r1 - r0, self.t, self.d, self.a, self.vd, inp["audio"][r0:r1],
                    inp["visual"][r0:r1], ids32=self.ids[r0:r1], table=self.table,
                    wtab32=inp["wtab"], flag=self.flag, s_half=self.s_half,
-                   out=(self.x[r0:r1], self.s[r0:r1], self.aux_of(c)))
+                   out=(self.x[r0:r1], self.s[r0:r1], self.aux_of(c)),
+                   colmax=self.colmax, colmax_ws=self.colmax_ws)
 
     def _consume_chunk(self, c: int):
         r0, r1 = self.bounds[c]
@@ -543,6 +590,8 @@ class FusedStep:
         if self.gram_parts:
             L.call("mmb_gram_part", L.ptr(self.x[r0:r1]), None, r1 - r0,
                    self.step_rows, self.d, int(c > 0), L.ptr(self.gws.buf), L.stream_ptr())
+        elif self.gram_i8:  # one chunk
+            gram_i8(self.x, self.colmax, self.G, ws=self.gws)
         else:
             gram(self.x[r0:r1], None, self.G, accumulate=c > 0, ws=self.gws)
 
@@ -579,7 +628,10 @@ class FusedStep:
             self._stream_chunk(0)  # every CU
         if self.fused_remove:
             with mark("gram"):
-                gram(self.x, None, self.G, ws=self.gws)
+                if self.gram_i8:
+                    gram_i8(self.x, self.colmax, self.G, ws=self.gws)
+                else:
+                    gram(self.x, None, self.G, ws=self.gws)
             pc = self._solve(trace, mark)
             with mark("mm2_project+pc_remove"):
                 mm2_project(self.s, self.x, self.aux_of(0), self.proj, out=self.mmb2, pc=pc,

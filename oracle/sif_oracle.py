@@ -159,6 +159,34 @@ def pc_from_gram(G, z0, npc=1, transposed=False, n_iter=7):
     return V * np.sign(V[np.arange(V.shape[0]), idx])[:, None]
 
 
+def sliced_gram(X, colmax=None):
+    """CPU restatement of the int8 Gram (csrc/pc_kernels.hip gram_i8_kernel):
+    each value a 30-bit fixed-point integer of its column's power-of-two bound
+    2^e (|x| <= colmax < 2^e), v = rint(x 2^(30-e)), cut into four balanced
+    base-256 digits (top in [-64, 64]); digit-pair products of level a + b <= 4
+    summed exactly, G = 2^(e_i + e_j - 60) sum over those pairs.  Test
+    infrastructure: the reference has no counterpart (its TruncatedSVD works
+    on X itself); this pins the device kernel's arithmetic."""
+    X = np.asarray(X, np.float32).astype(np.float64)
+    m = np.abs(X).max(0) if colmax is None else np.asarray(colmax, np.float64)
+    e = np.where(m > 0, np.frexp(m)[1], 0).astype(np.int64)
+    v = np.rint(np.ldexp(X, 30 - e[None, :])).astype(np.int64)
+    digs = []
+    for _ in range(4):
+        lo = ((v + 128) & 255) - 128
+        digs.append(lo)
+        v = (v - lo) >> 8
+    assert (v == 0).all()
+    digs = [d.astype(np.float64) for d in digs[::-1]]  # top digit first
+    assert np.abs(digs[0]).max(initial=0) <= 64
+    G = np.zeros((X.shape[1],) * 2)
+    for a in range(4):
+        for b in range(4):
+            if a + b <= 4:
+                G += (digs[a].T @ digs[b]) * 2.0 ** (8 * (6 - a - b) - 60)
+    return G * np.ldexp(1.0, e[:, None] + e[None, :])
+
+
 class CPUOps:
     """CPU doubles of the libmmb kernels that pipeline.global_pc composes
     (torch CPU tensors in/out) — lets the multi-rank orchestration run under

@@ -284,6 +284,30 @@ def test_projection_variants_bit_identical(gpu, N, variant, monkeypatch):
     assert torch.equal(s1, s3)
 
 
+@pytest.mark.parametrize("N,T", [(3000, 40), (129, 40), (40, 300)])
+def test_fused_step_int8_gram_vs_f64(gpu, N, T):
+    """The default step's Gram (mmb_gram_i8 on the column bounds the stream
+    kernel writes: wave kernel at T <= 64, workgroup kernel above) against the
+    exact-f64 step: column bounds equal max |x|, G within 2e-9 relative, PC
+    within 1e-9, MMB2 rows bit-identical, SIF rows to a few f32 ulps."""
+    inp = synth.device_workload(N, T, 20_000, A=300, Vd=300, seed=51, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    a = P.FusedStep(inp, gen.networks(), gram_kind="i8")
+    b = P.FusedStep(inp, gen.networks(), gram_kind="f64")
+    assert a.gram_i8 and not b.gram_i8
+    s1, m1 = [t.clone() for t in a.run()]
+    s2, m2 = b.run()
+    torch.cuda.synchronize()
+    cm = a.colmax.cpu().numpy().view(np.float32)
+    assert np.array_equal(cm, a.x.abs().amax(0).cpu().numpy())
+    G1, G2 = a.G.cpu().numpy(), b.G.cpu().numpy()
+    assert np.abs(G1 - G2).max() <= 2e-9 * np.abs(G2).max()
+    assert np.abs(a.pc.cpu().numpy() - b.pc.cpu().numpy()).max() < 1e-9
+    assert torch.equal(m1, m2)
+    assert M.row_rel_err(s1.cpu().numpy(), s2.cpu().numpy()) < 2e-7  # f32 output ulps
+
+
 def test_zero_weight_rows_sif_raises_mmb2_finite(gpu):
     """A row whose SIF weights are all zero: its a2 row is 0/0 = NaN (numpy,
     sif_functions.py:55) and the reference's TruncatedSVD rejects the split

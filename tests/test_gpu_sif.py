@@ -311,3 +311,39 @@ def test_fused_step_sharded_with_fake_allreduce(gpu, n_total, shards):
         mm2_parts.append(m.clone())
     assert torch.equal(torch.cat(mm2_parts), m_ref)
     assert M.row_rel_err(torch.cat(sif_parts).cpu().numpy(), s_ref.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("n,seed,scale", [(320, 0, 1.0), (5000, 1, 1.0), (70_000, 2, 1e-3),
+                                          (1000, 3, 1e4), (7, 4, 1.0)])
+def test_gram_i8_vs_sliced_oracle_and_f64(gpu, n, seed, scale):
+    """mmb_gram_i8 (int8 digits, exact integer level sums) against its CPU
+    restatement oracle.sif_oracle.sliced_gram (same digits; f64 summation
+    order only) and the exact f64 Gram (2e-9; heavy-tailed t(3) columns), rows
+    past 64-row chunks, tiny and huge magnitudes, a column of zeros."""
+    from oracle import sif_oracle as O
+
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_t(3, size=(n, 300)) * scale).astype(np.float32)
+    x[:, 17] = 0.0
+    xt = torch.tensor(x, device=gpu)
+    cm = P.colmax(xt)
+    assert np.array_equal(cm.cpu().numpy().view(np.float32), np.abs(x).max(0))
+    G = P.gram_i8(xt, cm).cpu().numpy()
+    ref = O.sliced_gram(x)
+    exact = x.astype(np.float64).T @ x.astype(np.float64)
+    assert np.abs(G - ref).max() <= 1e-13 * np.abs(ref).max()
+    assert np.abs(G - exact).max() <= 2e-9 * np.abs(exact).max()
+    assert np.array_equal(G, G.T)
+
+
+def test_gram_i8_pc_on_golden_splits(gpu, golden):
+    """The PC solved from the int8 Gram stays within 1e-9 of the reference's
+    TruncatedSVD component on the golden splits (gap-free g3 and npc = 2
+    included)."""
+    for case in ("g2_mosi", "g3_gap", "g3b_npc2"):
+        z = golden(case)
+        x = torch.tensor(z["emb"], device=gpu)
+        npc = z["pc"].shape[0]
+        G = P.gram_i8(x, P.colmax(x))
+        pc = P.pc_solve(G, P.omega(300, npc + 10, gpu), npc, False).cpu().numpy()
+        assert np.abs(pc - z["pc"]).max() < 1e-9, case

@@ -149,3 +149,19 @@ def test_metrics_match_reference(golden):
            "pom": MO.pom_loss(z["pred_pom"], z["y_pom"], verbose=False),
            "iemocap": MO.iemocap_loss(z["pred_iemocap"], z["y_iemocap"], verbose=False)}
     assert json.loads(json.dumps(got)) == ref
+
+
+def test_sliced_gram_restatement_meets_pc_bar(golden):
+    """The int8-digit Gram (oracle.sif_oracle.sliced_gram, the device
+    mmb_gram_i8's arithmetic): within 2e-10 of the exact Gram and its PC within
+    1e-9 of the reference TruncatedSVD component on every golden split."""
+    for case in ("g2_mosi", "g3_gap", "g3b_npc2"):
+        z = golden(case)
+        X = z["emb"].astype(np.float64)
+        G = X.T @ X
+        Gs = O.sliced_gram(z["emb"])
+        assert np.abs(Gs - G).max() <= 2e-10 * np.abs(G).max()
+        npc = z["pc"].shape[0]
+        z0 = np.random.RandomState(0).normal(size=(X.shape[1], npc + 10))
+        pc = O.pc_from_gram(Gs, z0, npc, False)
+        assert np.abs(pc - z["pc"]).max() < 1e-9, case

@@ -64,8 +64,23 @@ def main():
                                                    inp["visual"], ids32=inp["ids"],
                                                    table=inp["table"], wtab32=inp["wtab"],
                                                    out=(step.x, step.s, step.aux)), args.reps)
+    if "stream_cm" in which:  # with the column bounds for the int8 Gram
+        res["stream_cm"] = timed(lambda: P.mm2_stream(step.n, step.t, 300, 300, 300, inp["audio"],
+                                                      inp["visual"], ids32=inp["ids"],
+                                                      table=inp["table"], wtab32=inp["wtab"],
+                                                      out=(step.x, step.s, step.aux),
+                                                      colmax=step.colmax, colmax_ws=step.colmax_ws),
+                                 args.reps)
     if "gram" in which:
         res["gram"] = timed(lambda: P.gram(step.x, None, step.G, ws=step.gws), args.reps)
+    if "gram_i8" in which:  # int8-sliced Gram (+ the column bounds pass it needs)
+        cm = P.colmax(step.x)
+        Gi = torch.empty_like(step.G)
+        res["colmax"] = timed(lambda: P.colmax(step.x, out=cm), args.reps)
+        res["gram_i8"] = timed(lambda: P.gram_i8(step.x, cm, Gi, ws=step.gws), args.reps)
+        G64 = P.gram(step.x, None, ws=step.gws)
+        torch.cuda.synchronize()
+        print(f"gram_i8 vs f64 Gram: max rel {((Gi - G64).abs().max() / G64.abs().max()).item():.3e}")
     if "pcsolve" in which:
         res["pcsolve"] = timed(lambda: P.pc_solve(step.G, z0, 1, False), args.reps)
     if "remove" in which:
