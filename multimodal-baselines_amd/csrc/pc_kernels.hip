@@ -289,32 +289,39 @@ __device__ __forceinline__ int gi_exp(unsigned bits) {
   return e;
 }
 
-// the four digit bytes of v = rint(x 2^(30 - e)) (two's complement bytes of
-// the balanced digits, low digit first)
-__device__ __forceinline__ void gi_digits(float x, int e, int (&b)[kGiDig]) {
-  int v = static_cast<int>(rintf(ldexpf(x, 30 - e)));
-#pragma unroll
-  for (int a = 0; a < kGiDig - 1; ++a) {
-    const int d = __builtin_amdgcn_sbfe(v, 0, 8);  // sign-extended low byte
-    b[a] = v;                                        // its byte = d's byte
-    v = (v - d) >> 8;
-  }
-  b[kGiDig - 1] = v;
+// v' = rint(x 2^(30 - e)) + 0x808080: byte i < 3 of v' is d_i + 128 for the
+// balanced digit d_i in [-128, 127] (so XOR 0x80 gives d_i's two's-complement
+// byte), byte 3 is the top digit d_3 itself (|d_3| <= 64):
+//   v = sum_i d_i 256^i  =>  v + 128 (1 + 256 + 65536) = sum_i (d_i + 128) 256^i
+// for the low three, the top untouched.
+__device__ __forceinline__ unsigned gi_vbias(float x, int e) {
+  return static_cast<unsigned>(static_cast<int>(rintf(ldexpf(x, 30 - e)))) + 0x808080u;
 }
 
-// bytes 0 of a, b, c, d -> one dword (row order a, b, c, d)
-__device__ __forceinline__ unsigned gi_pack4(int a, int b, int c, int d) {
-  const unsigned ab = __builtin_amdgcn_perm(static_cast<unsigned>(b), static_cast<unsigned>(a), 0x0c0c0400u);
-  const unsigned cd = __builtin_amdgcn_perm(static_cast<unsigned>(d), static_cast<unsigned>(c), 0x0c0c0400u);
-  return __builtin_amdgcn_perm(cd, ab, 0x05040100u);
+// 4 values (rows r..r+3) -> the 4 digit-plane dwords, top digit first
+// (a 4 x 4 byte transpose in 8 v_perm_b32, then the bias flip)
+__device__ __forceinline__ void gi_planes(unsigned v0, unsigned v1, unsigned v2, unsigned v3,
+                                          unsigned (&w)[4]) {
+  const unsigned p0 = __builtin_amdgcn_perm(v1, v0, 0x05010400u);  // v0.b0 v1.b0 v0.b1 v1.b1
+  const unsigned p1 = __builtin_amdgcn_perm(v1, v0, 0x07030602u);  // v0.b2 v1.b2 v0.b3 v1.b3
+  const unsigned q0 = __builtin_amdgcn_perm(v3, v2, 0x05010400u);
+  const unsigned q1 = __builtin_amdgcn_perm(v3, v2, 0x07030602u);
+  w[0] = __builtin_amdgcn_perm(q1, p1, 0x07060302u);                // byte 3: top digit
+  w[1] = __builtin_amdgcn_perm(q1, p1, 0x05040100u) ^ 0x80808080u;  // byte 2
+  w[2] = __builtin_amdgcn_perm(q0, p0, 0x07060302u) ^ 0x80808080u;  // byte 1
+  w[3] = __builtin_amdgcn_perm(q0, p0, 0x05040100u) ^ 0x80808080u;  // byte 0
 }
 
+// DIAG (timing-only builds, wrong results; MMB_GRAM_DIAG): bit 0 no MFMAs
+// (operands kept live), bit 1 no f64 update, bit 2 no slicing, bit 3 no
+// x loads
+template <int DIAG = 0>
 __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict__ x,
                                                        const unsigned* __restrict__ colmax,
                                                        int64_t N, int D, int nt, int R,
                                                        int64_t chunk, int xcd_map,
                                                        double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_dig[];  // [4][kGiF][64]
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dig[];  // [2][4][kGiF][64]
   const int T = nt * (nt + 1) / 2;
   int half, range;
   if (xcd_map) {
@@ -377,6 +384,13 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
   }
   float xv[kIt][16];
   auto load = [&](int c) {
+    if constexpr ((DIAG & 8) != 0) {
+#pragma unroll
+      for (int u = 0; u < kIt; ++u)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(xv[u][j]));
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
@@ -385,54 +399,63 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
         xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
     }
   };
-  auto slice = [&]() {
+  // item u of the x values in registers -> digit bytes in LDS buffer `buf`
+  auto slice_item = [&](int u, unsigned char* buf) {
+    if constexpr ((DIAG & 4) != 0) return;
+    const int it = tid + kGiNT * u;
+    if (it < nitems) {
+      unsigned w[4][kGiDig];  // [row group g][plane]
 #pragma unroll
-    for (int u = 0; u < kIt; ++u) {
-      const int it = tid + kGiNT * u;
-      if (it < nitems) {
-        unsigned w[kGiDig][4];
+      for (int g = 0; g < 4; ++g)
+        gi_planes(gi_vbias(xv[u][4 * g + 0], it_e[u]), gi_vbias(xv[u][4 * g + 1], it_e[u]),
+                  gi_vbias(xv[u][4 * g + 2], it_e[u]), gi_vbias(xv[u][4 * g + 3], it_e[u]), w[g]);
+      const int f = it_f[u], slot = it_kq[u] ^ gi_swz(f);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          int b0[kGiDig], b1[kGiDig], b2[kGiDig], b3[kGiDig];
-          gi_digits(xv[u][4 * g + 0], it_e[u], b0);
-          gi_digits(xv[u][4 * g + 1], it_e[u], b1);
-          gi_digits(xv[u][4 * g + 2], it_e[u], b2);
-          gi_digits(xv[u][4 * g + 3], it_e[u], b3);
-          // plane a holds digit a from the top (b[kGiDig - 1 - a])
-#pragma unroll
-          for (int a = 0; a < kGiDig; ++a)
-            w[a][g] = gi_pack4(b0[kGiDig - 1 - a], b1[kGiDig - 1 - a], b2[kGiDig - 1 - a],
-                               b3[kGiDig - 1 - a]);
-        }
-        const int f = it_f[u], slot = it_kq[u] ^ gi_swz(f);
-#pragma unroll
-        for (int a = 0; a < kGiDig; ++a)
-          *reinterpret_cast<uint4*>(s_dig + ((a * kGiF + f) * 4 + slot) * 16) =
-              make_uint4(w[a][0], w[a][1], w[a][2], w[a][3]);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one item's digits live at a time
+      for (int a = 0; a < kGiDig; ++a)
+        *reinterpret_cast<uint4*>(buf + ((a * kGiF + f) * 4 + slot) * 16) =
+            make_uint4(w[0][a], w[1][a], w[2][a], w[3][a]);
     }
   };
+  constexpr int kBuf = kGiDig * kGiF * kGiRows;  // bytes of one chunk's digits
 
-  if (nchunks > 0) load(0);
+  // Double-buffered digits (2 x 80 KB): chunk c's MFMAs read buffer c & 1
+  // while this wave slices chunk c + 1 (x already in registers) into the
+  // other buffer, and the loads of chunk c + 2 are in flight.  One barrier per
+  // chunk: it publishes chunk c + 1's digits and retires every read of the
+  // buffer the next iteration overwrites.
+  if (nchunks > 0) {
+    load(0);
+#pragma unroll
+    for (int u = 0; u < kIt; ++u) slice_item(u, s_dig);
+    if (nchunks > 1) load(1);
+  }
+  __syncthreads();
+  const int lf = lane & 15, lsl = lane >> 4;
   for (int c = 0; c < nchunks; ++c) {
-    __syncthreads();  // every wave done reading the previous chunk's digits
-    slice();
-    if (c + 1 < nchunks) load(c + 1);
-    __syncthreads();
+    const unsigned char* cur = s_dig + (c & 1) * kBuf;
+    unsigned char* nxt = s_dig + ((c + 1) & 1) * kBuf;
+    const bool more = c + 1 < nchunks;
     // lane l: feature (l & 15) of the tile's block, 16 rows of slot (l >> 4)
-    const int lf = lane & 15, lsl = lane >> 4;
+    i32x4 A[kGiDig];
 #pragma unroll
     for (int q = 0; q < kGiMaxTiles; ++q) {
       if (q < ntl) {
-        const int fa = ti[q] * 16 + lf, fb = tj[q] * 16 + lf;
-        i32x4 A[kGiDig], B[kGiDig];
+        if (q == 0 || ti[q] != ti[q - 1]) {  // the row block changes (wave-uniform)
+          const int fa = ti[q] * 16 + lf;
 #pragma unroll
-        for (int a = 0; a < kGiDig; ++a) {
-          A[a] = *reinterpret_cast<const i32x4*>(s_dig + ((a * kGiF + fa) * 4 + (lsl ^ gi_swz(fa))) * 16);
-          B[a] = *reinterpret_cast<const i32x4*>(s_dig + ((a * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
+          for (int a = 0; a < kGiDig; ++a)
+            A[a] = *reinterpret_cast<const i32x4*>(cur + ((a * kGiF + fa) * 4 + (lsl ^ gi_swz(fa))) * 16);
         }
+        const int fb = tj[q] * 16 + lf;
+        i32x4 B[kGiDig];
+#pragma unroll
+        for (int a = 0; a < kGiDig; ++a)
+          B[a] = *reinterpret_cast<const i32x4*>(cur + ((a * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
         const i32x4 z = {0, 0, 0, 0};
+        if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+          for (int a = 0; a < kGiDig; ++a) asm volatile("" ::"v"(A[a]), "v"(B[a]));
+        } else {
         i32x4 H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[0], z, 0, 0, 0);
         H <<= 8;
         H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[1], H, 0, 0, 0);
@@ -448,17 +471,25 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
         i32x4 Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[3], z, 0, 0, 0);
         Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[2], Lo, 0, 0, 0);
         Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3], B[1], Lo, 0, 0, 0);
+        if constexpr ((DIAG & 2) != 0) {
+          asm volatile("" ::"v"(H), "v"(M), "v"(Lo));
+        } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           acc[q][e] = fma(static_cast<double>(H[e]), 0x1p-20, acc[q][e]);
           acc[q][e] = fma(static_cast<double>(M[e]), 0x1p-36, acc[q][e]);
           acc[q][e] = fma(static_cast<double>(Lo[e]), 0x1p-44, acc[q][e]);
         }
+        }
+        }
       }
-      // one tile's operands live at a time (12 tiles' f64 sums + the next
-      // chunk's x values already hold 144 registers)
+      // slicing of the next chunk spread between the tiles (item u after
+      // tile 4u + 3): VALU work beside the MFMAs in flight
+      if (more && (q & 3) == 3 && (q >> 2) < kIt) slice_item(q >> 2, nxt);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if (c + 2 < nchunks) load(c + 2);
+    __syncthreads();
   }
   // partials in gram_tri_kernel's layout, scaled by 2^(e_i + e_j) (exact):
   // C/D map of the 16x16 integer MFMA: row 4 (lane >> 4) + e, column lane & 15
@@ -1509,15 +1540,28 @@ static bool gram2_ok(const float* num, int d) {
 }
 
 
+template <int DIAG>
 static size_t gram_i8_lds() {
-  const size_t lds = kGiDig * kGiF * kGiRows;
+  const size_t lds = 2 * kGiDig * kGiF * kGiRows;  // 160 KB: double-buffered digits
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8_kernel<DIAG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
   return lds;
+}
+
+template <int DIAG>
+static void launch_gram_i8(const float* x, const uint32_t* colmax, int64_t n, int d,
+                           const Gram2Plan& q, double* part, hipStream_t stream) {
+  gram_i8_kernel<DIAG><<<2 * q.R, kGiNT, gram_i8_lds<DIAG>(), stream>>>(x, colmax, n, d, q.nt, q.R,
+                                                                        q.chunk, q.xcd, part);
+}
+
+static int gram_i8_diag() {  // timing-only ablations (MMB_GRAM_DIAG), re-read per launch
+  const char* e = getenv("MMB_GRAM_DIAG");
+  return e ? atoi(e) : 0;
 }
 }  // namespace mmb
 
@@ -1578,8 +1622,16 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
   MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
   // int32 level sums are per 64-row k-step, so any range length is safe
   double* part = static_cast<double*>(ws);
-  gram_i8_kernel<<<2 * q.R, kGiNT, gram_i8_lds(), stream>>>(x, colmax, n, d, q.nt, q.R, q.chunk,
-                                                             q.xcd, part);
+  switch (gram_i8_diag()) {
+    case 1: launch_gram_i8<1>(x, colmax, n, d, q, part, stream); break;
+    case 2: launch_gram_i8<2>(x, colmax, n, d, q, part, stream); break;
+    case 3: launch_gram_i8<3>(x, colmax, n, d, q, part, stream); break;
+    case 4: launch_gram_i8<4>(x, colmax, n, d, q, part, stream); break;
+    case 12: launch_gram_i8<12>(x, colmax, n, d, q, part, stream); break;
+    case 15: launch_gram_i8<15>(x, colmax, n, d, q, part, stream); break;
+    case 7: launch_gram_i8<7>(x, colmax, n, d, q, part, stream); break;
+    default: launch_gram_i8<0>(x, colmax, n, d, q, part, stream); break;
+  }
   MMB_LAUNCH_CHECK();
   const int64_t total = static_cast<int64_t>(d) * d;
   gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, q.nt, q.R,

@@ -81,6 +81,11 @@ def main():
         G64 = P.gram(step.x, None, ws=step.gws)
         torch.cuda.synchronize()
         print(f"gram_i8 vs f64 Gram: max rel {((Gi - G64).abs().max() / G64.abs().max()).item():.3e}")
+        for dg in os.environ.get("GRAM_DIAGS", "").split(","):  # timing-only ablations
+            if dg:
+                os.environ["MMB_GRAM_DIAG"] = dg
+                res[f"gram_i8 diag {dg}"] = timed(lambda: P.gram_i8(step.x, cm, Gi, ws=step.gws), args.reps)
+        os.environ.pop("MMB_GRAM_DIAG", None)
     if "pcsolve" in which:
         res["pcsolve"] = timed(lambda: P.pc_solve(step.G, z0, 1, False), args.reps)
     if "remove" in which:
