@@ -43,9 +43,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table
 F16_MFMA_PEAK_TFS = 2500.0  # dense f16 MFMA (no sparsity)
 F32_MFMA_PEAK_TFS = 157.3  # f32-input MFMA (= the f32 vector rate on gfx950)
 F64_MFMA_PEAK_TFS = 78.6  # fp64 MFMA
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x f16, no sparsity)
 METRIC = "utterance-embeds/sec (MMB2, 3 modalities, 300d) at 1/2/4/8 MI355X"
 DTYPE = ("f32 (MMB2 projection: fp16 hi/lo x3 split on the f16 MFMA pipe, fp32 accumulate; "
-         "Gram / PC solve / removal fp64)")
+         "Gram: int8 digits of 30-bit fixed point, exact int32 level sums + f64; "
+         "PC solve / removal fp64)")
 
 
 def log(*a):
@@ -219,7 +221,19 @@ def mfma_rooflines(step, phase_ms, U, D):
                                   "frac": round(tf / F16_MFMA_PEAK_TFS, 4), "flop_per_utt": flop,
                                   "padded_flop_per_utt": 3 * 2 * step.proj.kp * step.proj.ldw,
                                   "ms": round(proj_ms, 4), "includes": "fused PC-removal tail"}
-    if "gram" in phase_ms:
+    if "gram" in phase_ms and getattr(step, "gram_i8", False):
+        # 13 int8 digit-pair products of the upper triangle per row (the
+        # algorithmic work of the sliced Gram, gram_i8_kernel)
+        ops = 13 * D * (D + 1)
+        t = ops * U / (phase_ms["gram"] / 1e3) / 1e12
+        out["gram_i8 (int8 digits)"] = {"bound": "mfma", "achieved": round(t, 1),
+                                        "peak": I8_MFMA_PEAK_TOPS, "unit": "TOP/s",
+                                        "frac": round(t / I8_MFMA_PEAK_TOPS, 4), "op_per_utt": ops,
+                                        "ms": round(phase_ms["gram"], 4),
+                                        "note": "incl. the partial reduction; f64-equivalent "
+                                                f"{D * (D + 1) * U / (phase_ms['gram'] / 1e3) / 1e12:.1f} "
+                                                "TFLOP/s of G"}
+    elif "gram" in phase_ms:
         flop = D * (D + 1)  # 2 * D(D+1)/2 per row
         tf = flop * U / (phase_ms["gram"] / 1e3) / 1e12
         out["gram_tri (fp64)"] = {"bound": "mfma", "achieved": round(tf, 2),
