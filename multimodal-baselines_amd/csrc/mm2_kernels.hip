@@ -1376,6 +1376,147 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3d_kernel(
                                     lane, n0, N, D, num, aux, col_inv, c0, pc, out, sif);
 }
 
+
+// Variant 6 (r02): B fragments straight from L2 into registers, one chunk
+// ahead; the LDS holds only A, eight chunks deep.  The K-loop ablation
+// (r02d) put the default kernel's time in its staging: 144 KB of rings keep
+// B one chunk and A (from HBM) two chunks ahead, too little in flight.  The
+// weight image is L2-resident and shared by every workgroup, so each wave
+// loads its own B fragments (80 columns x hi/lo: 10 x 16 bytes per lane per
+// chunk, one coalesced KB per instruction; the two row waves of a column
+// block both load them, 2x L2 traffic) into three rotating register sets,
+// and the 128 KB A ring runs six chunks ahead.  Waves and MFMA order as
+// variant 2 (2 x 4 waves of 64 rows x 80 columns, hh + hl + lh per tile), so
+// the rows are bit-identical.  The B loads are inline asm (saddr form: the
+// chunk's image base in SGPRs, a per-lane 32-bit offset) so hipcc's vmcnt
+// bookkeeping never drains the A LDS-DMA stream; one counted wait per chunk.
+//   issue order per chunk c: B(c+1) (10 loads), A(c+6) (2 copies per thread)
+constexpr int kX3eAslots = 8;
+template <int CT>
+constexpr size_t x3e_lds_bytes() {
+  return kX3eAslots * kXAbufHalves * sizeof(_Float16) + kXM * sizeof(float);
+}
+
+__device__ __forceinline__ void gload16_saddr(half8& v, const void* sbase, int voff) {
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
+}
+
+template <int DIAG = 0>
+__global__ __launch_bounds__(kXT) void mm2_project_x3e_kernel(
+    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
+    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
+    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
+    const double* __restrict__ pc, float* __restrict__ sif) {
+  constexpr int CT = 5, LDW = 64 * CT;
+  constexpr int BBUF = x3_bbuf_halves<CT>();       // halves per B chunk image
+  constexpr int AQ = kXAbufHalves * 2 / 16 / kXT;  // 2 copies per thread per A chunk
+  static_assert(AQ == 2, "staging split");
+  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
+  _Float16* aring = lds;
+  float* s_rs = reinterpret_cast<float*>(aring + kX3eAslots * kXAbufHalves);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int lq = lane >> 4, lc = lane & 15;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
+  const int nch = Kp / kXK;
+
+  const _Float16* asrc[AQ];
+#pragma unroll
+  for (int q = 0; q < AQ; ++q) {
+    const int g = q * kXT + tid;
+    const int plane = g >> 9, row = (g >> 2) & (kXM - 1);
+    const int64_t r = min(n0 + row, N - 1);
+    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
+  }
+  auto stage_a = [&](int c) {
+    const int cc = min(c, nch - 1);
+    _Float16* dst = aring + (c & (kX3eAslots - 1)) * kXAbufHalves;
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) glds16(asrc[q] + cc * kXK, dst + (q * kXT + wave * 64) * 8);
+  };
+  // lane's B fragment of column tile t, plane p of a chunk image: column
+  // wc*80 + 16 t + lc, k slot lq at position lq ^ swz(col) (swz depends on
+  // lc only: 16 t and wc*80 are multiples of 16)
+  const int boff = ((wc * CT * 16 + lc) * kXK + ((lq ^ x3_swz(lc)) * 8)) * 2;  // bytes
+  using B10 = half8[2 * CT];
+  auto load_b = [&](int c, B10& b) {
+    const int cc = min(c, nch - 1);
+    const void* base = img + static_cast<int64_t>(cc) * BBUF;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      gload16_saddr(b[2 * t], base, boff + t * 16 * kXK * 2);
+      gload16_saddr(b[2 * t + 1], base, boff + (LDW * kXK + t * 16 * kXK) * 2);
+    }
+  };
+
+  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
+
+  f32x4 acc[4][CT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < CT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  B10 b0, b1;
+#pragma unroll
+  for (int c = 0; c < kX3eAslots - 2; ++c) stage_a(c);
+  load_b(0, b0);
+
+  // chunk c: A(c) in ring slot c & 7, B(c) in (b); loads B(c+1) into (nb),
+  // then A(c+6).  Loads return in issue order, so the short-lead B loads go
+  // first: waiting for B(c) (chunk c-1's first ops) leaves A(c+5) in flight
+  // prologue: A(0..5), then B(0) -- all of it landed before chunk 0
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(b0[0]), "+v"(b0[1]), "+v"(b0[2]), "+v"(b0[3]), "+v"(b0[4]),
+               "+v"(b0[5]), "+v"(b0[6]), "+v"(b0[7]), "+v"(b0[8]), "+v"(b0[9])::"memory");
+  auto chunk = [&](int c, B10& b, B10& nb) {
+    asm volatile("s_waitcnt vmcnt(2)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]),
+                 "+v"(b[5]), "+v"(b[6]), "+v"(b[7]), "+v"(b[8]), "+v"(b[9])::"memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    load_b(c + 1, nb);
+    stage_a(c + kX3eAslots - 2);
+    const _Float16* a = aring + (c & (kX3eAslots - 1)) * kXAbufHalves;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + i * 16 + lc;
+      const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
+      const half8 ah = *reinterpret_cast<const half8*>(a + ao);
+      const half8 al = *reinterpret_cast<const half8*>(a + kXM * kXK + ao);
+      if constexpr ((DIAG & 8) != 0) {
+        asm volatile("" ::"v"(ah), "v"(al));
+      } else {
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b[2 * t], acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b[2 * t + 1], acc[i][t], 0, 0, 0);
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, b[2 * t], acc[i][t], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr ((DIAG & 8) != 0) {
+#pragma unroll
+      for (int t = 0; t < 2 * CT; ++t) asm volatile("" ::"v"(b[t]));
+    }
+  };
+#pragma unroll 1
+  for (int c = 0; c < nch; c += 2) {
+    chunk(c, b0, b1);
+    if (c + 1 < nch) chunk(c + 1, b1, b0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < CT; ++t) asm volatile("" ::"v"(acc[i][t]));
+    return;
+  }
+  x3_row_epilogue<CT, 4>(acc, reinterpret_cast<float*>(lds), s_rs, kXM, wr, wc, lq, lc, wave, lane,
+                         n0, N, D, num, aux, col_inv, c0, pc, out, sif);
+}
+
 template <int CT>
 constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(float); }
 
@@ -1471,6 +1612,29 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
                         (sif == nullptr || a16(sif)) && proj_row_epilogue();
     const bool pipe = proj_variant() == 2;
     if constexpr (CT == 5) {
+      if (rowepi && proj_variant() == 6) {
+        constexpr size_t ldse = x3e_lds_bytes<CT>();
+        static_assert(ldse <= 160 * 1024, "x3e ring exceeds LDS");
+        static_assert(64 * 324 * sizeof(float) <= kX3eAslots * kXAbufHalves * sizeof(_Float16),
+                      "row epilogue scratch exceeds the A ring");
+        static bool attr_e = false;
+        if (!attr_e) {
+          for (const void* f : {reinterpret_cast<const void*>(&mm2_project_x3e_kernel<0>),
+                                reinterpret_cast<const void*>(&mm2_project_x3e_kernel<1>),
+                                reinterpret_cast<const void*>(&mm2_project_x3e_kernel<9>)})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldse));
+          attr_e = true;
+        }
+        const int dg = proj_diag();
+        if (dg == 1)
+          mm2_project_x3e_kernel<1><<<grid, kXT, ldse, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        else if (dg == 9)
+          mm2_project_x3e_kernel<9><<<grid, kXT, ldse, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        else
+          mm2_project_x3e_kernel<0><<<grid, kXT, ldse, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
+        MMB_LAUNCH_CHECK();
+        return MMB_OK;
+      }
       if (rowepi && proj_variant() == 4) {
         constexpr size_t ldsd = x3d_lds_bytes<CT>();
         static_assert(ldsd <= 160 * 1024, "x3d rings exceed LDS");

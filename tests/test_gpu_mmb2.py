@@ -262,7 +262,7 @@ def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
     assert M.row_rel_err(s4.cpu().numpy(), s1.cpu().numpy()) < 1e-6
 
 
-@pytest.mark.parametrize("variant", ["3", "4"])
+@pytest.mark.parametrize("variant", ["3", "4", "6"])
 @pytest.mark.parametrize("N", [700, 128, 129, 1000])
 def test_projection_variants_bit_identical(gpu, N, variant, monkeypatch):
     """Variant 3 (A fragments straight from HBM into registers, B through a
