@@ -61,9 +61,10 @@ __device__ __forceinline__ void store_frag(float* p, const f32x16& v) {
 }
 
 __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
-  extern __shared__ float smem[];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int DP = a.DP, HP = a.HP, O = a.O;
-  float* sx = smem;                                   // [32][DP+1]
+  int64_t* s_perm = reinterpret_cast<int64_t*>(smem);  // [2][32] row indices (prefetch)
+  float* sx = smem + 4 * kBatchMax;                   // [32][DP+1]
   float* spart = sx + kBatchMax * (DP + 1);           // [G][32][HP]  (aliased by sdh)
   float* shid = spart + a.G * kBatchMax * HP;         // [32][HP]
   float* sW2 = shid + kBatchMax * HP;                 // [O][HP]
@@ -103,21 +104,54 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
 
   const int64_t spe = (a.n_per_epoch + a.B - 1) / a.B;
   const int64_t nsteps = spe * a.n_epochs;
+  auto batch_of = [&](int64_t st, int64_t& base, int& bc) {
+    const int64_t ep = st / spe, bi = st % spe;
+    base = ep * a.n_per_epoch + bi * a.B;
+    bc = static_cast<int>(min<int64_t>(a.B, a.n_per_epoch - bi * a.B));
+  };
+  // The batch gather was two dependent round trips (permutation index, then
+  // the row) per step.  Now wave 0 reads step s+1's indices into LDS during
+  // step s, so a step issues its row loads at once (16-byte loads when
+  // D % 4 == 0).
+  auto fetch_perm = [&](int64_t st) {
+    if (wave == 0 && lane < kBatchMax && st < nsteps) {
+      int64_t base;
+      int bc;
+      batch_of(st, base, bc);
+      s_perm[(st & 1) * kBatchMax + lane] = lane < bc ? a.perm[base + lane] : 0;
+    }
+  };
+  const bool v4 = (a.D & 3) == 0 && (reinterpret_cast<uintptr_t>(a.lat) & 15) == 0;
+  fetch_perm(0);
+  __syncthreads();
   for (int64_t step = 0; step < nsteps; ++step) {
-    const int64_t ep = step / spe, bi = step % spe;
-    const int64_t base = ep * a.n_per_epoch + bi * a.B;
-    const int Bc = static_cast<int>(min<int64_t>(a.B, a.n_per_epoch - bi * a.B));
+    int64_t base;
+    int Bc;
+    batch_of(step, base, Bc);
+    const int64_t* pp = s_perm + (step & 1) * kBatchMax;
     // 1. gather the batch rows (DataLoader order) into LDS
-    for (int e = tid; e < kBatchMax * DP; e += kMlpNT) {
-      const int b = e / DP, d = e % DP;
-      float v = 0.f;
-      if (b < Bc && d < a.D) v = a.lat[a.perm[base + b] * a.D + d];
-      sx[b * SX + d] = v;
+    if (v4) {
+      const int U = DP >> 2;  // float4 units of a padded row
+      for (int e = tid; e < kBatchMax * U; e += kMlpNT) {
+        const int b = e / U, u = e - b * U;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (b < Bc && 4 * u < a.D) v = *reinterpret_cast<const float4*>(a.lat + pp[b] * a.D + 4 * u);
+        float* dst = sx + b * SX + 4 * u;
+        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+      }
+    } else {
+      for (int e = tid; e < kBatchMax * DP; e += kMlpNT) {
+        const int b = e / DP, d = e % DP;
+        float v = 0.f;
+        if (b < Bc && d < a.D) v = a.lat[pp[b] * a.D + d];
+        sx[b * SX + d] = v;
+      }
     }
     for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
       const int b = e / O, o = e % O;
-      sy[e] = (b < Bc) ? a.lab[a.perm[base + b] * O + o] : 0.f;
+      sy[e] = (b < Bc) ? a.lab[pp[b] * O + o] : 0.f;
     }
+    fetch_perm(step + 1);  // lands during this step
     __syncthreads();
     // 2. forward partials: pre[b][h] over this wave's feature tiles (MFMA)
     if (mw) {
@@ -146,16 +180,33 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
       shid[e] = (h < a.H && p > 0.f) ? p : 0.f;
     }
     __syncthreads();
-    // 4. output layer, L1 loss and its gradient (mean over Bc*O elements)
+    // 4. output layer, L1 loss and its gradient (mean over Bc*O elements);
+    //    O = 1: a half-wave per batch row (16 waves x 2 = 32 rows), lane
+    //    h-stride partial dots and a 32-lane shuffle sum, instead of a
+    //    100-long serial chain per row
     float lsum = 0.f;
-    for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
-      const int b = e / O, o = e % O;
-      float out = sb2[o];
-      for (int h = 0; h < a.H; ++h) out = fmaf(sW2[o * HP + h], shid[b * HP + h], out);
-      const float diff = out - sy[e];
+    if (O == 1) {
+      const int b = 2 * wave + (lane >> 5), l32 = lane & 31;
+      float part = 0.f;
+      for (int h = l32; h < a.H; h += 32) part = fmaf(sW2[h], shid[b * HP + h], part);
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
+      const float diff = (sb2[0] + part) - sy[b];
       const bool valid = b < Bc;
-      sg[e] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc * O) : 0.f;
-      if (valid) lsum += fabsf(diff);
+      if (l32 == 0) {
+        sg[b] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc) : 0.f;
+        if (valid) lsum = fabsf(diff);
+      }
+    } else {
+      for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
+        const int b = e / O, o = e % O;
+        float out = sb2[o];
+        for (int h = 0; h < a.H; ++h) out = fmaf(sW2[o * HP + h], shid[b * HP + h], out);
+        const float diff = out - sy[e];
+        const bool valid = b < Bc;
+        sg[e] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc * O) : 0.f;
+        if (valid) lsum += fabsf(diff);
+      }
     }
     lsum = wave_sum(lsum);
     if (lane == 0) s_red[wave] = lsum;
@@ -474,7 +525,7 @@ extern "C" int mmb_mlp_train(const float* latents, const float* labels, const in
   if (a.G > a.nTd) a.G = a.nTd;
   a.DP = a.nTd * 32;
   a.HP = a.nTh * 32;
-  const size_t lds = sizeof(float) * (static_cast<size_t>(kBatchMax) * (a.DP + 1) +
+  const size_t lds = sizeof(float) * (4 * kBatchMax + static_cast<size_t>(kBatchMax) * (a.DP + 1) +
                                       static_cast<size_t>(a.G) * kBatchMax * a.HP +
                                       static_cast<size_t>(kBatchMax) * a.HP + o * a.HP + a.HP +
                                       o + 2 * kBatchMax * o + kMaxWaves);

@@ -662,8 +662,18 @@ __global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __rest
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int f = blockIdx.x * 64 + c;
   float m = 0.f;
-  if (f < D)
-    for (int r = g; r < P; r += 16) m = fmaxf(m, part[static_cast<int64_t>(r) * D + f]);
+  if (f < D) {
+    // 8 independent loads in flight per thread (a single chain is latency-bound)
+    float mm[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int r = g;
+    for (; r + 7 * 16 < P; r += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) mm[u] = fmaxf(mm[u], part[static_cast<int64_t>(r + 16 * u) * D + f]);
+    }
+    for (; r < P; r += 16) mm[0] = fmaxf(mm[0], part[static_cast<int64_t>(r) * D + f]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m = fmaxf(m, mm[u]);
+  }
   s_m[g][c] = m;
   __syncthreads();
   if (g == 0 && f < D) {
