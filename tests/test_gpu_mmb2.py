@@ -495,3 +495,50 @@ def test_gpu2_rejects_combinations_that_are_not_concatenations(gpu, golden):
     with torch.no_grad():
         ok = sif2.estimate_embedding_overall_gpu2(base, masks, nets, sw, text)
     assert M.row_rel_err(ok.cpu().numpy(), z["cs_f64"]) < TOL
+
+
+def test_full_size_step_sampled_rows_vs_oracle(gpu):
+    """BASELINE configs[3] at full size (1M utterances x 40 x 3 x 300-d, V =
+    400k, Zipf ids): the bench step itself, checked against the oracle where
+    the check is size-independent.  MMB2 rows are per-utterance: 512 sampled
+    rows against the oracle's sif2.estimate_embedding_overall_gpu2 on those
+    rows (1e-5).  The SIF a2 rows of the sample against the oracle's
+    get_weighted_average (2e-6), the step's PC (int8 Gram + device solve)
+    against the oracle's randomized-SVD-from-Gram on the exact f64 Gram of
+    all 1M a2 rows (1e-9), and the sample's PC-removed rows against the
+    oracle's removal with that PC (1e-5)."""
+    from oracle import sif_oracle as O
+
+    N, T, V = 1_000_000, 40, 400_000
+    inp = synth.device_workload(N, T, V, seed=1, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks())
+    assert step.gram_i8
+    sif_out, mm2_out = step.run()
+    step.check()
+    torch.cuda.synchronize()
+    rows = np.sort(np.random.default_rng(5).choice(N, 512, replace=False))
+    ridx = torch.as_tensor(rows, device=gpu)
+    E = inp["table"].cpu().numpy()
+    wt = inp["wtab"].cpu().numpy()
+    ids = inp["ids"][ridx].cpu().numpy().astype(np.int64)
+    audio = inp["audio"][ridx].cpu().numpy()
+    visual = inp["visual"][ridx].cpu().numpy()
+    sw = wt[ids].astype(np.float32)
+    text = E[ids]
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                            M.params_from_module(gen.cpu()), sw, text)
+    assert M.row_rel_err(mm2_out[ridx].cpu().numpy(), ref) < TOL
+    # a2 rows of the sample, then the PC over all rows from the exact Gram
+    x_ref = O.get_weighted_average(E, ids, wt[ids].astype(np.float64))
+    x = step.x.cpu().numpy()
+    assert M.row_rel_err(x[rows], x_ref) < 2e-6
+    X = x.astype(np.float64)
+    G = X.T @ X
+    del X
+    z0 = np.random.RandomState(0).normal(size=(300, 11))
+    pc = O.pc_from_gram(G, z0, 1, False)
+    assert np.abs(step.pc.cpu().numpy() - pc).max() < 1e-9
+    sif_ref = x_ref - (x_ref @ pc.T) @ pc
+    assert M.row_rel_err(sif_out[ridx].cpu().numpy(), sif_ref) < TOL
