@@ -536,8 +536,16 @@ __global__ void gram_tri_reduce_kernel(const double* __restrict__ part, int D, i
     const int bi = p / 16, bj = q / 16;
     const int tau = bi * nt - bi * (bi - 1) / 2 + (bj - bi);
     const int64_t off = static_cast<int64_t>(tau) * 256 + (p % 16) * 16 + (q % 16);
-    double sum = 0.0;
-    for (int r = 0; r < R; ++r) sum += part[static_cast<int64_t>(r) * T * 256 + off];
+    // eight independent partial sums (eight loads in flight; a single chain
+    // waited on every load), combined in a fixed order: deterministic
+    double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int r = 0;
+    for (; r + 8 <= R; r += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s8[u] += part[static_cast<int64_t>(r + u) * T * 256 + off];
+    }
+    for (; r < R; ++r) s8[0] += part[static_cast<int64_t>(r) * T * 256 + off];
+    const double sum = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     g[e] = accumulate ? g[e] + sum : sum;
   }
 }

@@ -320,10 +320,24 @@ class MMB2Projection:
                                      for p in (mu.weight, mu.bias, ls.weight, ls.bias)))
         self.refresh()
 
+    def _versions(self):
+        return tuple(t._version for ps in self.params for t in ps)
+
     def refresh(self):
         arr = lambda i: (ctypes_ptr_array([p[i].data_ptr() for p in self.params]))
         L.call("mmb_mm2_prepare", arr(0), arr(1), arr(2), arr(3), self.d, self.a, self.vd, self.t,
                L.ptr(self.wm), self.ldw, L.ptr(self.c0), L.ptr(self.wsplit), L.stream_ptr())
+        self._seen = self._versions()
+
+    def refresh_if_changed(self) -> bool:
+        """Re-merge only when a generator parameter changed in place since the
+        last merge (torch's version counters: an optimiser step bumps them), so
+        a step over a new batch with the same weights skips the five prepare
+        launches.  Returns whether it re-merged."""
+        if getattr(self, "_seen", None) == self._versions():
+            return False
+        self.refresh()
+        return True
 
 
 def ctypes_ptr_array(ptrs):
@@ -623,7 +637,7 @@ class FusedStep:
         d, k = self.d, self.npc + N_OVERSAMPLES
         nb = len(self.bounds)
         with mark("mm2_prepare"):
-            self.proj.refresh()
+            self.proj.refresh_if_changed()
         with mark("mm2_stream"):
             self._stream_chunk(0)  # every CU
         if self.fused_remove:

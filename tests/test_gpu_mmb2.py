@@ -542,3 +542,26 @@ def test_full_size_step_sampled_rows_vs_oracle(gpu):
     assert np.abs(step.pc.cpu().numpy() - pc).max() < 1e-9
     sif_ref = x_ref - (x_ref @ pc.T) @ pc
     assert M.row_rel_err(sif_out[ridx].cpu().numpy(), sif_ref) < TOL
+
+
+def test_step_remerges_weights_only_after_an_update(gpu):
+    """FusedStep re-merges the generator weights (mmb_mm2_prepare) only when a
+    parameter changed in place since the last merge: a second step with the
+    same weights skips it, an in-place update (what an optimiser step does)
+    triggers it, and the rows then equal a fresh step's."""
+    inp = synth.device_workload(700, 40, 5000, A=300, Vd=300, seed=61, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks())
+    _, m1 = [t.clone() for t in step.run()]
+    assert not step.proj.refresh_if_changed()
+    with torch.no_grad():
+        gen.embed2out["audio"]["mu"].weight.add_(0.05)
+    assert step.proj.refresh_if_changed()
+    with torch.no_grad():
+        gen.embed2out["textvisual"]["log_sigma"].bias.mul_(0.9)
+    _, m2 = [t.clone() for t in step.run()]
+    _, m3 = P.FusedStep(inp, gen.networks()).run()
+    torch.cuda.synchronize()
+    assert not torch.equal(m1, m2)
+    assert torch.equal(m2, m3)
