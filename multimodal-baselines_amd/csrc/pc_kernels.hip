@@ -1531,6 +1531,20 @@ static Gram2Plan gram2_plan(int64_t n, int d) {
   return p;
 }
 
+// int8 Gram: ranges of >= 64 rows (one k-step) instead of gram2_plan's
+// >= 512, so a 10k-row split (POM) fills every CU instead of 32 of them
+static Gram2Plan gram_i8_plan(int64_t n, int d) {
+  Gram2Plan q = gram2_plan(n, d);
+  int64_t R = n / kGiRows;
+  if (R < 1) R = 1;
+  if (R > kG2MaxR) R = kG2MaxR;
+  if (R >= 8) R = R / 8 * 8;
+  q.R = static_cast<int>(R);
+  q.xcd = (q.R % 8 == 0) ? 1 : 0;
+  q.chunk = ceil_div(ceil_div(n, q.R), kGiRows) * kGiRows;
+  return q;
+}
+
 static size_t gram2_lds() {
   const size_t lds = sizeof(double) * 2 * kG2Rows * kG2Stride;
   static bool attr = false;
@@ -1580,7 +1594,10 @@ extern "C" size_t mmb_gram_workspace_bytes(int64_t n, int d) {
   const size_t v1 = static_cast<size_t>(p.S) * p.npairs * kGB * kGB * sizeof(double);
   const Gram2Plan q = gram2_plan(n, d);
   const size_t v2 = static_cast<size_t>(q.R) * q.T * 256 * sizeof(double);
-  return v1 > v2 ? v1 : v2;
+  const Gram2Plan qi = gram_i8_plan(n, d);
+  const size_t v3 = static_cast<size_t>(qi.R) * qi.T * 256 * sizeof(double);
+  const size_t v23 = v2 > v3 ? v2 : v3;
+  return v1 > v23 ? v1 : v23;
 }
 
 extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, double* g,
@@ -1626,7 +1643,7 @@ extern "C" int mmb_colmax(const float* x, int64_t n, int d, uint32_t* colmax, in
 extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
                            int accumulate, void* ws, hipStream_t stream) {
   MMB_REQUIRE(x && colmax && g && ws && n >= 0 && d > 0 && d <= 304 && d % 4 == 0);
-  const Gram2Plan q = gram2_plan(n, d);
+  const Gram2Plan q = gram_i8_plan(n, d);
   MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
   // int32 level sums are per 64-row k-step, so any range length is safe
   double* part = static_cast<double*>(ws);
