@@ -64,6 +64,15 @@ def stream_kernel_bytes(L, D, A, Vd, text_rows=None):
     return 4 * L + 4 * L + 4 * D * tr + 4 * A * L + 4 * Vd * L + 4 * D + 4 * 2 * (D + A + Vd) + 8
 
 
+def fused_kernel_bytes(L, D, A, Vd, text_rows=None):
+    """Algorithmic HBM bytes per utterance of mmb_mm2_stream_project (the
+    stream kernel with the projection fused in): the same reads as
+    stream_kernel_bytes; writes the a2 row, the MMB2 row and aux (count,
+    sum w, row scale) -- the frame sums never leave the chip."""
+    tr = L if text_rows is None else text_rows
+    return 4 * L + 4 * L + 4 * D * tr + 4 * A * L + 4 * Vd * L + 4 * D + 4 * D + 12
+
+
 def path_bytes(L, D, A, Vd, text_rows=None):
     """SURVEY.md §8d B_utt for the whole step (149,120 B at the config-3 shape)."""
     tr = L if text_rows is None else text_rows
@@ -150,8 +159,9 @@ def phase_times(traces, steps):
             for n in names}
 
 
-def load_traffic(name, utts_per_launch, tokens):
-    """PMC-measured HBM bytes per stream-kernel launch for this exact workload,
+def load_traffic(name, utts_per_launch, tokens, phase="mm2_stream"):
+    """PMC-measured HBM bytes per stream-kernel launch for this exact workload
+    and kernel (the fused stream + projection or the plain stream kernel),
     from the committed rocprofv3 summaries (profiles/), never this run."""
     fn = {"synthetic": "traffic_latest.json"}.get(name, f"traffic_{name}_latest.json")
     path = os.path.join(ROOT, "profiles", fn)
@@ -159,7 +169,8 @@ def load_traffic(name, utts_per_launch, tokens):
         return None, None
     with open(path) as f:
         tj = json.load(f)
-    if tj.get("utts_per_launch") == utts_per_launch and tj.get("tokens") == tokens:
+    if (tj.get("utts_per_launch") == utts_per_launch and tj.get("tokens") == tokens
+            and tj.get("phase", "mm2_stream") == phase):
         return tj.get("mm2_stream_hbm_bytes_per_launch"), f"profiles/{fn} ({tj.get('tag')})"
     return None, None
 
@@ -190,11 +201,18 @@ def run_workload(P, inp, gen, steps, warmup, allreduce=None, world=1, rank=0):
     return step, elapsed, traces
 
 
+def stream_phase(phase_ms):
+    """The step's dominant (HBM-bound) phase: the fused stream + projection
+    kernel, or the stream kernel of the two-kernel step."""
+    return "mm2_stream_project" if "mm2_stream_project" in phase_ms else "mm2_stream"
+
+
 def stream_roofline(phase_ms, traces, steps, kbytes, U, kernel, traffic_key, T):
-    n_launch = sum(len(tr["mm2_stream"]) for tr in traces)
-    launch_ms = phase_ms["mm2_stream"] * steps / n_launch
+    ph = stream_phase(phase_ms)
+    n_launch = sum(len(tr[ph]) for tr in traces)
+    launch_ms = phase_ms[ph] * steps / n_launch
     achieved = kbytes * U / (launch_ms / 1e3) / 1e9
-    traffic, src = load_traffic(traffic_key, U, T)
+    traffic, src = load_traffic(traffic_key, U, T, ph)
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": (f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE passes of this workload, "
@@ -212,6 +230,18 @@ def mfma_rooflines(step, phase_ms, U, D):
     fp64 (D(D+1)/2 dot products of U terms)."""
     out = {}
     k_alg = 2 * (step.d + step.a + step.vd)
+    if "mm2_stream_project" in phase_ms:
+        # the projection runs inside the HBM-bound fused kernel (its own waves,
+        # overlapped with the stream): the MFMA rate over the whole kernel
+        flop = 3 * 2 * k_alg * (D + 1)
+        ms = phase_ms["mm2_stream_project"]
+        tf = flop * U / (ms / 1e3) / 1e12
+        out["mm2_stream_project (projector waves)"] = {
+            "bound": "hbm (the fused kernel)", "achieved": round(tf, 1),
+            "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(tf / F16_MFMA_PEAK_TFS, 4),
+            "flop_per_utt": flop, "ms": round(ms, 4),
+            "note": "fp16 x3 products issued beside the stream inside one kernel; the kernel is "
+                    "HBM-bound, so this is the MFMA work it hides, not a ceiling"}
     proj_ms = phase_ms.get("mm2_project+pc_remove", phase_ms.get("mm2_project+gram"))
     if proj_ms and step.s_half:
         flop = 3 * 2 * k_alg * (D + 1)
@@ -280,17 +310,33 @@ def time_fp32_projection(P, step, reps=3):
             "note": "mmb_mm2_project: fp32-input MFMA (exact f32 products), no fused removal"}
 
 
+def dominant_kernel(step, T, D, text_rows=None):
+    """(algorithmic bytes per utterance, name) of the step's HBM-bound kernel."""
+    if step.stream_project:
+        return (fused_kernel_bytes(T, D, step.a, step.vd, text_rows=text_rows),
+                "utt_fused_kernel (mmb_mm2_stream_project: 4 streaming waves, one per "
+                "utterance, + 4 projecting waves per CU, sums in an LDS ring)")
+    kname = ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
+             else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)")
+    return stream_kernel_bytes(T, D, step.a, step.vd, text_rows=text_rows), kname
+
+
 def stream_uniform_ids(P, step, kbytes, reps=3):
-    """The stream kernel on the same workload with UNIFORM token ids over
+    """The dominant kernel on the same workload with UNIFORM token ids over
     [1, V): every text row a likely L2 / Infinity-Cache miss, so the
     algorithmic-bytes roofline no longer counts Zipf cache hits."""
     import torch
 
     inp = step.inp
     ids_u = torch.randint(1, step.V, step.ids.shape, dtype=torch.int32, device=step.ids.device)
-    run = lambda: P.mm2_stream(step.n, step.t, step.d, step.a, step.vd, inp["audio"], inp["visual"],
-                               ids32=ids_u, table=step.table, wtab32=inp["wtab"], s_half=True,
-                               out=(step.x, step.s, step.aux))
+    if step.stream_project:
+        run = lambda: P.mm2_stream_project(step.n, step.t, step.d, step.a, step.vd, inp["audio"],
+                                           inp["visual"], step.proj, ids32=ids_u, table=step.table,
+                                           wtab32=inp["wtab"], out=(step.x, step.aux, step.mmb2))
+    else:
+        run = lambda: P.mm2_stream(step.n, step.t, step.d, step.a, step.vd, inp["audio"],
+                                   inp["visual"], ids32=ids_u, table=step.table,
+                                   wtab32=inp["wtab"], s_half=True, out=(step.x, step.s, step.aux))
     run()
     evs = []
     for _ in range(reps):
@@ -306,6 +352,34 @@ def stream_uniform_ids(P, step, kbytes, reps=3):
     return {"avg_launch_ms": round(ms, 4), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "note": "same frames and table, token ids uniform over [1, V) instead of Zipf(1.1)"}
+
+
+def two_kernel_step(P, step, gen, steps=5, warmup=1):
+    """The same workload through the two-kernel step (mmb_mm2_stream writes the
+    sums s to HBM, mmb_mm2_project_x3_rmpc reads them back and fuses the PC
+    removal), timed beside the fused default: the A/B of the fusion."""
+    import torch
+
+    two = P.FusedStep(step.inp, gen.networks(), stream_project=False)
+    for _ in range(warmup):
+        two.run()
+    traces = [dict() for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        two.run(trace=traces[k])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ph = phase_times(traces, steps)
+    diff = ((two.mmb2 - step.mmb2).abs().amax(1) / step.mmb2.abs().amax(1)).max().item()
+    out = {"ms_per_step": round(el * 1e3 / steps, 4), "value": round(step.n * steps / el, 1),
+           "phase_ms": {k: round(v, 4) for k, v in ph.items()},
+           "mmb2_row_rel_diff_vs_fused": diff,
+           "note": "mmb_mm2_stream -> s (fp16 hi/lo, 7.3 KB per utterance) in HBM -> "
+                   "mmb_mm2_project_x3_rmpc; same Gram / PC solve"}
+    del two
+    torch.cuda.empty_cache()
+    return out
 
 
 def ragged_config(P, models, synth, dev, steps, warmup, U):
@@ -325,9 +399,8 @@ def ragged_config(P, models, synth, dev, steps, warmup, U):
     gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
     step, elapsed, traces = run_workload(P, inp, gen, steps, warmup)
     ph = phase_times(traces, steps)
-    kb = stream_kernel_bytes(T, D, 300, 300, text_rows=nz + any0)
-    roof = stream_roofline(ph, traces, steps, kb, U, "utt_wave_kernel (one wave per utterance, "
-                           "T = 64)", "ragged", T)
+    kb, kname = dominant_kernel(step, T, D, text_rows=nz + any0)
+    roof = stream_roofline(ph, traces, steps, kb, U, kname + ", T = 64", "ragged", T)
     pb = path_bytes(T, D, 300, 300, text_rows=nz + any0)
     out = {"workload": "configs[3] ragged: Poisson(40) lengths clipped to [1, 64], padded to 64 "
                        "with id 0 (w0 = 1.0) and -10 frames, V = 400k, Zipf(1.1) ids, 3 x 300-d",
@@ -632,9 +705,7 @@ def main():
         return 0
 
     utts_per_launch = U // len(step.bounds) if len(step.bounds) > 1 else U
-    kb = stream_kernel_bytes(T, D, 300, 300, text_rows=text_rows)
-    kname = ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
-             else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)")
+    kb, kname = dominant_kernel(step, T, D, text_rows=text_rows)
     roof = stream_roofline(phase_ms, traces, args.steps, kb, utts_per_launch, kname, kind, T)
     pb = path_bytes(T, D, 300, 300, text_rows=text_rows)
     mfma = mfma_rooflines(step, phase_ms, U, D)
@@ -671,11 +742,20 @@ def main():
         "mfma_rooflines": mfma,
         "chunks": len(step.bounds),
     }
+    if "pc_remove" in phase_ms:  # separate removal pass: x read, SIF row written
+        rb = 2 * 4 * D
+        ach = rb * U / (phase_ms["pc_remove"] / 1e3) / 1e9
+        out["pc_remove_roofline"] = {"bound": "hbm", "achieved": round(ach, 1),
+                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_utt": rb,
+                                     "ms": round(phase_ms["pc_remove"], 4)}
     if world > 1:
         out["phase_ms"].setdefault("allreduce", None)
     cpu = None
     extras = world == 1 and not args.only_main and kind == "synthetic"
     if extras:
+        if step.stream_project:
+            out["step_two_kernels"] = two_kernel_step(P, step, gen)
         out["projection_fp32_mfma"] = time_fp32_projection(P, step)
         out["stream_uniform_ids"] = stream_uniform_ids(P, step, kb)
     sample = None

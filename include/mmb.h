@@ -37,6 +37,10 @@ extern "C" {
 /* an utterance whose SIF weights are all 0 (its a2 row is 0/0 = NaN, like
  * numpy's; the reference's TruncatedSVD then raises ValueError on the split) */
 #define MMB_FLAG_ZERO_WEIGHTS 2
+/* mmb_mm2_stream_project: a hand-over between its streaming and projecting
+ * waves waited ~0.5 s without progress (a bug, never expected); the kernel
+ * then ends at once and its MMB2 rows are invalid */
+#define MMB_FLAG_SYNC_TIMEOUT 4
 
 /* Library version (major*10000 + minor*100 + patch). */
 int mmb_version(void);
@@ -180,6 +184,37 @@ int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const floa
                    const float* audio, const float* visual, int64_t n, int t, int d, int a,
                    int vd, float* num_out, void* s_out, int s_half, float* aux_out,
                    int32_t* flag, uint32_t* colmax, void* colmax_ws, hipStream_t stream);
+
+/* mmb_mm2_stream and mmb_mm2_project_x3 in ONE kernel (the bench step's
+ * MMB2 path): the same num (x), aux[0..1] and colmax outputs as mmb_mm2_stream
+ * (aux[2] is the text piece's scale) and the MMB2 rows of mmb_mm2_project_x3
+ * (same fp16 x3 products; within f32 rounding of its sum order), but the
+ * per-utterance sums s never reach HBM: each workgroup's streaming waves
+ * stream a batch of 48 utterances modality by modality and leave each
+ * (utterance, modality) piece of sums in an LDS ring, its projecting waves
+ * multiply each piece of the batch with the piece-ordered fp16 hi/lo split
+ * of wm (wpieces from mmb_mm2_split_pieces; c0 from mmb_mm2_prepare).  Text
+ * by ids (table, wtab32 or w_dense) or dense (text_dense with w_dense, the
+ * weighted sum over the same rows).  Shapes: mmb_mm2_stream_project_supported
+ * (t <= 64, 256 <= d < 320, a and vd <= 320, widths % 4); 16-byte aligned
+ * rows.  MMB_EINVAL otherwise.
+ * replaces: the frame loops and projections of sif2.estimate_embedding_overall_gpu2
+ *   /root/reference/sif2.py:181-207 and the gathers at simplesif.py:862-871 */
+int mmb_mm2_stream_project_supported(int t, int d, int a, int vd);
+int mmb_mm2_stream_project(const int32_t* ids, const float* table, int64_t v,
+                           const float* wtab32, const float* text_dense, const float* w_dense,
+                           const float* audio, const float* visual, int64_t n, int t, int d,
+                           int a, int vd, const void* wpieces, const float* c0, float* num_out,
+                           float* aux_out, float* mmb2_out, int32_t* flag, uint32_t* colmax,
+                           void* colmax_ws, hipStream_t stream);
+
+/* The fp16 hi/lo split of wm [k, ldw] (mmb_mm2_prepare) in piece order for
+ * mmb_mm2_stream_project: each modality's 2 w_m rows [Sx_m | Sxx_m] padded
+ * to a multiple of 32, chunks and column scales as mmb_mm2_split_bytes'
+ * image, then the per-column 1/scale [ldw] f32.                             */
+size_t mmb_mm2_split_pieces_bytes(int d, int a, int vd);
+int mmb_mm2_split_pieces(const float* wm, int d, int a, int vd, int ldw, void* img,
+                         hipStream_t stream);
 
 /* colmax (nullable; d <= 640): the column bounds max_i |num[i,:]| of the a2
  * rows as float bits, the input of mmb_gram_i8 -- a by-product of the stream

@@ -169,13 +169,6 @@ __global__ void mm2_c0_reduce_kernel(const double* __restrict__ part, int D, int
 // C/D: col = l&31, row = (reg&3) + 8*(reg>>2) + 4*(l>>5).
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-// The weighted text sum sum_t w_t E_t of a row from the a2 row x = sum / count
-// that mmb_mm2_stream writes (count = count_nonzero(w), aux[0]): x * count,
-// within one rounding of the sum; 0 for a row whose weights are all zero
-// (x is then 0/0 = NaN, like the reference's a2, but the MMB2 text term is 0).
-__device__ __forceinline__ float text_sum(float x, float count) {
-  return count != 0.f ? x * count : 0.f;
-}
 
 constexpr int kPM = 64;   // rows per workgroup
 constexpr int kPK = 32;   // K chunk staged in LDS
@@ -297,9 +290,7 @@ __global__ __launch_bounds__(256) void mm2_project_kernel(const float* __restric
 // ~22 significant bits per operand, products exact, fp32 accumulation —
 // 5.3x fewer MFMA cycles than fp32 MFMA at fp32-class accuracy.
 // f16 32x32x16: lane l holds A[l&31][8(l>>5)+j] and B[8(l>>5)+j][l&31], j<8.
-using half8 = __attribute__((ext_vector_type(8))) _Float16;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
-using f32x4 = __attribute__((ext_vector_type(4))) float;
 using half4 = __attribute__((ext_vector_type(4))) _Float16;
 
 constexpr int kXM = 128;  // rows per workgroup (8 waves: 4 row tiles x 2 column halves)
@@ -308,17 +299,6 @@ constexpr int kXT = 512;  // threads
 constexpr int kXAbuf = 4; // A chunk ring (3 chunks in flight from HBM)
 constexpr int kXBbuf = 2; // B chunk ring (1 chunk in flight from L2)
 
-// 16-byte slot swizzle of a 64-byte LDS row (4 slots of 8 halves): row r
-// keeps data slot j at position j ^ swz(r).  A 64-byte row puts slot
-// position p of row r on bank set 4 (r mod 4) + p, so a ds_read_b128 lane
-// group (16 lanes: {0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same +32)
-// is conflict-free iff its 16 (row mod 4, position) pairs differ.  For the
-// 16x16x32 fragment reads (lane l: row 16 t + (l & 15), data slot l >> 4)
-// the groups read rows {0-3, 12-15} at one slot and rows {4-11} at the
-// next: swz over the four 4-row groups of a 16-row tile = 0, 2, 3, 1 makes
-// every group conflict-free (the former (r >> 2) & 3 left them 2-way:
-// SQ_LDS_BANK_CONFLICT = 48 % of the kernel's LDS cycles, r02 counters).
-__host__ __device__ constexpr int x3_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
 
 // Weight split, written in the projection kernel's B chunk image order so the
 // kernel stages B with straight 16-byte global->LDS copies:
@@ -343,6 +323,55 @@ __global__ void mm2_split_wm_kernel(const float* __restrict__ wm, int Kp, int ld
   }
   for (int k = tid; k < Kp; k += blockDim.x) {
     const float v = wm[static_cast<int64_t>(k) * ldw + j] * sc;
+    const _Float16 h = static_cast<_Float16>(v);
+    const int c = k / kXK, kk = k % kXK;
+    const int64_t at = static_cast<int64_t>(c) * 2 * ldw * kXK + static_cast<int64_t>(j) * kXK +
+                       ((kk >> 3) ^ x3_swz(j)) * 8 + (kk & 7);
+    img[at] = h;
+    img[at + static_cast<int64_t>(ldw) * kXK] = static_cast<_Float16>(v - static_cast<float>(h));
+  }
+  if (tid == 0) col_inv[j] = 1.f / sc;
+}
+
+// The same split in PIECE order for the fused stream + projection kernel
+// (mmb_mm2_stream_project): the K rows of each raw modality's sums
+// [Sx_m | Sxx_m] (2 w_m rows) padded to a multiple of 32, so every 32-deep
+// chunk belongs to one modality piece.  Chunk layout and column scales as
+// mm2_split_wm_kernel (the same col_inv).
+__global__ void mm2_split_wm_pieces_kernel(const float* __restrict__ wm, int ldw, int D, int A,
+                                           int Vd, _Float16* __restrict__ img,
+                                           float* __restrict__ col_inv) {
+  __shared__ float s_m[4];
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int w[3] = {D, A, Vd};
+  int src0[3], dst0[3], kq[3];
+  int sb = 0, db = 0;
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    src0[m] = sb;
+    dst0[m] = db;
+    kq[m] = (2 * w[m] + 31) / 32 * 32;
+    sb += 2 * w[m];
+    db += kq[m];
+  }
+  const int K = sb, Kq = db;
+  float m = 0.f;
+  for (int k = tid; k < K; k += blockDim.x) m = fmaxf(m, fabsf(wm[static_cast<int64_t>(k) * ldw + j]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, kWave));
+  if (lane == 0) s_m[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+  float sc = 1.f;
+  if (m > 0.f && isfinite(m)) {
+    int ex;
+    frexpf(m, &ex);
+    sc = ldexpf(1.f, 15 - ex);
+  }
+  for (int k = tid; k < Kq; k += blockDim.x) {
+    const int pm = k < dst0[1] ? 0 : (k < dst0[2] ? 1 : 2);
+    const int r = k - dst0[pm];
+    const float v = r < 2 * w[pm] ? wm[static_cast<int64_t>(src0[pm] + r) * ldw + j] * sc : 0.f;
     const _Float16 h = static_cast<_Float16>(v);
     const int c = k / kXK, kk = k % kXK;
     const int64_t at = static_cast<int64_t>(c) * 2 * ldw * kXK + static_cast<int64_t>(j) * kXK +
@@ -1814,4 +1843,24 @@ extern "C" int mmb_mm2_project(const float* s, const float* num, const float* au
     case 6: return launch_project<6>(s, num, aux, wm, c0, n, k, d, out, stream);
     default: return MMB_EINVAL;
   }
+}
+
+static int mm2_pieces_k(int d, int a, int vd) {
+  auto q = [](int w) { return (2 * w + 31) / 32 * 32; };
+  return q(d) + q(a) + q(vd);
+}
+
+extern "C" size_t mmb_mm2_split_pieces_bytes(int d, int a, int vd) {
+  const size_t ldw = mmb_mm2_ldw(d), kq = mm2_pieces_k(d, a, vd);
+  return 2 * ldw * kq * sizeof(_Float16) + ldw * sizeof(float);
+}
+
+extern "C" int mmb_mm2_split_pieces(const float* wm, int d, int a, int vd, int ldw, void* img,
+                                    hipStream_t stream) {
+  MMB_REQUIRE(wm && img && d > 0 && a > 0 && vd > 0 && ldw == mmb_mm2_ldw(d));
+  _Float16* im = static_cast<_Float16*>(img);
+  float* ci = reinterpret_cast<float*>(im + 2 * static_cast<size_t>(ldw) * mm2_pieces_k(d, a, vd));
+  mm2_split_wm_pieces_kernel<<<ldw, 256, 0, stream>>>(wm, ldw, d, a, vd, im, ci);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
 }

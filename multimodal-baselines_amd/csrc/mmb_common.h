@@ -99,6 +99,30 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// fp16 x3 projection operands (mm2_kernels.hip, the fused stream kernel)
+using half8 = __attribute__((ext_vector_type(8))) _Float16;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// The weighted text sum sum_t w_t E_t of a row from the a2 row x = sum / count
+// that mmb_mm2_stream writes (count = count_nonzero(w), aux[0]): x * count,
+// within one rounding of the sum; 0 for a row whose weights are all zero
+// (x is then 0/0 = NaN, like the reference's a2, but the MMB2 text term is 0).
+__device__ __forceinline__ float text_sum(float x, float count) {
+  return count != 0.f ? x * count : 0.f;
+}
+
+// 16-byte slot swizzle of a 64-byte LDS row (4 slots of 8 halves): row r
+// keeps data slot j at position j ^ swz(r).  A 64-byte row puts slot
+// position p of row r on bank set 4 (r mod 4) + p, so a ds_read_b128 lane
+// group (16 lanes: {0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same +32)
+// is conflict-free iff its 16 (row mod 4, position) pairs differ.  For the
+// 16x16x32 fragment reads (lane l: row 16 t + (l & 15), data slot l >> 4)
+// the groups read rows {0-3, 12-15} at one slot and rows {4-11} at the
+// next: swz over the four 4-row groups of a 16-row tile = 0, 2, 3, 1 makes
+// every group conflict-free (the former (r >> 2) & 3 left them 2-way:
+// SQ_LDS_BANK_CONFLICT = 48 % of the kernel's LDS cycles, r02 counters).
+__host__ __device__ constexpr int x3_swz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // CUs a launch on `stream` can use: the device's, or the subset a stream made

@@ -11,6 +11,7 @@
 // reductions leave the chip: the [N,L,300] gathered text tensor the reference
 // materialises (simplesif.py:319-340, :871) never exists.
 #include <cstdlib>
+#include <type_traits>
 
 #include "mmb_common.h"
 
@@ -457,120 +458,151 @@ __device__ __forceinline__ void split_store4(_Float16* hi, _Float16* lo, float4 
   }
 }
 
-template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false, bool SPLIT = false,
-          bool NTS = false>
-__global__ __launch_bounds__(256) void utt_wave_kernel(StreamArgs a) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
-  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+// Per-utterance sums of the wave-per-utterance kernels (utt_wave_kernel,
+// utt_fused_kernel): lane t stages token t, the frame loop broadcasts it with
+// v_readlane, lane l owns float4 columns l + 64 c of every row.
+template <int CT, int CA, int CV>
+struct UttSums {
+  float4 num[CT], sx[CT], sxx[CT], sa[CA], saa[CA], sv[CV], svv[CV];
+  float cnt, sw;
+};
+
+template <bool MM2, int CT, int CA, int CV, int UNR, bool NT, bool SPLIT>
+__device__ __forceinline__ void utt_sums(const StreamArgs& a, int64_t i, int lane,
+                                         UttSums<CT, CA, CV>& u) {
   const int UT = a.D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
   const float* tsrc = a.ids ? a.table : a.text_dense;
   const float* esrc = a.ids ? a.table : a.emb_dense;
   constexpr bool split_emb = MM2 && SPLIT;  // weighted sum over a different dense tensor
   const bool gather = a.ids != nullptr;
+  // stage: lane t <- token t (row id or -1, weight)
+  int rid = -1;
+  float w = 0.f;
+  if (lane < a.L) {
+    int64_t off;
+    stage_token(a, i, lane, off, w);
+    rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
+  }
+  u.cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+  u.sw = wave_sum(w);
+  // every weight 0: x is 0/0 = NaN (numpy's answer); the reference's
+  // TruncatedSVD then rejects the split -- report it through the flag word
+  if (lane == 0 && u.cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+
+  float4 (&num)[CT] = u.num;
+  float4 (&sx)[CT] = u.sx;
+  float4 (&sxx)[CT] = u.sxx;
+  float4 (&sa)[CA] = u.sa;
+  float4 (&saa)[CA] = u.saa;
+  float4 (&sv)[CV] = u.sv;
+  float4 (&svv)[CV] = u.svv;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int c = 0; c < CT; ++c) num[c] = sx[c] = sxx[c] = z4;
+#pragma unroll
+  for (int c = 0; c < CA; ++c) sa[c] = saa[c] = z4;
+#pragma unroll
+  for (int c = 0; c < CV; ++c) sv[c] = svv[c] = z4;
+  const float* abase = a.audio + i * a.L * a.A;
+  const float* vbase = a.visual + i * a.L * a.Vd;
+  const int64_t dbase = i * a.L;
+  // Column offsets clamped into the row so every lane loads unconditionally:
+  // lanes past a row's width read a valid duplicate and never store it.  A
+  // group of UNR frames issues ALL its loads before any accumulation — no
+  // branch separates them, so UNR frames x (CT+CA+CV) 16-B loads per lane
+  // are in flight together (a guarded load per lane would be waited on
+  // right after its branch: one load in flight per wave).
+  int ct[CT], ca[CA], cv[CV];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) ct[c] = 4 * min(lane + kWave * c, UT - 1);
+#pragma unroll
+  for (int c = 0; c < CA; ++c) ca[c] = 4 * min(lane + kWave * c, MM2 ? UA - 1 : 0);
+#pragma unroll
+  for (int c = 0; c < CV; ++c) cv[c] = 4 * min(lane + kWave * c, MM2 ? UV - 1 : 0);
+  auto frame = [&](int t, float4 (&vt)[CT], float4 (&ve)[CT], float4 (&va)[CA],
+                   float4 (&vv)[CV], float& wt, bool& ok) {
+    const int r = __builtin_amdgcn_readlane(rid, t);
+    wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+    ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
+    const int64_t o = (gather ? static_cast<int64_t>(ok ? r : 0) : dbase + t) * a.D;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      vt[c] = ld4(tsrc + o + ct[c]);
+      if (split_emb) ve[c] = ld4(esrc + o + ct[c]);
+    }
+    if constexpr (MM2) {
+#pragma unroll
+      for (int c = 0; c < CA; ++c) va[c] = ldnt4<NT>(abase + static_cast<int64_t>(t) * a.A + ca[c]);
+#pragma unroll
+      for (int c = 0; c < CV; ++c) vv[c] = ldnt4<NT>(vbase + static_cast<int64_t>(t) * a.Vd + cv[c]);
+    }
+  };
+  auto accum = [&](float4 (&vt)[CT], float4 (&ve)[CT], float4 (&va)[CA], float4 (&vv)[CV],
+                   float wt, bool ok) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const float4 v = ok ? vt[c] : z4;
+      fma4(num[c], wt, split_emb ? (ok ? ve[c] : z4) : v);
+      if constexpr (MM2) {
+        add4(sx[c], v);
+        sq4(sxx[c], v);
+      }
+    }
+    if constexpr (MM2) {
+#pragma unroll
+      for (int c = 0; c < CA; ++c) {
+        add4(sa[c], va[c]);
+        sq4(saa[c], va[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < CV; ++c) {
+        add4(sv[c], vv[c]);
+        sq4(svv[c], vv[c]);
+      }
+    }
+  };
+  int t = 0;
+  for (; t + UNR <= a.L; t += UNR) {
+    float4 vt[UNR][CT], ve[UNR][CT], va[UNR][CA], vv[UNR][CV];
+    float wt[UNR];
+    bool ok[UNR];
+#pragma unroll
+    for (int q = 0; q < UNR; ++q) frame(t + q, vt[q], ve[q], va[q], vv[q], wt[q], ok[q]);
+#pragma unroll
+    for (int q = 0; q < UNR; ++q) accum(vt[q], ve[q], va[q], vv[q], wt[q], ok[q]);
+  }
+  for (; t < a.L; ++t) {
+    float4 vt[CT], ve[CT], va[CA], vv[CV];
+    float wt;
+    bool ok;
+    frame(t, vt, ve, va, vv, wt, ok);
+    accum(vt, ve, va, vv, wt, ok);
+  }
+}
+
+template <bool MM2, int CT, int CA, int CV, int UNR = 2, bool NT = false, bool SPLIT = false,
+          bool NTS = false, int OCC = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void utt_wave_kernel(
+    StreamArgs a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  const int UT = a.D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
 
   float4 cmx[CT];  // running max |x| of this lane's columns (MMB2, mmb_gram_i8)
 #pragma unroll
   for (int c = 0; c < CT; ++c) cmx[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t i = wid; i < a.N; i += nw) {
-    // stage: lane t <- token t (row id or -1, weight)
-    int rid = -1;
-    float w = 0.f;
-    if (lane < a.L) {
-      int64_t off;
-      stage_token(a, i, lane, off, w);
-      rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
-    }
-    const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
-    const float sw = wave_sum(w);
-    // every weight 0: x is 0/0 = NaN (numpy's answer); the reference's
-    // TruncatedSVD then rejects the split -- report it through the flag word
-    if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
-
-    float4 num[CT], sx[CT], sxx[CT], sa[CA], saa[CA], sv[CV], svv[CV];
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int c = 0; c < CT; ++c) num[c] = sx[c] = sxx[c] = z4;
-#pragma unroll
-    for (int c = 0; c < CA; ++c) sa[c] = saa[c] = z4;
-#pragma unroll
-    for (int c = 0; c < CV; ++c) sv[c] = svv[c] = z4;
-    const float* abase = a.audio + i * a.L * a.A;
-    const float* vbase = a.visual + i * a.L * a.Vd;
-    const int64_t dbase = i * a.L;
-
-    // Column offsets clamped into the row so every lane loads unconditionally:
-    // lanes past a row's width read a valid duplicate and never store it.  A
-    // group of UNR frames issues ALL its loads before any accumulation — no
-    // branch separates them, so UNR frames x (CT+CA+CV) 16-B loads per lane
-    // are in flight together (a guarded load per lane would be waited on
-    // right after its branch: one load in flight per wave).
-    int ct[CT], ca[CA], cv[CV];
-#pragma unroll
-    for (int c = 0; c < CT; ++c) ct[c] = 4 * min(lane + kWave * c, UT - 1);
-#pragma unroll
-    for (int c = 0; c < CA; ++c) ca[c] = 4 * min(lane + kWave * c, MM2 ? UA - 1 : 0);
-#pragma unroll
-    for (int c = 0; c < CV; ++c) cv[c] = 4 * min(lane + kWave * c, MM2 ? UV - 1 : 0);
-    auto frame = [&](int t, float4 (&vt)[CT], float4 (&ve)[CT], float4 (&va)[CA],
-                     float4 (&vv)[CV], float& wt, bool& ok) {
-      const int r = __builtin_amdgcn_readlane(rid, t);
-      wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
-      ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
-      const int64_t o = (gather ? static_cast<int64_t>(ok ? r : 0) : dbase + t) * a.D;
-#pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        vt[c] = ld4(tsrc + o + ct[c]);
-        if (split_emb) ve[c] = ld4(esrc + o + ct[c]);
-      }
-      if constexpr (MM2) {
-#pragma unroll
-        for (int c = 0; c < CA; ++c) va[c] = ldnt4<NT>(abase + static_cast<int64_t>(t) * a.A + ca[c]);
-#pragma unroll
-        for (int c = 0; c < CV; ++c) vv[c] = ldnt4<NT>(vbase + static_cast<int64_t>(t) * a.Vd + cv[c]);
-      }
-    };
-    auto accum = [&](float4 (&vt)[CT], float4 (&ve)[CT], float4 (&va)[CA], float4 (&vv)[CV],
-                     float wt, bool ok) {
-#pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        const float4 v = ok ? vt[c] : z4;
-        fma4(num[c], wt, split_emb ? (ok ? ve[c] : z4) : v);
-        if constexpr (MM2) {
-          add4(sx[c], v);
-          sq4(sxx[c], v);
-        }
-      }
-      if constexpr (MM2) {
-#pragma unroll
-        for (int c = 0; c < CA; ++c) {
-          add4(sa[c], va[c]);
-          sq4(saa[c], va[c]);
-        }
-#pragma unroll
-        for (int c = 0; c < CV; ++c) {
-          add4(sv[c], vv[c]);
-          sq4(svv[c], vv[c]);
-        }
-      }
-    };
-    int t = 0;
-    for (; t + UNR <= a.L; t += UNR) {
-      float4 vt[UNR][CT], ve[UNR][CT], va[UNR][CA], vv[UNR][CV];
-      float wt[UNR];
-      bool ok[UNR];
-#pragma unroll
-      for (int q = 0; q < UNR; ++q) frame(t + q, vt[q], ve[q], va[q], vv[q], wt[q], ok[q]);
-#pragma unroll
-      for (int q = 0; q < UNR; ++q) accum(vt[q], ve[q], va[q], vv[q], wt[q], ok[q]);
-    }
-    for (; t < a.L; ++t) {
-      float4 vt[CT], ve[CT], va[CA], vv[CV];
-      float wt;
-      bool ok;
-      frame(t, vt, ve, va, vv, wt, ok);
-      accum(vt, ve, va, vv, wt, ok);
-    }
+    UttSums<CT, CA, CV> u;
+    utt_sums<MM2, CT, CA, CV, UNR, NT, SPLIT>(a, i, lane, u);
+    const float cnt = u.cnt, sw = u.sw;
+    float4 (&num)[CT] = u.num;
+    float4 (&sx)[CT] = u.sx;
+    float4 (&sxx)[CT] = u.sxx;
+    float4 (&sa)[CA] = u.sa;
+    float4 (&saa)[CA] = u.saa;
+    float4 (&sv)[CV] = u.sv;
+    float4 (&svv)[CV] = u.svv;
 
     if constexpr (MM2) {
       float m = 0.f;
@@ -689,20 +721,19 @@ __global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __rest
 // policy 0/1/2/3/4/5/6/7 = 20.65/20.62/21.00/19.94/20.54/19.80/20.57/20.09 ms;
 // uniform ids 26.87 (0) -> 24.23 (5).  MMB_STREAM_POLICY overrides it (read
 // once) for such sweeps.
+// Read per launch (in-process A/B sweeps flip it).  Bit 3 (policy 13):
+// the default variant compiled for two waves per SIMD (amdgpu_waves_per_eu).
 static int stream_policy() {
-  static const int p = [] {
-    const char* e = getenv("MMB_STREAM_POLICY");
-    return e ? atoi(e) : 5;
-  }();
-  return p;
+  const char* e = getenv("MMB_STREAM_POLICY");
+  return e ? atoi(e) : 5;
 }
 
-template <bool MM2, int CT, int CA, int CV, int UNR, bool NT, bool NTS>
+template <bool MM2, int CT, int CA, int CV, int UNR, bool NT, bool NTS, int OCC = 1>
 static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
   if (MM2 && a.ids == nullptr && a.emb_dense != a.text_dense) {
-    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, true, NTS><<<grid, 256, 0, stream>>>(a);
+    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, true, NTS, OCC><<<grid, 256, 0, stream>>>(a);
   } else {
-    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, false, NTS><<<grid, 256, 0, stream>>>(a);
+    utt_wave_kernel<MM2, CT, CA, CV, UNR, NT, false, NTS, OCC><<<grid, 256, 0, stream>>>(a);
   }
 }
 
@@ -729,7 +760,8 @@ static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nul
   if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
   if (parts) *parts = grid * 4;
-  switch (MM2 ? stream_policy() & 7 : 0) {
+  switch (MM2 ? stream_policy() & 15 : 0) {
+    case 13: launch_wave_v<MM2, CT, CA, CV, 4, true, false, 2>(a, grid, stream); break;
     case 1: launch_wave_v<MM2, CT, CA, CV, 2, true, false>(a, grid, stream); break;
     case 2: launch_wave_v<MM2, CT, CA, CV, 2, false, true>(a, grid, stream); break;
     case 3: launch_wave_v<MM2, CT, CA, CV, 2, true, true>(a, grid, stream); break;
@@ -738,6 +770,561 @@ static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nul
     case 6: launch_wave_v<MM2, CT, CA, CV, 4, false, true>(a, grid, stream); break;
     case 7: launch_wave_v<MM2, CT, CA, CV, 4, true, true>(a, grid, stream); break;
     default: launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream); break;
+  }
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+// ---------------------------------------------------------------- fused step
+// Stream + projection in ONE kernel (the bench step's MMB2 path): the frame
+// sums s of an utterance never leave the chip.  One persistent workgroup per
+// CU, 8 waves (two per SIMD):
+//   waves 0-3 (streamers)  stream the utterances of a batch of 48 consecutive
+//     rows modality by modality (text pass: gathered rows, the a2 row x, aux,
+//     the column bounds; then the audio pass, then the visual pass), leaving
+//     each (row, modality) piece of sums -- [Sx_m | Sxx_m], fp16 hi | lo of
+//     the piece scaled by a power of two -- in an LDS ring slot
+//   waves 4-7 (projectors) per piece of a batch: [48, 2 w_m] x [2 w_m, 320]
+//     fp16 x3 products (v_mfma_f32_16x16x32_f16, 3 row tiles x 5 column tiles
+//     per wave) with A from the ring and B straight from L2 (the piece-ordered
+//     weight split, mmb_mm2_split_pieces); the accumulators carry over from
+//     piece to piece (rescaled exactly by the ratio of the pieces' power-of-2
+//     scales); after the third piece the epilogue of mm2_project_x3b_kernel
+//     (text sum, total weight, L2 norm) on 80 columns per wave, the row totals
+//     and norms exchanged through LDS
+// Why piece-major 48-row batches: every batch re-reads the whole 2.3 MB weight
+// image from L2, and that L2 traffic is what competes with the HBM stream
+// (r02 ablation: 16-row whole-row batches -- 146 GB of L2 reads per 1M rows --
+// took the kernel from 20.2 ms, stream alone, to 26.0 ms).  LDS cannot hold 48
+// whole rows (7.3 KB each), but it holds 60 single-modality pieces (2.5 KB):
+// the projectors read piece m of the batch while the streamers fill piece m+1.
+// Hand-over through LDS counters (the two groups run at their own pace):
+//   fill[p % 4]  piece-rows of piece p (= 3 batch + modality) written
+//   consumed     projector waves done reading a piece (the streamers wait
+//                before overwriting a slot)
+//   pbar         the projectors' own exchange points (two per batch)
+// Every wait is bounded: after ~0.5 s without progress it raises
+// MMB_FLAG_SYNC_TIMEOUT and every later wait returns at once, so a broken
+// hand-over ends the kernel (wrong rows, flagged) instead of hanging the GPU.
+constexpr int kGR = 48;                 // rows per batch
+constexpr int kGRT = kGR / 16;          // MFMA row tiles per batch
+constexpr int kGSlots = 60;             // ring slots (piece-rows)
+constexpr int kGUnits = 80;             // 16-byte units per plane (piece <= 640 sums; XOR-16 headroom)
+constexpr int kGPlane = kGUnits * 8;    // halves per plane
+constexpr int kGSlot = 2 * kGPlane;     // halves per slot (hi | lo)
+constexpr int kFTiles = 5;              // 16-column tiles per projector (ldw = 320)
+constexpr int kFLdw = 320;
+constexpr int kFThreads = 512;
+constexpr size_t kGRingBytes = static_cast<size_t>(kGSlots) * kGSlot * sizeof(_Float16);
+// ring | irs [60] | counters [8] | cnt, tw [2][48] each | tot [2][48] | ssq [2][4][48]
+constexpr size_t kGLdsBytes =
+    kGRingBytes + kGSlots * 4 + 8 * 4 + 2 * 2 * kGR * 4 + 2 * kGR * 4 + 2 * 4 * kGR * 4;
+static_assert(kGLdsBytes <= 160 * 1024, "fused ring exceeds LDS");
+static_assert((kGSlot * 2) % 256 == 0 && (kGPlane * 2) % 256 == 0,
+              "slot and plane strides keep the XOR swizzle conflict-free");
+
+struct FusedArgs {
+  StreamArgs s;
+  const _Float16* img;     // piece-ordered B image (mmb_mm2_split_pieces), ldw = 320
+  const float* col_inv;    // [320] 1 / column scale
+  const float* c0;         // [320]
+  float* out;              // mmb2 [N][D]
+  int64_t nb;              // batches = ceil(N / 48)
+  int kq[3];               // padded piece widths (multiples of 32)
+};
+
+// bounded wait for *p >= target (workgroup scope); false once anything timed out
+__device__ __forceinline__ bool fused_wait(int* p, int target, int* abort_flag, int32_t* gflag) {
+  for (int it = 0; it < (1 << 23); ++it) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      return true;
+    }
+    if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (gflag && (threadIdx.x & (kWave - 1)) == 0) atomicOr(gflag, MMB_FLAG_SYNC_TIMEOUT);
+  return false;
+}
+// one increment per wave, ordered after this wave's earlier LDS / global writes
+__device__ __forceinline__ void fused_signal(int* p) {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Text piece of utterance i (one wave, lane l owns float4 columns l, l + 64):
+// the weighted sum num = sum_t w_t E_t, Sx, Sxx of the gathered rows, the
+// count of nonzero weights and their sum (utt_sums' text half).
+template <int UNR>
+__device__ __forceinline__ void text_piece(const StreamArgs& a, int64_t i, int lane, float4 (&num)[2],
+                                           float4 (&sx)[2], float4 (&sxx)[2], float& cnt, float& sw) {
+  const int UT = a.D >> 2;
+  const float* tsrc = a.ids ? a.table : a.text_dense;
+  const bool gather = a.ids != nullptr;
+  int rid = -1;
+  float w = 0.f;
+  if (lane < a.L) {
+    int64_t off;
+    stage_token(a, i, lane, off, w);
+    rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
+  }
+  cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+  sw = wave_sum(w);
+  if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
+  const int64_t dbase = i * a.L;
+  const int ct0 = 4 * min(lane, UT - 1), ct1 = 4 * min(lane + kWave, UT - 1);
+  auto frame = [&](int t, float4 (&v)[2], float& wt, bool& ok) {
+    const int r = __builtin_amdgcn_readlane(rid, t);
+    wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+    ok = r >= 0;
+    const int64_t o = (gather ? static_cast<int64_t>(ok ? r : 0) : dbase + t) * a.D;
+    v[0] = ld4(tsrc + o + ct0);
+    v[1] = ld4(tsrc + o + ct1);
+  };
+  auto accum = [&](const float4 (&v)[2], float wt, bool ok) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float4 x = ok ? v[c] : z4;
+      fma4(num[c], wt, x);
+      add4(sx[c], x);
+      sq4(sxx[c], x);
+    }
+  };
+  int t = 0;
+  for (; t + UNR <= a.L; t += UNR) {
+    float4 v[UNR][2];
+    float wt[UNR];
+    bool ok[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) frame(t + u, v[u], wt[u], ok[u]);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) accum(v[u], wt[u], ok[u]);
+  }
+  for (; t + 4 <= a.L; t += 4) {  // tail groups: keep loads in flight
+    float4 v[4][2];
+    float wt[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) frame(t + u, v[u], wt[u], ok[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) accum(v[u], wt[u], ok[u]);
+  }
+  for (; t < a.L; ++t) {
+    float4 v[2];
+    float wt;
+    bool ok;
+    frame(t, v, wt, ok);
+    accum(v, wt, ok);
+  }
+}
+
+// Audio / visual piece: Sx, Sxx over the L frames [L][W] at `base`
+// (read-once streams: non-temporal loads).
+template <int UNR, bool NT>
+__device__ __forceinline__ void frame_piece(const float* base, int W, int L, int lane,
+                                            float4 (&sx)[2], float4 (&sxx)[2]) {
+  const int UW = W >> 2;
+  const int c0 = 4 * min(lane, UW - 1), c1 = 4 * min(lane + kWave, UW - 1);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  sx[0] = sx[1] = sxx[0] = sxx[1] = z4;
+  int t = 0;
+  for (; t + UNR <= L; t += UNR) {
+    float4 v[UNR][2];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      v[u][0] = ldnt4<NT>(base + static_cast<int64_t>(t + u) * W + c0);
+      v[u][1] = ldnt4<NT>(base + static_cast<int64_t>(t + u) * W + c1);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        add4(sx[c], v[u][c]);
+        sq4(sxx[c], v[u][c]);
+      }
+  }
+  for (; t + 4 <= L; t += 4) {  // tail groups: keep loads in flight
+    float4 v[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u][0] = ldnt4<NT>(base + static_cast<int64_t>(t + u) * W + c0);
+      v[u][1] = ldnt4<NT>(base + static_cast<int64_t>(t + u) * W + c1);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        add4(sx[c], v[u][c]);
+        sq4(sxx[c], v[u][c]);
+      }
+  }
+  for (; t < L; ++t) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float4 x = ldnt4<NT>(base + static_cast<int64_t>(t) * W + (c ? c1 : c0));
+      add4(sx[c], x);
+      sq4(sxx[c], x);
+    }
+  }
+}
+
+// DIAG (timing-only builds, MMB_FUSED_DIAG; wrong MMB2 rows): bit 0 the
+// projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
+// no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
+// the frames (constant sums: the projectors alone)
+template <int UNR, bool NT, int DIAG = 0>
+__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_fused_kernel(
+    FusedArgs f) {
+  const StreamArgs& a = f.s;
+  extern __shared__ __attribute__((aligned(16))) _Float16 flds[];
+  _Float16* ring = flds;
+  float* s_irs = reinterpret_cast<float*>(flds + kGSlots * kGSlot);
+  int* ctr = reinterpret_cast<int*>(s_irs + kGSlots);   // fill[4], consumed, pbar, abort, -
+  float* s_cnt = reinterpret_cast<float*>(ctr + 8);     // [2][48]
+  float* s_tw = s_cnt + 2 * kGR;                        // [2][48]
+  float* s_tot = s_tw + 2 * kGR;                        // [2][48]
+  float* s_ssq = s_tot + 2 * kGR;                       // [2][4][48]
+  int* fill = ctr;
+  int* consumed = ctr + 4;
+  int* pbar = ctr + 5;
+  int* abort_flag = ctr + 6;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
+  if (tid < 8) ctr[tid] = 0;
+  __syncthreads();
+  const int64_t N = a.N;
+  const int G = gridDim.x;
+  const int D = a.D;
+
+  if (wave < 4) {
+    // ------------------------------------------------------------ streamer
+    const int wdt[3] = {a.D, a.A, a.Vd};
+    float4 cmx[2];
+    cmx[0] = cmx[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t j = 0;; ++j) {
+      const int64_t B = blockIdx.x + j * G;
+      if (B >= f.nb) break;
+#pragma unroll 1
+      for (int m = 0; m < 3; ++m) {
+        const int p = 3 * static_cast<int>(j) + m;  // piece sequence number
+        const int W = wdt[m], U = W >> 2;
+#pragma unroll 1
+        for (int r = 0; r < kGR / 4; ++r) {
+          const int q = wave + 4 * r;
+          const int64_t i = B * kGR + q;
+          if (i >= N) break;
+          float4 num[2], sx[2], sxx[2];
+          float cnt = 0.f, sw = 0.f;
+          if constexpr ((DIAG & 8) != 0) {
+            const float4 o4 = make_float4(1.f, 1.f, 1.f, 1.f);
+            num[0] = num[1] = sx[0] = sx[1] = sxx[0] = sxx[1] = o4;
+            cnt = sw = 1.f;
+          } else if (m == 0) {
+            text_piece<UNR>(a, i, lane, num, sx, sxx, cnt, sw);
+          } else {
+            const float* base = m == 1 ? a.audio + i * a.L * a.A : a.visual + i * a.L * a.Vd;
+            frame_piece<UNR, NT>(base, W, a.L, lane, sx, sxx);
+          }
+          float mx = 0.f;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) mx = fmaxf(mx, fmaxf(amax4(sx[c]), amax4(sxx[c])));
+          const float rs = row_scale(wave_max(mx));
+          if (m == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const int uu = lane + kWave * c;
+              if (uu < U) {
+                const float4 xr = div4(num[c], cnt);
+                st4(a.num_out + i * D + 4 * uu, xr);  // x = the a2 row
+                cmx[c] = make_float4(fmaxf(cmx[c].x, fabsf(xr.x)), fmaxf(cmx[c].y, fabsf(xr.y)),
+                                     fmaxf(cmx[c].z, fabsf(xr.z)), fmaxf(cmx[c].w, fabsf(xr.w)));
+              }
+            }
+            if (lane == 0) {
+              a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | text-piece scale
+              a.aux_out[N + i] = sw;
+              a.aux_out[2 * N + i] = rs;
+              s_cnt[(j & 1) * kGR + q] = cnt;
+              s_tw[(j & 1) * kGR + q] = sw;
+            }
+          }
+          // the slot's previous piece-row (pos - 60) must have been read by every projector
+          const int pos = p * kGR + q;
+          const int slot = pos % kGSlots;
+          if (pos >= kGSlots) fused_wait(consumed, ((pos - kGSlots) / kGR + 1) * 4, abort_flag, a.flag);
+          _Float16* srow = ring + slot * kGSlot;
+          const int qx = q & 15;  // row within its MFMA row tile: the XOR swizzle key
+          auto put = [&](int k, float4 v) {
+            const float x4[4] = {v.x * rs, v.y * rs, v.z * rs, v.w * rs};
+            h4 h, l;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              h[e] = static_cast<_Float16>(x4[e]);
+              l[e] = static_cast<_Float16>(x4[e] - static_cast<float>(h[e]));
+            }
+            const int o = (((k >> 3) ^ qx) << 3) + (k & 7);
+            *reinterpret_cast<h4*>(srow + o) = h;
+            *reinterpret_cast<h4*>(srow + kGPlane + o) = l;
+          };
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int uu = lane + kWave * c;
+            if (uu < U) {
+              put(4 * uu, sx[c]);
+              put(W + 4 * uu, sxx[c]);
+            }
+          }
+          for (int k = 2 * W + 4 * lane; k < f.kq[m]; k += 4 * kWave) put(k, make_float4(0.f, 0.f, 0.f, 0.f));
+          if (lane == 0) s_irs[slot] = 1.f / rs;  // a power of two: exact
+          fused_signal(&fill[p & 3]);
+        }
+      }
+    }
+    if (a.cmax_part) {  // this wave's column bounds (mmb_gram_i8)
+      const int64_t wid = static_cast<int64_t>(blockIdx.x) * 4 + wave;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int uu = lane + kWave * c;
+        if (uu < (D >> 2)) st4(a.cmax_part + wid * D + 4 * uu, cmx[c]);
+      }
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------- projector
+  const int pw = wave - 4;
+  const int q = lane & 15, g = lane >> 4;  // A row / B column in a tile; k group
+  constexpr int CH = 2 * kFLdw * 32, PL = kFLdw * 32;  // B image chunk / plane (halves)
+  const int nch = (f.kq[0] + f.kq[1] + f.kq[2]) / 32;
+  const int cb[3] = {0, f.kq[0] / 32, (f.kq[0] + f.kq[1]) / 32};
+  const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.img), 0, nch * CH * 2,
+                                                       0x00020000);
+  int boff[kFTiles];
+  float cinv[kFTiles], cadd[kFTiles];
+#pragma unroll
+  for (int t = 0; t < kFTiles; ++t) {
+    const int col = 16 * (kFTiles * pw + t) + q;
+    boff[t] = col * 32 + ((g ^ x3_swz(col)) << 3);
+    cinv[t] = f.col_inv[col];
+    cadd[t] = f.c0[col];
+  }
+  // column D (the total weight) lives in projector tD_w, tile tD_t, lane q == tD_q
+  const int tD = D >> 4, tD_w = tD / kFTiles, tD_t = tD % kFTiles, tD_q = D & 15;
+  // this projector's tiles holding columns <= D (the rest of the 320 are
+  // zero); 256 <= D < 320 leaves at most one dead tile, on projector 3
+  const int ntiles = max(kFTiles - 1, min(kFTiles, tD + 1 - kFTiles * pw));
+  int ep = 0;  // projector exchange points passed
+  for (int64_t j = 0;; ++j) {
+    const int64_t B = blockIdx.x + j * G;
+    if (B >= f.nb) break;
+    const int nvalid = static_cast<int>(N - B * kGR < kGR ? N - B * kGR : kGR);
+    f32x4 acc[kGRT][kFTiles];
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+      for (int t = 0; t < kFTiles; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float irs[kGRT][4];
+#pragma unroll 1
+    for (int m = 0; m < 3; ++m) {
+      const int p = 3 * static_cast<int>(j) + m;
+      fused_wait(&fill[p & 3], kGR * (p >> 2) + nvalid, abort_flag, a.flag);
+      if constexpr ((DIAG & 1) != 0) {
+        fused_signal(consumed);
+        continue;
+      }
+      // this piece's power-of-2 scales of the lane's output rows 16 rt + 4 g + jj;
+      // the running sums move to this piece's scale (exact: ratios of powers of 2)
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float v = s_irs[(p * kGR + 16 * rt + 4 * g + jj) % kGSlots];
+          if (m > 0) {
+            const float ratio = irs[rt][jj] / v;
+#pragma unroll
+            for (int t = 0; t < kFTiles; ++t) acc[rt][t][jj] *= ratio;
+          }
+          irs[rt][jj] = v;
+        }
+      const _Float16* arow[kGRT];
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt) arow[rt] = ring + ((p * kGR + 16 * rt + q) % kGSlots) * kGSlot;
+      const int npc = f.kq[m] / 32, c0g = cb[m];
+      // the K loop for NT live column tiles (tiles past column D hold zero
+      // padding: projector 3 at D = 300 skips their loads and MFMAs)
+      auto kloop = [&](auto nt_c) {
+        constexpr int NL = decltype(nt_c)::value;
+        half8 bh[2][NL], bl[2][NL];
+        auto ld_b = [&](int c, half8 (&h)[NL], half8 (&l)[NL]) {
+          const int so = (c0g + (c < npc ? c : npc - 1)) * CH * 2;
+#pragma unroll
+          for (int t = 0; t < NL; ++t) {
+            h[t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[t] * 2, so, 0));
+            l[t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (boff[t] + PL) * 2, so, 0));
+          }
+        };
+        auto chunk = [&](int c, const half8 (&h)[NL], const half8 (&l)[NL]) {
+          const int o = (((4 * c + g) ^ q) << 3);
+#pragma unroll
+          for (int rt = 0; rt < kGRT; ++rt) {
+            const half8 ah = *reinterpret_cast<const half8*>(arow[rt] + o);
+            const half8 al = *reinterpret_cast<const half8*>(arow[rt] + kGPlane + o);
+            if constexpr ((DIAG & 2) != 0) {
+              asm volatile("" ::"v"(ah), "v"(al));
+#pragma unroll
+              for (int t = 0; t < NL; ++t) asm volatile("" ::"v"(h[t]), "v"(l[t]));
+            } else {
+#pragma unroll
+              for (int t = 0; t < NL; ++t) {
+                acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, h[t], acc[rt][t], 0, 0, 0);
+                acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, l[t], acc[rt][t], 0, 0, 0);
+                acc[rt][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, h[t], acc[rt][t], 0, 0, 0);
+              }
+            }
+          }
+        };
+        ld_b(0, bh[0], bl[0]);
+        ld_b(1, bh[1], bl[1]);
+#pragma unroll 1
+        for (int c = 0; c < npc; c += 2) {
+          chunk(c, bh[0], bl[0]);
+          ld_b(c + 2, bh[0], bl[0]);
+          if (c + 1 < npc) {
+            chunk(c + 1, bh[1], bl[1]);
+            ld_b(c + 3, bh[1], bl[1]);
+          }
+        }
+      };
+      if (ntiles == kFTiles) {
+        kloop(std::integral_constant<int, kFTiles>{});
+      } else {
+        kloop(std::integral_constant<int, kFTiles - 1>{});
+      }
+      fused_signal(consumed);  // this projector's reads of the piece's slots are done
+    }
+    if constexpr ((DIAG & 5) != 0) {
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+        for (int t = 0; t < kFTiles; ++t) asm volatile("" ::"v"(acc[rt][t]));
+      continue;
+    }
+
+    // epilogue: lane value (rt, t, jj) = row 16 rt + 4 g + jj, column 16 (5 pw + t) + q
+    const int64_t row0 = B * kGR;
+    const float* cntb = s_cnt + (j & 1) * kGR;
+    const float* twb = s_tw + (j & 1) * kGR;
+    float* tot = s_tot + (j & 1) * kGR;
+    float* ssq = s_ssq + (j & 1) * 4 * kGR;
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt) {
+      float xv[kFTiles][4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int64_t rowc = min(row0 + 16 * rt + 4 * g + jj, N - 1);
+#pragma unroll
+        for (int t = 0; t < kFTiles; ++t) {
+          const int col = 16 * (kFTiles * pw + t) + q;
+          xv[t][jj] = a.num_out[rowc * D + min(col, D - 1)];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int r = 16 * rt + 4 * g + jj;
+        const float cn = cntb[r], tw = twb[r];
+#pragma unroll
+        for (int t = 0; t < kFTiles; ++t) {
+          const int col = 16 * (kFTiles * pw + t) + q;
+          const float add = col < D ? text_sum(xv[t][jj], cn) : (col == D ? tw : 0.f);
+          acc[rt][t][jj] = acc[rt][t][jj] * (cinv[t] * irs[rt][jj]) + add + cadd[t];
+        }
+        if (pw == tD_w && q == tD_q) {
+#pragma unroll
+          for (int t = 0; t < kFTiles; ++t)
+            if (t == tD_t) tot[r] = acc[rt][t][jj];
+        }
+      }
+    }
+    fused_signal(pbar);
+    fused_wait(pbar, 4 * ++ep, abort_flag, a.flag);
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int r = 16 * rt + 4 * g + jj;
+        const float rtot = 1.f / tot[r];
+        float ss = 0.f;
+#pragma unroll
+        for (int t = 0; t < kFTiles; ++t) {
+          const int col = 16 * (kFTiles * pw + t) + q;
+          acc[rt][t][jj] *= rtot;
+          if (col < D) ss = fmaf(acc[rt][t][jj], acc[rt][t][jj], ss);
+        }
+        ss = row16_sum(ss);
+        if (q == 0) ssq[pw * kGR + r] = ss;
+      }
+    }
+    fused_signal(pbar);
+    fused_wait(pbar, 4 * ++ep, abort_flag, a.flag);
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt) {
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int r = 16 * rt + 4 * g + jj;
+        const float inv = 1.f / sqrtf((ssq[r] + ssq[kGR + r]) + (ssq[2 * kGR + r] + ssq[3 * kGR + r]));
+        if (r < nvalid) {
+          float* orow = f.out + (row0 + r) * D;
+#pragma unroll
+          for (int t = 0; t < kFTiles; ++t) {
+            const int col = 16 * (kFTiles * pw + t) + q;
+            if (col < D) orow[col] = acc[rt][t][jj] * inv;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int DIAG, int UNR = 8>
+static void launch_fused_v(const FusedArgs& f, int grid, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_fused_kernel<UNR, true, DIAG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kGLdsBytes));
+    attr = true;
+  }
+  utt_fused_kernel<UNR, true, DIAG><<<grid, kFThreads, kGLdsBytes, stream>>>(f);
+}
+static int fused_unr() {  // streamer frames per load group (in-process sweeps)
+  const char* e = getenv("MMB_FUSED_UNR");
+  return e ? atoi(e) : 8;
+}
+
+static int fused_diag() {  // re-read per launch (in-process timing sweeps)
+  const char* e = getenv("MMB_FUSED_DIAG");
+  return e ? atoi(e) : 0;
+}
+
+static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
+  const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
+  if (parts) *parts = grid * 4;
+  const int dg = fused_diag(), un = fused_unr();
+  if (dg == 0 && un == 12) {
+    launch_fused_v<0, 12>(f, grid, stream);
+  } else if (dg == 0 && un == 16) {
+    launch_fused_v<0, 16>(f, grid, stream);
+  } else if (dg == 1 && un == 16) {
+    launch_fused_v<1, 16>(f, grid, stream);
+  } else switch (dg) {
+    case 1: launch_fused_v<1>(f, grid, stream); break;
+    case 2: launch_fused_v<2>(f, grid, stream); break;
+    case 4: launch_fused_v<4>(f, grid, stream); break;
+    case 8: launch_fused_v<8>(f, grid, stream); break;
+    default: launch_fused_v<0>(f, grid, stream); break;
   }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
@@ -977,6 +1564,63 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   if (rc != MMB_OK || !s_half) return rc;
   split_rows_kernel<<<static_cast<unsigned>(n), 256, s.Kp * sizeof(float), stream>>>(
       s.s_out, aux_out + 2 * n, s.Kp);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_mm2_stream_project_supported(int t, int d, int a_, int vd) {
+  // every piece [Sx | Sxx] of one modality fits a ring slot (2 w <= 640),
+  // two float4 columns per lane (w <= 512), the 320-column weight image
+  return t > 0 && t <= kWave && d >= 256 && d < 320 && d % 4 == 0 && a_ > 0 && vd > 0 &&
+         a_ % 4 == 0 && vd % 4 == 0 && 2 * a_ <= kGPlane && 2 * vd <= kGPlane;
+}
+
+extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, int64_t v,
+                                      const float* wtab32, const float* text_dense,
+                                      const float* w_dense, const float* audio, const float* visual,
+                                      int64_t n, int t, int d, int a_, int vd, const void* wpieces,
+                                      const float* c0, float* num_out, float* aux_out,
+                                      float* mmb2_out, int32_t* flag, uint32_t* colmax,
+                                      void* colmax_ws, hipStream_t stream) {
+  MMB_REQUIRE(n >= 0 && mmb_mm2_stream_project_supported(t, d, a_, vd));
+  MMB_REQUIRE(audio && visual && num_out && aux_out && mmb2_out && wpieces && c0);
+  MMB_REQUIRE(colmax == nullptr || colmax_ws != nullptr);
+  if (ids) {
+    MMB_REQUIRE(table && v > 0 && (wtab32 || w_dense) && aligned16(table));
+  } else {
+    MMB_REQUIRE(text_dense && w_dense && aligned16(text_dense));
+  }
+  MMB_REQUIRE(aligned16(audio) && aligned16(visual) && aligned16(num_out) && aligned16(wpieces));
+  if (n == 0) {
+    if (colmax) {
+      const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return MMB_OK;
+  }
+  FusedArgs f{};
+  StreamArgs& s = f.s;
+  s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.w_dense = w_dense;
+  s.text_dense = text_dense; s.emb_dense = text_dense; s.audio = audio; s.visual = visual;
+  s.N = n; s.L = t; s.D = d; s.A = a_; s.Vd = vd; s.Kp = mmb_mm2_k(d, a_, vd);
+  s.num_out = num_out; s.aux_out = aux_out; s.flag = flag; s.s_half = 1;
+  s.cmax_part = colmax ? static_cast<float*>(colmax_ws) : nullptr;
+  const int w3[3] = {d, a_, vd};
+  int kq = 0;
+  for (int m = 0; m < 3; ++m) {
+    f.kq[m] = (2 * w3[m] + 31) / 32 * 32;
+    kq += f.kq[m];
+  }
+  f.img = static_cast<const _Float16*>(wpieces);
+  f.col_inv = reinterpret_cast<const float*>(f.img + 2 * static_cast<size_t>(kFLdw) * kq);
+  f.c0 = c0;
+  f.out = mmb2_out;
+  f.nb = ceil_div(n, kGR);
+  int parts = 0;
+  const int rc = launch_fused(f, stream, &parts);
+  if (rc != MMB_OK || !colmax) return rc;
+  colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(
+      static_cast<const float*>(colmax_ws), parts, d, colmax);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(HERE, "libmmb.so")
 
 MMB_FLAG_ID_RANGE = 1
 MMB_FLAG_ZERO_WEIGHTS = 2
+MMB_FLAG_SYNC_TIMEOUT = 4
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -56,8 +57,13 @@ SIGNATURES = {
     "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _I,
                             _P, _P, _P, _P, _P]),
     "mmb_mm2_colmax_ws_bytes": (_S, [_I]),
+    "mmb_mm2_stream_project_supported": (_I, [_I, _I, _I, _I]),
+    "mmb_mm2_stream_project": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P,
+                                    _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "mmb_mm2_split_bytes": (_S, [_I, _I, _I]),
+    "mmb_mm2_split_pieces_bytes": (_S, [_I, _I, _I]),
+    "mmb_mm2_split_pieces": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
     "mmb_mm2_project_x3": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
     "mmb_mm2_project_x3_rmpc": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P, _P, _P]),

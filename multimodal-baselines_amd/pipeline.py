@@ -69,6 +69,9 @@ def check_flag(flag: torch.Tensor, V: int, zero_weights: bool = False):
     0/0 = NaN (sif_functions.py:55) and the reference's TruncatedSVD rejects
     the split (sklearn check_array: "Input X contains NaN")."""
     f = int(flag.item())
+    if f & L.MMB_FLAG_SYNC_TIMEOUT:
+        raise RuntimeError("mmb_mm2_stream_project: a hand-over between its streaming and "
+                           "projecting waves timed out; the step's MMB2 rows are invalid")
     if f & L.MMB_FLAG_ID_RANGE:
         raise IndexError(f"token id out of bounds for a vocabulary of size {V}")
     if zero_weights and f & L.MMB_FLAG_ZERO_WEIGHTS:
@@ -327,7 +330,20 @@ class MMB2Projection:
         arr = lambda i: (ctypes_ptr_array([p[i].data_ptr() for p in self.params]))
         L.call("mmb_mm2_prepare", arr(0), arr(1), arr(2), arr(3), self.d, self.a, self.vd, self.t,
                L.ptr(self.wm), self.ldw, L.ptr(self.c0), L.ptr(self.wsplit), L.stream_ptr())
+        if getattr(self, "wpieces", None) is not None:
+            L.call("mmb_mm2_split_pieces", L.ptr(self.wm), self.d, self.a, self.vd, self.ldw,
+                   L.ptr(self.wpieces), L.stream_ptr())
         self._seen = self._versions()
+
+    def enable_pieces(self):
+        """Also keep the piece-ordered split of wm (mmb_mm2_split_pieces), the
+        B operand of the fused stream + projection kernel."""
+        if getattr(self, "wpieces", None) is None:
+            nbytes = L.query("mmb_mm2_split_pieces_bytes", self.d, self.a, self.vd)
+            self.wpieces = torch.empty((nbytes + 15) // 16 * 16, dtype=torch.uint8,
+                                       device=self.wm.device)
+            L.call("mmb_mm2_split_pieces", L.ptr(self.wm), self.d, self.a, self.vd, self.ldw,
+                   L.ptr(self.wpieces), L.stream_ptr())
 
     def refresh_if_changed(self) -> bool:
         """Re-merge only when a generator parameter changed in place since the
@@ -371,6 +387,33 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
            L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag), L.ptr(colmax),
            L.ptr(colmax_ws), L.stream_ptr())
     return num, s, aux
+
+
+def stream_project_supported(t: int, d: int, a: int, vd: int) -> bool:
+    """Shapes the fused stream + projection kernel takes (t <= 64 frames,
+    256 <= d < 320, widths % 4, k <= 1920): the bench / MOSI-like configs."""
+    return bool(L.query("mmb_mm2_stream_project_supported", t, d, a, vd))
+
+
+def mm2_stream_project(n, t, d, a, vd, audio, visual, proj: "MMB2Projection", ids32=None,
+                       table=None, wtab32=None, text_dense=None, w_dense=None, flag=None,
+                       out=None, colmax=None, colmax_ws=None):
+    """a6-a8 in ONE kernel (mmb_mm2_stream_project): x, aux (and the column
+    bounds) as mm2_stream, plus the MMB2 rows of mm2_project -- the sums s
+    stay in LDS.  Returns (x, aux, mmb2)."""
+    dev = audio.device
+    if out is None:
+        out = (torch.empty((n, d), dtype=torch.float32, device=dev),
+               torch.empty((3, n), dtype=torch.float32, device=dev),
+               torch.empty((n, d), dtype=torch.float32, device=dev))
+    num, aux, mmb2 = out
+    proj.enable_pieces()
+    V = table.shape[0] if table is not None else 0
+    L.call("mmb_mm2_stream_project", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32),
+           L.ptr(text_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
+           L.ptr(proj.wpieces), L.ptr(proj.c0), L.ptr(num), L.ptr(aux), L.ptr(mmb2), L.ptr(flag),
+           L.ptr(colmax), L.ptr(colmax_ws), L.stream_ptr())
+    return num, aux, mmb2
 
 
 def s_buffer(n: int, kp: int, s_half: bool, device) -> torch.Tensor:
@@ -499,7 +542,7 @@ class FusedStep:
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
                  side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True,
-                 gram_kind: str | None = None):
+                 gram_kind: str | None = None, stream_project: bool | None = None):
         self.inp = inputs
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
@@ -512,7 +555,15 @@ class FusedStep:
         kp = self.proj.kp
         self.x = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.s_half = x3_supported(self.proj)
-        self.s = s_buffer(self.n, kp, self.s_half, dev)
+        # stream + projection in one kernel (s never in HBM): one chunk, the
+        # shapes the kernel takes; MMB_STREAM_PROJECT=0 keeps the two kernels
+        if stream_project is None:
+            stream_project = os.environ.get("MMB_STREAM_PROJECT", "1") != "0"
+        self.stream_project = (bool(stream_project) and (chunks or 1) == 1 and self.s_half
+                               and stream_project_supported(self.t, self.d, self.a, self.vd))
+        self.s = None if self.stream_project else s_buffer(self.n, kp, self.s_half, dev)
+        if self.stream_project:
+            self.proj.enable_pieces()
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
@@ -638,6 +689,24 @@ class FusedStep:
         nb = len(self.bounds)
         with mark("mm2_prepare"):
             self.proj.refresh_if_changed()
+        if self.stream_project:
+            inp = self.inp
+            with mark("mm2_stream_project"):
+                mm2_stream_project(self.n, self.t, self.d, self.a, self.vd, inp["audio"],
+                                   inp["visual"], self.proj, ids32=self.ids, table=self.table,
+                                   wtab32=inp["wtab"], flag=self.flag,
+                                   out=(self.x, self.aux_of(0), self.mmb2), colmax=self.colmax,
+                                   colmax_ws=self.colmax_ws)
+            with mark("gram"):
+                if self.gram_i8:
+                    gram_i8(self.x, self.colmax, self.G, ws=self.gws)
+                else:
+                    gram(self.x, None, self.G, ws=self.gws)
+            pc = self._solve(trace, mark)
+            with mark("pc_remove"):
+                remove_pc(self.x, None, pc, out=self.sif)
+            self.pc = pc
+            return self.sif, self.mmb2
         with mark("mm2_stream"):
             self._stream_chunk(0)  # every CU
         if self.fused_remove:

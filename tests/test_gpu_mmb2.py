@@ -201,12 +201,12 @@ def test_fused_pc_removal_matches_separate_kernel(gpu, N):
     inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=21, device=gpu)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    fused = P.FusedStep(inp, gen.networks())
+    fused = P.FusedStep(inp, gen.networks(), stream_project=False)
     assert fused.fused_remove
     trace = {}
     s1, m1 = [t.clone() for t in fused.run(trace=trace)]
     assert "mm2_project+pc_remove" in trace and "pc_remove" not in trace
-    sep = P.FusedStep(inp, gen.networks(), fuse_remove=False)
+    sep = P.FusedStep(inp, gen.networks(), fuse_remove=False, stream_project=False)
     assert not sep.fused_remove
     s2, m2 = sep.run()
     torch.cuda.synchronize()
@@ -228,7 +228,7 @@ def test_chunked_overlapped_step_matches_single_chunk(gpu):
     inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=11, device=gpu)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    one = P.FusedStep(inp, gen.networks(), chunks=1)
+    one = P.FusedStep(inp, gen.networks(), chunks=1, stream_project=False)
     s1, m1 = [t.clone() for t in one.run()]
     three = P.FusedStep(inp, gen.networks(), chunks=3)
     assert len(three.bounds) == 3
@@ -251,7 +251,7 @@ def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
     inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=12, device=gpu)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    one = P.FusedStep(inp, gen.networks(), chunks=1)
+    one = P.FusedStep(inp, gen.networks(), chunks=1, stream_project=False)
     s1, m1 = [t.clone() for t in one.run()]
     four = P.FusedStep(inp, gen.networks(), chunks=4, side_cus=side_cus)
     assert len(four.bounds) == 4 and four.gram_parts
@@ -273,7 +273,7 @@ def test_projection_variants_bit_identical(gpu, N, variant, monkeypatch):
     inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=41, device=gpu)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    step = P.FusedStep(inp, gen.networks())
+    step = P.FusedStep(inp, gen.networks(), stream_project=False)
     s1, m1 = [t.clone() for t in step.run()]
     monkeypatch.setenv("MMB_PROJ_VARIANT", variant)
     step.sif.zero_()
@@ -565,3 +565,74 @@ def test_step_remerges_weights_only_after_an_update(gpu):
     torch.cuda.synchronize()
     assert not torch.equal(m1, m2)
     assert torch.equal(m2, m3)
+
+
+@pytest.mark.parametrize("N,T,A,Vd", [(2048, 40, 300, 300), (1, 40, 300, 300), (15, 40, 300, 300),
+                                     (17, 12, 300, 300), (700, 64, 300, 300), (5003, 40, 300, 300),
+                                     (999, 33, 260, 292), (300, 40, 300, 256), (97, 40, 300, 20),
+                                     (49, 40, 100, 300)])
+def test_stream_project_matches_two_kernel_step(gpu, N, T, A, Vd):
+    """The fused stream + projection kernel (mmb_mm2_stream_project: the sums
+    s stay in an LDS ring, 48-row batches streamed modality by modality,
+    partial last batch, narrow audio / visual widths)
+    against the two-kernel step (mmb_mm2_stream -> HBM s -> mmb_mm2_project_x3):
+    x, count, weight sum and the column bounds bit-identical, MMB2 rows to f32
+    rounding (per-piece scales, the same fp16 x3 products), PC-removed rows to
+    the fp64 dot order -- and both against the CPU oracle."""
+    from oracle import sif_oracle as O
+
+    V = 20_000
+    inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=61, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
+    a = P.FusedStep(inp, gen.networks(), stream_project=True)
+    b = P.FusedStep(inp, gen.networks(), stream_project=False)
+    assert a.stream_project and a.s is None and not b.stream_project
+    trace = {}
+    s1, m1 = [t.clone() for t in a.run(trace=trace)]
+    assert "mm2_stream_project" in trace and "pc_remove" in trace
+    s2, m2 = b.run()
+    torch.cuda.synchronize()
+    a.check()
+    assert int(a.flag.item()) == 0
+    # aux[2] is the text piece's scale in the fused kernel (the whole row's before)
+    assert torch.equal(a.x, b.x) and torch.equal(a.aux[:2], b.aux[:2])
+    assert torch.equal(a.colmax, b.colmax)
+    assert M.row_rel_err(m1.cpu().numpy(), m2.cpu().numpy()) < 1e-6
+    assert torch.equal(a.pc, b.pc)
+    # SIF rows to the fp64 dot order, relative to the a2 rows (N = 1 removes
+    # the whole row: x - (x . pc) pc is ~1e-14 of x)
+    xmax = a.x.abs().max().item()
+    assert (s1 - s2).abs().max().item() <= 1e-6 * xmax
+    E = inp["table"].cpu().numpy()
+    wt = inp["wtab"].cpu().numpy().astype(np.float64)
+    ids = inp["ids"].cpu().numpy().astype(np.int64)
+    if N > 1:
+        ref_sif = O.get_sentence_embeddings(E, wt, ids)
+        assert M.row_rel_err(s1.cpu().numpy(), ref_sif) < TOL
+    if N == 1:  # the reference's gpu2 cannot take one utterance (squeeze, sif2.py:200-207)
+        return
+    audio, visual = inp["audio"].cpu().numpy(), inp["visual"].cpu().numpy()
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    text = E[ids]
+    ref_mm2 = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio, visual),
+                                                 M.params_from_module(gen.cpu()), sw, text)
+    assert M.row_rel_err(m1.cpu().numpy(), ref_mm2) < TOL
+
+
+def test_stream_project_repeatable_and_unit_rows(gpu):
+    """Bench-like size (60k utterances, V = 400k Zipf ids): two steps of the
+    fused kernel are bit-identical (the ring hand-over is order-independent),
+    rows are unit length, no hand-over timed out."""
+    inp = synth.device_workload(60_000, 40, 400_000, seed=62, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks())
+    assert step.stream_project
+    s1, m1 = [t.clone() for t in step.run()]
+    s2, m2 = step.run()
+    torch.cuda.synchronize()
+    step.check()
+    assert torch.equal(s1, s2) and torch.equal(m1, m2)
+    norms = torch.linalg.norm(m1.double(), dim=1)
+    assert (norms - 1).abs().max().item() < 1e-5

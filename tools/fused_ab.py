@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""In-process A/B of the bench step: two kernels (stream -> HBM s ->
+projection with the fused PC removal) vs the fused stream + projection
+kernel (s in LDS; separate PC removal).  Interleaved rounds, per-phase HIP
+event times, median per variant.
+
+    python tools/fused_ab.py [--n 1000000] [--rounds 4] [--steps 3]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-baselines_amd"))
+
+import torch  # noqa: E402
+
+import models  # noqa: E402
+import pipeline as P  # noqa: E402
+import synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--diags", default="",
+                    help="comma list of MMB_FUSED_DIAG[:MMB_FUSED_UNR] values: kernel-only "
+                         "timing of the fused kernel's ablations / streamer load-group sizes "
+                         "beside the plain stream kernel")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    inp = synth.device_workload(args.n, 40, 400_000, seed=1, device=dev)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
+    steps = {"two_kernel": P.FusedStep(inp, gen.networks(), stream_project=False),
+             "fused": P.FusedStep(inp, gen.networks(), stream_project=True)}
+    for k, st in steps.items():
+        st.run()
+    torch.cuda.synchronize()
+    for st in steps.values():
+        st.check()
+    a, b = steps["two_kernel"], steps["fused"]
+    print("x equal:", torch.equal(a.x, b.x), " mmb2 max abs diff:",
+          (a.mmb2 - b.mmb2).abs().max().item(), " sif max abs diff:",
+          (a.sif - b.sif).abs().max().item(), flush=True)
+    res = {k: {} for k in steps}
+    for r in range(args.rounds):
+        for k, st in steps.items():
+            tr = {}
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.steps):
+                st.run(trace=tr)
+            e1.record()
+            torch.cuda.synchronize()
+            res[k].setdefault("step", []).append(e0.elapsed_time(e1) / args.steps)
+            for ph, evs in tr.items():
+                res[k].setdefault(ph, []).append(sum(x.elapsed_time(y) for x, y in evs) / args.steps)
+        print(f"round {r}: " + "  ".join(f"{k} {res[k]['step'][-1]:.3f} ms" for k in steps), flush=True)
+    for k in steps:
+        print(k + ": " + ", ".join(f"{ph} {statistics.median(v):.3f}" for ph, v in res[k].items()))
+    steps["fused"].check()
+    if not args.diags:
+        return
+    inputs = dict(audio=inp["audio"], visual=inp["visual"], ids32=inp["ids"], table=inp["table"],
+                  wtab32=inp["wtab"])
+
+    def stream():
+        P.mm2_stream(a.n, 40, 300, 300, 300, out=(a.x, a.s, a.aux), colmax=a.colmax,
+                     colmax_ws=a.colmax_ws, **inputs)
+
+    def fused():
+        P.mm2_stream_project(b.n, 40, 300, 300, 300, proj=b.proj, out=(b.x, b.aux, b.mmb2),
+                             colmax=b.colmax, colmax_ws=b.colmax_ws, **inputs)
+
+    variants = [("stream", "0", stream), ("fused", "0", fused)]
+    variants += [(f"fused diag:unr {d}", d, fused) for d in args.diags.split(",") if d]
+    kt = {name: [] for name, _, _ in variants}
+    for r in range(args.rounds):
+        for name, dg, fn in variants:
+            dg, _, un = dg.partition(":")
+            os.environ["MMB_FUSED_DIAG"] = dg
+            os.environ["MMB_FUSED_UNR"] = un or "8"
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.steps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            kt[name].append(e0.elapsed_time(e1) / args.steps)
+    os.environ["MMB_FUSED_DIAG"] = "0"
+    os.environ["MMB_FUSED_UNR"] = "8"
+    for name in kt:
+        print(f"kernel {name}: median {statistics.median(kt[name]):.3f} ms  min {min(kt[name]):.3f}")
+
+
+if __name__ == "__main__":
+    main()

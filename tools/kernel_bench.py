@@ -50,7 +50,7 @@ def main():
         inp["ids"].copy_((base[:, None] + torch.arange(args.t, device=dev)[None, :] + 1).to(torch.int32))
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
-    step = P.FusedStep(inp, gen.networks(), chunks=1)
+    step = P.FusedStep(inp, gen.networks(), chunks=1, stream_project=False)
     step.run()
     torch.cuda.synchronize()
     which = set(args.which)

@@ -37,7 +37,7 @@ def main():
     inp = synth.device_workload(args.n, 40, 400_000, seed=1, device=dev)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
-    step = P.FusedStep(inp, gen.networks(), chunks=1)
+    step = P.FusedStep(inp, gen.networks(), chunks=1, stream_project=False)
     step.run()
     torch.cuda.synchronize()
     pc = step.pc

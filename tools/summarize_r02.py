@@ -38,7 +38,8 @@ def main(src, tag):
              json.dumps(bench, indent=1), "```", ""]
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
     tb = json.load(open(os.path.join(src, "trace_bench.json")))
-    rp = [float(r["AverageNs"]) / 1e6 for r in stats if "utt_wave_kernel" in r["Name"]]
+    rp = [float(r["AverageNs"]) / 1e6 for r in stats
+          if "utt_fused_kernel" in r["Name"] or "utt_wave_kernel" in r["Name"]]
     lines += ["## traced run: HIP events vs rocprofv3 (same process)", "",
               f"stream kernel avg launch: HIP events {tb['roofline']['avg_launch_ms']:.4f} ms, "
               f"rocprofv3 {rp[0] if rp else float('nan'):.4f} ms; traced-run value "
@@ -72,7 +73,9 @@ def main(src, tag):
             b = (2 * fv + wv) * 1024
             traffic[k] = b
             lines.append(f"| `{k}` | {len(fetch[k])} | {fv:.0f} | {wv:.0f} | {b:.4g} |")
-        stream = [v for k, v in traffic.items() if "utt_stream_kernel" in k or "utt_wave_kernel" in k]
+        fused = [v for k, v in traffic.items() if "utt_fused_kernel" in k]
+        stream = fused or [v for k, v in traffic.items()
+                           if "utt_stream_kernel" in k or "utt_wave_kernel" in k]
         cfg = wb["config"]
         alg = wb["roofline"]["algorithmic_bytes_per_utt"] * cfg["utts_per_gpu"]
         if stream:
@@ -81,6 +84,7 @@ def main(src, tag):
         lines.append("")
         tj = {"tag": tag, "workload": wl, "utts_per_launch": cfg["utts_per_gpu"],
               "tokens": cfg["tokens"], "mm2_stream_hbm_bytes_per_launch": stream[0] if stream else None,
+              "phase": "mm2_stream_project" if fused else "mm2_stream",
               "algorithmic_bytes_per_launch": alg, "per_kernel_hbm_bytes_per_launch": traffic}
         name = "traffic_latest.json" if wl == "synthetic" else f"traffic_{wl}_latest.json"
         for fn in (f"{tag}_traffic_{wl}.json", name):
