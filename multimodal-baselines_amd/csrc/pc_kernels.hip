@@ -1478,6 +1478,90 @@ __global__ __launch_bounds__(256) void pc_remove_kernel(const TX* __restrict__ n
   }
 }
 
+// One PC, f32 rows of 256 < D <= 512 (float4 columns l and l + 64 per lane):
+// R rows per wave in flight -- all 2R row loads issued before the first dot,
+// the R wave sums interleaved -- where pc_remove_kernel has one row and its
+// dependent load -> dot -> sum -> store chain per wave; the PC's lane values
+// stay in registers.  Arithmetic (f64 fma order, shuffle-tree wave sum, f32
+// rounding) is pc_remove_kernel<4, 2>'s: bit-identical.
+template <int R>
+__global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict__ num,
+                                                         const float* __restrict__ cnt, int64_t N,
+                                                         int D, const double* __restrict__ pc,
+                                                         float* __restrict__ out32) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int U = D / 4;
+  const bool h1 = lane + kWave < U;
+  double p[2][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    p[0][e] = lane < U ? pc[4 * lane + e] : 0.0;
+    p[1][e] = h1 ? pc[4 * (lane + kWave) + e] : 0.0;
+  }
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  for (int64_t base = (static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave) * R;
+       base < N; base += nw * R) {
+    float4 v[R][2];
+    float sc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t row = min(base + r, N - 1);
+      const float* src = num + row * D;
+      v[r][0] = lane < U ? *reinterpret_cast<const float4*>(src + 4 * lane) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[r][1] = h1 ? *reinterpret_cast<const float4*>(src + 4 * (lane + kWave)) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sc[r] = cnt ? cnt[row] : 1.f;
+    }
+    double x[R][2][4], d[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const float e4[4] = {v[r][m].x, v[r][m].y, v[r][m].z, v[r][m].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[r][m][e] = static_cast<double>(cnt ? e4[e] / sc[r] : e4[e]);
+      }
+      double acc = 0.0;
+      if (lane < U) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = fma(x[r][0][e], p[0][e], acc);
+      }
+      if (h1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = fma(x[r][1][e], p[1][e], acc);
+      }
+      d[r] = acc;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[r] += __shfl_xor(d[r], o, kWave);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (base + r >= N) break;
+      float* dst = out32 + (base + r) * D;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        if (m == 0 ? lane < U : h1) {
+          float4 q;
+          q.x = static_cast<float>(x[r][m][0] - fma(d[r], p[m][0], 0.0));
+          q.y = static_cast<float>(x[r][m][1] - fma(d[r], p[m][1], 0.0));
+          q.z = static_cast<float>(x[r][m][2] - fma(d[r], p[m][2], 0.0));
+          q.w = static_cast<float>(x[r][m][3] - fma(d[r], p[m][3], 0.0));
+          *reinterpret_cast<float4*>(dst + 4 * (lane + kWave * m)) = q;
+        }
+      }
+    }
+  }
+}
+
+// pc_remove1_kernel rows per wave (2, 4, 8); 0 = pc_remove_kernel (default
+// until measured)
+static int remove_rows() {
+  const char* e = getenv("MMB_PC_REMOVE_R");
+  return e ? atoi(e) : 0;
+}
+
 template <int VEC, int PER, typename TX = float>
 static int launch_remove(const TX* num, const float* cnt, int64_t n, int d, const double* pc,
                          int npc, float* out32, double* out64, hipStream_t stream) {
@@ -1726,6 +1810,20 @@ extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int 
                   (out32 == nullptr || (reinterpret_cast<uintptr_t>(out32) & 15) == 0);
   const int U = v4 ? d / 4 : d;
   const int per = static_cast<int>(ceil_div(U, kWave));
+  const int rr = remove_rows();
+  if (v4 && per == 2 && npc == 1 && out32 && rr > 0) {
+    const int64_t waves = ceil_div(n, rr);
+    const int grid = static_cast<int>(std::min<int64_t>(ceil_div(waves, 4), 256 * 8));
+    if (rr == 2) {
+      pc_remove1_kernel<2><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
+    } else if (rr == 8) {
+      pc_remove1_kernel<8><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
+    } else {
+      pc_remove1_kernel<4><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
+    }
+    MMB_LAUNCH_CHECK();
+    return MMB_OK;
+  }
   if (v4) {
     if (per <= 1) return launch_remove<4, 1>(num, cnt, n, d, pc, npc, out32, out64, stream);
     if (per <= 2) return launch_remove<4, 2>(num, cnt, n, d, pc, npc, out32, out64, stream);

@@ -831,6 +831,8 @@ struct FusedArgs {
   float* out;              // mmb2 [N][D]
   int64_t nb;              // batches = ceil(N / 48)
   int kq[3];               // padded piece widths (multiples of 32)
+  int psleep;              // projector: s_sleep 1 (64 clk) x psleep after each K chunk
+  int sprio;               // streamer waves at s_setprio 3
 };
 
 // bounded wait for *p >= target (workgroup scope); false once anything timed out
@@ -852,6 +854,16 @@ __device__ __forceinline__ void fused_signal(int* p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if ((threadIdx.x & (kWave - 1)) == 0)
     __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// the same without waiting for this wave's global loads / stores (the
+// pipelined streamer: its next frame groups stay in flight); the LDS writes it
+// orders are complete before the increment (lgkmcnt), and LDS operations of
+// one wave retire in order
+__device__ __forceinline__ void fused_signal_lds(int* p) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    __hip_atomic_fetch_add(p, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Text piece of utterance i (one wave, lane l owns float4 columns l, l + 64):
@@ -973,11 +985,12 @@ __device__ __forceinline__ void frame_piece(const float* base, int W, int L, int
   }
 }
 
-// DIAG (timing-only builds, MMB_FUSED_DIAG; wrong MMB2 rows): bit 0 the
+// DIAG (timing-only builds, MMB_FUSED_DIAG; wrong MMB2 rows): bit 4 every B
+// chunk read from the piece's first chunk, bit 5 no B loads; bit 0 the
 // projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
 // no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
 // the frames (constant sums: the projectors alone)
-template <int UNR, bool NT, int DIAG = 0>
+template <int UNR, bool NT, int DIAG = 0, bool PIPE = false>
 __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_fused_kernel(
     FusedArgs f) {
   const StreamArgs& a = f.s;
@@ -1002,86 +1015,290 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 
   if (wave < 4) {
     // ------------------------------------------------------------ streamer
+    if (f.sprio) __builtin_amdgcn_s_setprio(3);
     const int wdt[3] = {a.D, a.A, a.Vd};
     float4 cmx[2];
     cmx[0] = cmx[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t j = 0;; ++j) {
-      const int64_t B = blockIdx.x + j * G;
-      if (B >= f.nb) break;
-#pragma unroll 1
-      for (int m = 0; m < 3; ++m) {
-        const int p = 3 * static_cast<int>(j) + m;  // piece sequence number
-        const int W = wdt[m], U = W >> 2;
-#pragma unroll 1
-        for (int r = 0; r < kGR / 4; ++r) {
-          const int q = wave + 4 * r;
-          const int64_t i = B * kGR + q;
-          if (i >= N) break;
-          float4 num[2], sx[2], sxx[2];
-          float cnt = 0.f, sw = 0.f;
-          if constexpr ((DIAG & 8) != 0) {
-            const float4 o4 = make_float4(1.f, 1.f, 1.f, 1.f);
-            num[0] = num[1] = sx[0] = sx[1] = sxx[0] = sxx[1] = o4;
-            cnt = sw = 1.f;
-          } else if (m == 0) {
-            text_piece<UNR>(a, i, lane, num, sx, sxx, cnt, sw);
-          } else {
-            const float* base = m == 1 ? a.audio + i * a.L * a.A : a.visual + i * a.L * a.Vd;
-            frame_piece<UNR, NT>(base, W, a.L, lane, sx, sxx);
-          }
-          float mx = 0.f;
+    // Row q (utterance i) of batch j, modality m summed: its power-of-2 scale,
+    // the text row's x / aux / column bounds, then the scaled fp16 hi | lo
+    // sums into the ring slot (once the slot's previous piece-row was read by
+    // every projector) and one fill increment.  DRAIN: the increment waits for
+    // every earlier global access of this wave (the group-at-a-time streamer);
+    // the pipelined streamer waits only for its LDS writes, its next loads
+    // stay in flight (its x / aux stores are drained once per batch, before
+    // the audio piece's first increment -- the projectors read x only after
+    // the visual piece).
+    auto finish_row = [&](auto drain_c, int64_t j, int m, int q, int64_t i, const float4 (&num)[2],
+                          const float4 (&sx)[2], const float4 (&sxx)[2], float cnt, float sw) {
+      const int W = wdt[m], U = W >> 2;
+      const int p = 3 * static_cast<int>(j) + m;  // piece sequence number
+      float mx = 0.f;
 #pragma unroll
-          for (int c = 0; c < 2; ++c) mx = fmaxf(mx, fmaxf(amax4(sx[c]), amax4(sxx[c])));
-          const float rs = row_scale(wave_max(mx));
-          if (m == 0) {
+      for (int c = 0; c < 2; ++c) mx = fmaxf(mx, fmaxf(amax4(sx[c]), amax4(sxx[c])));
+      const float rs = row_scale(wave_max(mx));
+      if (m == 0) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int uu = lane + kWave * c;
+          if (uu < U) {
+            const float4 xr = div4(num[c], cnt);
+            st4(a.num_out + i * D + 4 * uu, xr);  // x = the a2 row
+            cmx[c] = make_float4(fmaxf(cmx[c].x, fabsf(xr.x)), fmaxf(cmx[c].y, fabsf(xr.y)),
+                                 fmaxf(cmx[c].z, fabsf(xr.z)), fmaxf(cmx[c].w, fabsf(xr.w)));
+          }
+        }
+        if (lane == 0) {
+          a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | text-piece scale
+          a.aux_out[N + i] = sw;
+          a.aux_out[2 * N + i] = rs;
+          s_cnt[(j & 1) * kGR + q] = cnt;
+          s_tw[(j & 1) * kGR + q] = sw;
+        }
+      }
+      // the slot's previous piece-row (pos - 60) must have been read by every projector
+      const int pos = p * kGR + q;
+      const int slot = pos % kGSlots;
+      // (DIAG 64, timing only: never wait -- the ring's back-pressure removed)
+      if ((DIAG & 64) == 0 && pos >= kGSlots)
+        fused_wait(consumed, ((pos - kGSlots) / kGR + 1) * 4, abort_flag, a.flag);
+      _Float16* srow = ring + slot * kGSlot;
+      const int qx = q & 15;  // row within its MFMA row tile: the XOR swizzle key
+      auto put = [&](int k, float4 v) {
+        const float x4[4] = {v.x * rs, v.y * rs, v.z * rs, v.w * rs};
+        h4 h, l;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          h[e] = static_cast<_Float16>(x4[e]);
+          l[e] = static_cast<_Float16>(x4[e] - static_cast<float>(h[e]));
+        }
+        const int o = (((k >> 3) ^ qx) << 3) + (k & 7);
+        *reinterpret_cast<h4*>(srow + o) = h;
+        *reinterpret_cast<h4*>(srow + kGPlane + o) = l;
+      };
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int uu = lane + kWave * c;
+        if (uu < U) {
+          put(4 * uu, sx[c]);
+          put(W + 4 * uu, sxx[c]);
+        }
+      }
+      for (int k = 2 * W + 4 * lane; k < f.kq[m]; k += 4 * kWave) put(k, make_float4(0.f, 0.f, 0.f, 0.f));
+      if (lane == 0) s_irs[slot] = 1.f / rs;  // a power of two: exact
+      if constexpr (decltype(drain_c)::value) {
+        fused_signal(&fill[p & 3]);
+      } else {
+        fused_signal_lds(&fill[p & 3]);
+      }
+    };
+
+    if constexpr (!PIPE) {
+      for (int64_t j = 0;; ++j) {
+        const int64_t B = blockIdx.x + j * G;
+        if (B >= f.nb) break;
+#pragma unroll 1
+        for (int m = 0; m < 3; ++m) {
+          const int W = wdt[m];
+#pragma unroll 1
+          for (int r = 0; r < kGR / 4; ++r) {
+            const int q = wave + 4 * r;
+            const int64_t i = B * kGR + q;
+            if (i >= N) break;
+            float4 num[2], sx[2], sxx[2];
+            float cnt = 0.f, sw = 0.f;
+            if constexpr ((DIAG & 8) != 0) {
+              const float4 o4 = make_float4(1.f, 1.f, 1.f, 1.f);
+              num[0] = num[1] = sx[0] = sx[1] = sxx[0] = sxx[1] = o4;
+              cnt = sw = 1.f;
+            } else if (m == 0) {
+              text_piece<UNR>(a, i, lane, num, sx, sxx, cnt, sw);
+            } else {
+              const float* base = m == 1 ? a.audio + i * a.L * a.A : a.visual + i * a.L * a.Vd;
+              frame_piece<UNR, NT>(base, W, a.L, lane, sx, sxx);
+            }
+            finish_row(std::true_type{}, j, m, q, i, num, sx, sxx, cnt, sw);
+          }
+        }
+      }
+    } else {
+      // Pipelined streamer: the (row, frame group) sequence of one (batch,
+      // modality) piece -- this wave's rows i0 + 4 r, ceil(L / UNR) groups of
+      // UNR frames each -- as ONE load pipeline two groups deep: group g + 1's
+      // 2 UNR loads are issued before group g is summed (alternating register
+      // sets b0 / b1; the compiler's counted vmcnt waits only for the older
+      // group), so loads stay in flight across group and row boundaries where
+      // the group-at-a-time streamer drained them.  Text rows: row r + 1's ids
+      // are loaded while row r's first group is summed, its weights gathered
+      // (wtab[id]) at the second -- the next row's first group is issued after
+      // that (>= 3 groups per row, launch_fused).  Per lane the frames are
+      // summed in the same order as text_piece / frame_piece: bit-identical.
+      // (A pipeline running on across piece and batch boundaries, one issue /
+      // consume pair for all three modalities, measured 29.4 vs 22.1 ms: the
+      // shared register sets made the compiler drain every group, vmcnt(0).)
+      const bool gather = a.ids != nullptr;
+      const int L = a.L;
+      // the wave index made visibly wave-uniform (SGPR): rows, loop bounds and
+      // buffer descriptors derive from it (a descriptor in VGPRs would be
+      // waterfall-looped around every load)
+      const int uw = __builtin_amdgcn_readfirstlane(wave);
+      auto tok_issue = [&](int64_t i, int& raw, float& wd) {
+        raw = -1;
+        wd = 0.f;
+        if (lane < L) {
+          const int64_t ft = i * L + lane;
+          if (gather) raw = a.ids[ft];
+          if (a.w_dense) wd = a.w_dense[ft];
+        }
+      };
+      auto tok_resolve = [&](int raw, float wd, int& rid, float& w) {  // stage_token's semantics
+        rid = -1;
+        w = 0.f;
+        if (lane < L) {
+          if (gather) {
+            int64_t id = raw;
+            w = a.w_dense ? wd : ((id >= 0 && id < a.V) ? a.wtab[id] : 0.f);
+            if (id < 0) id += a.V;
+            if (id < 0 || id >= a.V) {
+              if (a.flag) atomicOr(a.flag, MMB_FLAG_ID_RANGE);
+              w = 0.f;
+            } else {
+              rid = static_cast<int>(id);
+            }
+          } else {
+            w = wd;
+            rid = lane;
+          }
+        }
+      };
+      auto piece = [&](auto text_c, int64_t j, int m, int64_t i0, int nrows) {
+        constexpr bool TEXT = decltype(text_c)::value;
+        const int W = wdt[m], UW = W >> 2;
+        const int c0 = 4 * min(lane, UW - 1), c1 = 4 * min(lane + kWave, UW - 1);
+        const int ngr = (L + UNR - 1) / UNR, ng = nrows * ngr;
+        const float* src = TEXT ? (gather ? a.table : a.text_dense) : (m == 1 ? a.audio : a.visual);
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        int cur = 0;                        // the row being summed
+        int rid_c = -1, rid_n = -1, raw_n = -1;
+        float w_c = 0.f, w_n = 0.f, wd_n = 0.f;
+        float4 num[2], sx[2], sxx[2];
+        float cnt = 0.f, sw = 0.f;
+        if constexpr (TEXT) {
+          int raw;
+          float wd;
+          tok_issue(i0, raw, wd);
+          tok_resolve(raw, wd, rid_c, w_c);
+        }
+        // loads through buffer descriptors: one scalar offset per frame (the
+        // gathered row's or the frame's), per-lane column offsets vo0 / vo1 --
+        // no 64-bit address arithmetic in VGPRs
+        const int vo0 = 4 * c0, vo1 = 4 * c1;
+        auto issue = [&](int g, float4 (&v)[UNR][2]) {
+          const int rr = g / ngr, t0 = (g - rr * ngr) * UNR;
+          const int64_t i = i0 + 4 * rr;
+          int rid = 0;
+          if constexpr (TEXT) rid = rr == cur ? rid_c : rid_n;
+          const bool rowbase = !TEXT || !gather;  // frames [L][W] of row i
+          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<float*>(rowbase ? src + i * L * W : src), 0,
+              rowbase ? L * W * 4 : static_cast<int>(a.V * D * 4), 0x00020000);
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const int t = min(t0 + u, L - 1);
+            int so;
+            if constexpr (TEXT) {
+              const int r = __builtin_amdgcn_readlane(rid, t);
+              so = gather ? (r >= 0 ? r : 0) * D * 4 : t * W * 4;
+            } else {
+              so = t * W * 4;
+            }
+            constexpr int pol = (!TEXT && NT) ? 2 : 0;  // non-temporal frame streams
+            v[u][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo0, so, pol));
+            v[u][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo1, so, pol));
+          }
+        };
+        auto sum_frame = [&](int t, const float4 (&v)[2]) {
+          if constexpr (TEXT) {
+            const int r = __builtin_amdgcn_readlane(rid_c, t);
+            const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w_c), t));
+            const bool ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-              const int uu = lane + kWave * c;
-              if (uu < U) {
-                const float4 xr = div4(num[c], cnt);
-                st4(a.num_out + i * D + 4 * uu, xr);  // x = the a2 row
-                cmx[c] = make_float4(fmaxf(cmx[c].x, fabsf(xr.x)), fmaxf(cmx[c].y, fabsf(xr.y)),
-                                     fmaxf(cmx[c].z, fabsf(xr.z)), fmaxf(cmx[c].w, fabsf(xr.w)));
-              }
+              const float4 x = ok ? v[c] : z4;
+              fma4(num[c], wt, x);
+              add4(sx[c], x);
+              sq4(sxx[c], x);
             }
-            if (lane == 0) {
-              a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | text-piece scale
-              a.aux_out[N + i] = sw;
-              a.aux_out[2 * N + i] = rs;
-              s_cnt[(j & 1) * kGR + q] = cnt;
-              s_tw[(j & 1) * kGR + q] = sw;
+          } else {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              add4(sx[c], v[c]);
+              sq4(sxx[c], v[c]);
             }
           }
-          // the slot's previous piece-row (pos - 60) must have been read by every projector
-          const int pos = p * kGR + q;
-          const int slot = pos % kGSlots;
-          if (pos >= kGSlots) fused_wait(consumed, ((pos - kGSlots) / kGR + 1) * 4, abort_flag, a.flag);
-          _Float16* srow = ring + slot * kGSlot;
-          const int qx = q & 15;  // row within its MFMA row tile: the XOR swizzle key
-          auto put = [&](int k, float4 v) {
-            const float x4[4] = {v.x * rs, v.y * rs, v.z * rs, v.w * rs};
-            h4 h, l;
+        };
+        auto consume = [&](int g, const float4 (&v)[UNR][2]) {
+          const int rr = g / ngr, gg = g - rr * ngr, t0 = gg * UNR;
+          if (gg == 0) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              h[e] = static_cast<_Float16>(x4[e]);
-              l[e] = static_cast<_Float16>(x4[e] - static_cast<float>(h[e]));
-            }
-            const int o = (((k >> 3) ^ qx) << 3) + (k & 7);
-            *reinterpret_cast<h4*>(srow + o) = h;
-            *reinterpret_cast<h4*>(srow + kGPlane + o) = l;
-          };
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int uu = lane + kWave * c;
-            if (uu < U) {
-              put(4 * uu, sx[c]);
-              put(W + 4 * uu, sxx[c]);
+            for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
+            if constexpr (TEXT) {
+              cnt = wave_sum((w_c != 0.f) ? 1.f : 0.f);
+              sw = wave_sum(w_c);
+              // every weight 0: x is 0/0 = NaN (numpy's answer); TruncatedSVD
+              // would reject the split -- report it through the flag word
+              if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+              if (rr + 1 < nrows) tok_issue(i0 + 4 * (rr + 1), raw_n, wd_n);
             }
           }
-          for (int k = 2 * W + 4 * lane; k < f.kq[m]; k += 4 * kWave) put(k, make_float4(0.f, 0.f, 0.f, 0.f));
-          if (lane == 0) s_irs[slot] = 1.f / rs;  // a power of two: exact
-          fused_signal(&fill[p & 3]);
+          if constexpr (TEXT) {
+            if (gg == 1 && rr + 1 < nrows) tok_resolve(raw_n, wd_n, rid_n, w_n);
+          }
+          if (t0 + UNR <= L) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) sum_frame(t0 + u, v[u]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+              if (t0 + u < L) sum_frame(t0 + u, v[u]);
+          }
+          if (gg == ngr - 1) {
+            const int q = uw + 4 * rr;
+            finish_row(std::false_type{}, j, m, q, i0 + 4 * rr, num, sx, sxx, cnt, sw);
+            cur = rr + 1;
+            if constexpr (TEXT) {
+              rid_c = rid_n;
+              w_c = w_n;
+            }
+          }
+        };
+        float4 b0[UNR][2], b1[UNR][2];
+        issue(0, b0);
+        int g = 0;
+#pragma unroll 1
+        for (; g + 2 < ng; g += 2) {
+          issue(g + 1, b1);
+          consume(g, b0);
+          issue(g + 2, b0);
+          consume(g + 1, b1);
         }
+        if (g + 1 < ng) {
+          issue(g + 1, b1);
+          consume(g, b0);
+          consume(g + 1, b1);
+        } else {
+          consume(g, b0);
+        }
+      };
+      for (int64_t j = 0;; ++j) {
+        const int64_t B = blockIdx.x + j * G;
+        if (B >= f.nb) break;
+        const int64_t i0 = B * kGR + uw;
+        const int nrows = i0 < N ? static_cast<int>(min<int64_t>(kGR / 4, (N - i0 + 3) / 4)) : 0;
+        if (nrows == 0) continue;
+        piece(std::true_type{}, j, 0, i0, nrows);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x / aux stores before the audio increments
+        piece(std::false_type{}, j, 1, i0, nrows);
+        piece(std::false_type{}, j, 2, i0, nrows);
       }
     }
     if (a.cmax_part) {  // this wave's column bounds (mmb_gram_i8)
@@ -1160,11 +1377,16 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         constexpr int NL = decltype(nt_c)::value;
         half8 bh[2][NL], bl[2][NL];
         auto ld_b = [&](int c, half8 (&h)[NL], half8 (&l)[NL]) {
-          const int so = (c0g + (c < npc ? c : npc - 1)) * CH * 2;
+          // DIAG 16: every chunk reads the piece's chunk 0 (a 20 KB L2 footprint)
+          const int so = (DIAG & 16) ? c0g * CH * 2 : (c0g + (c < npc ? c : npc - 1)) * CH * 2;
 #pragma unroll
           for (int t = 0; t < NL; ++t) {
-            h[t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[t] * 2, so, 0));
-            l[t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (boff[t] + PL) * 2, so, 0));
+            if constexpr ((DIAG & 32) != 0) {  // no B loads at all
+              h[t] = l[t] = half8{1, 1, 1, 1, 1, 1, 1, 1};
+            } else {
+              h[t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[t] * 2, so, 0));
+              l[t] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (boff[t] + PL) * 2, so, 0));
+            }
           }
         };
         auto chunk = [&](int c, const half8 (&h)[NL], const half8 (&l)[NL]) {
@@ -1189,12 +1411,15 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         };
         ld_b(0, bh[0], bl[0]);
         ld_b(1, bh[1], bl[1]);
+        const int ps = f.psleep;
 #pragma unroll 1
         for (int c = 0; c < npc; c += 2) {
           chunk(c, bh[0], bl[0]);
+          for (int k = 0; k < ps; ++k) __builtin_amdgcn_s_sleep(1);
           ld_b(c + 2, bh[0], bl[0]);
           if (c + 1 < npc) {
             chunk(c + 1, bh[1], bl[1]);
+            for (int k = 0; k < ps; ++k) __builtin_amdgcn_s_sleep(1);
             ld_b(c + 3, bh[1], bl[1]);
           }
         }
@@ -1289,15 +1514,15 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   }
 }
 
-template <int DIAG, int UNR = 8>
+template <int DIAG, int UNR = 8, bool PIPE = false>
 static void launch_fused_v(const FusedArgs& f, int grid, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_fused_kernel<UNR, true, DIAG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_fused_kernel<UNR, true, DIAG, PIPE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kGLdsBytes));
     attr = true;
   }
-  utt_fused_kernel<UNR, true, DIAG><<<grid, kFThreads, kGLdsBytes, stream>>>(f);
+  utt_fused_kernel<UNR, true, DIAG, PIPE><<<grid, kFThreads, kGLdsBytes, stream>>>(f);
 }
 static int fused_unr() {  // streamer frames per load group (in-process sweeps)
   const char* e = getenv("MMB_FUSED_UNR");
@@ -1309,11 +1534,37 @@ static int fused_diag() {  // re-read per launch (in-process timing sweeps)
   return e ? atoi(e) : 0;
 }
 
+// streamer: 1 = pipelined (two groups in flight; default: kernel 23.35 ->
+// 22.49 ms, step 25.14 -> 24.41 ms in a same-process A/B, r02k), 0 = one group
+// at a time (the bit-identical reference of the tests)
+static int fused_pipe() {
+  const char* e = getenv("MMB_FUSED_PIPE");
+  return e ? atoi(e) : 1;
+}
+
 static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
   if (parts) *parts = grid * 4;
   const int dg = fused_diag(), un = fused_unr();
-  if (dg == 0 && un == 12) {
+  // the pipelined streamer stages a text row's tokens two groups before its
+  // first group is issued: >= 3 groups per row
+  // and addresses the word table through one buffer descriptor (< 2^31 bytes)
+  const bool pipe = fused_pipe() != 0 && (f.s.L + un - 1) / un >= 3 &&
+                    (f.s.ids == nullptr || f.s.V * f.s.D * 4 < (int64_t{1} << 31));
+  if (pipe && un == 8) {
+    switch (dg) {
+      case 1: launch_fused_v<1, 8, true>(f, grid, stream); break;
+      case 2: launch_fused_v<2, 8, true>(f, grid, stream); break;
+      case 4: launch_fused_v<4, 8, true>(f, grid, stream); break;
+      case 16: launch_fused_v<16, 8, true>(f, grid, stream); break;
+      case 32: launch_fused_v<32, 8, true>(f, grid, stream); break;
+      case 64: launch_fused_v<64, 8, true>(f, grid, stream); break;
+      default: launch_fused_v<0, 8, true>(f, grid, stream); break;
+    }
+  } else if (pipe && dg == 0 && un == 6) {
+    launch_fused_v<0, 6, true>(f, grid, stream);
+
+  } else if (dg == 0 && un == 12) {
     launch_fused_v<0, 12>(f, grid, stream);
   } else if (dg == 0 && un == 16) {
     launch_fused_v<0, 16>(f, grid, stream);
@@ -1616,6 +1867,12 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   f.c0 = c0;
   f.out = mmb2_out;
   f.nb = ceil_div(n, kGR);
+  {  // measurement knobs (in-process sweeps): projector throttle, streamer priority
+    const char* e = getenv("MMB_FUSED_PSLEEP");
+    f.psleep = e ? atoi(e) : 0;
+    e = getenv("MMB_FUSED_SPRIO");
+    f.sprio = e ? atoi(e) : 0;
+  }
   int parts = 0;
   const int rc = launch_fused(f, stream, &parts);
   if (rc != MMB_OK || !colmax) return rc;

@@ -636,3 +636,65 @@ def test_stream_project_repeatable_and_unit_rows(gpu):
     assert torch.equal(s1, s2) and torch.equal(m1, m2)
     norms = torch.linalg.norm(m1.double(), dim=1)
     assert (norms - 1).abs().max().item() < 1e-5
+
+
+def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False):
+    """One mmb_mm2_stream_project launch with the streamer selected by
+    MMB_FUSED_PIPE (read per launch by the library); every output cloned."""
+    import os
+
+    dev = inp["audio"].device
+    d = 300
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    colmax = torch.empty(d, dtype=torch.int32, device=dev)
+    ws = torch.empty((8192, d), dtype=torch.float32, device=dev)
+    kw = dict(ids32=inp["ids"], table=inp["table"], wtab32=inp["wtab"])
+    if dense:
+        ids = inp["ids"].long()
+        kw = dict(text_dense=inp["table"][ids.clamp(min=0)].contiguous(),
+                  w_dense=inp["wtab"][ids.clamp(min=0)] * (ids >= 0))
+    old = os.environ.get("MMB_FUSED_PIPE")
+    os.environ["MMB_FUSED_PIPE"] = "1" if pipe else "0"
+    try:
+        x, aux, m = P.mm2_stream_project(n, t, d, a, vd, inp["audio"], inp["visual"], proj,
+                                         flag=flag, colmax=colmax, colmax_ws=ws, **kw)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["MMB_FUSED_PIPE"]
+        else:
+            os.environ["MMB_FUSED_PIPE"] = old
+    return [v.clone() for v in (x, aux, m, colmax, flag)]
+
+
+@pytest.mark.parametrize("N,T,A,Vd,dense,bad", [(2048, 40, 300, 300, False, False),
+                                                (15, 40, 300, 300, False, False),
+                                                (700, 64, 300, 300, False, True),
+                                                (999, 33, 260, 292, False, False),
+                                                (97, 40, 300, 20, False, False),
+                                                (300, 17, 300, 256, False, False),
+                                                (5003, 24, 300, 300, False, True),
+                                                (50, 16, 300, 300, False, False),
+                                                (500, 40, 300, 300, True, False),
+                                                (49, 40, 100, 300, False, False)])
+def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
+    """The pipelined streamer of utt_fused_kernel (two frame groups in flight
+    across group, row and text-token boundaries; buffer-descriptor loads)
+    against the group-at-a-time streamer: x, aux, MMB2 rows, column bounds
+    and the flag word bit-identical -- partial batches, partial last groups
+    (T = 33, 17), the 3-group minimum (T = 24; T = 16 falls back), narrow
+    frames, dense text, negative and out-of-range ids."""
+    inp = synth.device_workload(N, T, 20_000, A=A, Vd=Vd, seed=71, device=gpu)
+    if bad:  # negative ids wrap; ids >= V are flagged and contribute zero rows
+        inp["ids"][3, 5] = -7
+        inp["ids"][N // 2, T - 1] = 20_000 + 11
+        inp["ids"][N - 1, 0] = -20_001
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
+    proj = P.MMB2Projection(gen.networks(), 300, A, Vd, T, gpu)
+    ref = _fused_outputs(inp, proj, N, T, A, Vd, pipe=False, dense=dense)
+    got = _fused_outputs(inp, proj, N, T, A, Vd, pipe=True, dense=dense)
+    names = ["x", "aux", "mmb2", "colmax", "flag"]
+    for nm, r, g in zip(names, ref, got):
+        assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), nm
+    assert (int(ref[4].item()) != 0) == bad

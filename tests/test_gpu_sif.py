@@ -347,3 +347,36 @@ def test_gram_i8_pc_on_golden_splits(gpu, golden):
         G = P.gram_i8(x, P.colmax(x))
         pc = P.pc_solve(G, P.omega(300, npc + 10, gpu), npc, False).cpu().numpy()
         assert np.abs(pc - z["pc"]).max() < 1e-9, case
+
+
+@pytest.mark.parametrize("n,d,with_cnt", [(1, 300, False), (5, 300, True), (1003, 300, False),
+                                          (4099, 300, True), (777, 260, False), (130, 292, True)])
+def test_remove_multirow_kernel_bit_identical(gpu, n, d, with_cnt):
+    """pc_remove1_kernel (one PC, R rows per wave in flight, the PC in
+    registers) against pc_remove_kernel (MMB_PC_REMOVE_R=0): bit-identical
+    rows -- row counts not multiples of R, narrow rows, a count divisor --
+    and within 1e-6 of the f64 removal of the oracle."""
+    import os
+
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.randn(n, d, generator=g, device=gpu) * 3 + 0.5
+    cnt = torch.randint(1, 40, (n,), generator=g, device=gpu).float() if with_cnt else None
+    pc = torch.randn(1, d, generator=g, device=gpu, dtype=torch.float64)
+    pc /= torch.linalg.norm(pc)
+    outs = []
+    old = os.environ.get("MMB_PC_REMOVE_R")
+    try:
+        for r in ("0", "4", "2", "8"):
+            os.environ["MMB_PC_REMOVE_R"] = r
+            outs.append(P.remove_pc(x, cnt, pc).clone())
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("MMB_PC_REMOVE_R", None)
+        else:
+            os.environ["MMB_PC_REMOVE_R"] = old
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    xs = x.double() / (cnt.double()[:, None] if with_cnt else 1.0)
+    ref = xs - (xs @ pc.T) @ pc
+    assert (outs[0].double() - ref).abs().max().item() <= 1e-6 * xs.abs().max().item()

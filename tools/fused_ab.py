@@ -27,19 +27,25 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--diags", default="",
-                    help="comma list of MMB_FUSED_DIAG[:MMB_FUSED_UNR] values: kernel-only "
-                         "timing of the fused kernel's ablations / streamer load-group sizes "
-                         "beside the plain stream kernel")
+                    help="comma list of MMB_FUSED_DIAG[:MMB_FUSED_UNR[:MMB_FUSED_PIPE]] values: "
+                         "kernel-only timing of the fused kernel's ablations / streamer "
+                         "load-group sizes / pipelined streamer beside the plain stream kernel")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     inp = synth.device_workload(args.n, 40, 400_000, seed=1, device=dev)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
     steps = {"two_kernel": P.FusedStep(inp, gen.networks(), stream_project=False),
-             "fused": P.FusedStep(inp, gen.networks(), stream_project=True)}
+             "fused": P.FusedStep(inp, gen.networks(), stream_project=True),
+             "fused_pipe": P.FusedStep(inp, gen.networks(), stream_project=True)}
+    pipe_of = {"two_kernel": "0", "fused": "0", "fused_pipe": "1"}
     for k, st in steps.items():
+        os.environ["MMB_FUSED_PIPE"] = pipe_of[k]
         st.run()
     torch.cuda.synchronize()
+    c = steps["fused_pipe"]
+    print("pipelined streamer bit-identical:", torch.equal(steps["fused"].x, c.x),
+          torch.equal(steps["fused"].mmb2, c.mmb2), torch.equal(steps["fused"].sif, c.sif), flush=True)
     for st in steps.values():
         st.check()
     a, b = steps["two_kernel"], steps["fused"]
@@ -50,6 +56,7 @@ def main():
     for r in range(args.rounds):
         for k, st in steps.items():
             tr = {}
+            os.environ["MMB_FUSED_PIPE"] = pipe_of[k]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.steps):
@@ -81,9 +88,11 @@ def main():
     kt = {name: [] for name, _, _ in variants}
     for r in range(args.rounds):
         for name, dg, fn in variants:
-            dg, _, un = dg.partition(":")
+            dg, _, rest = dg.partition(":")
+            un, _, pp = rest.partition(":")
             os.environ["MMB_FUSED_DIAG"] = dg
             os.environ["MMB_FUSED_UNR"] = un or "8"
+            os.environ["MMB_FUSED_PIPE"] = pp or "0"
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -94,6 +103,7 @@ def main():
             kt[name].append(e0.elapsed_time(e1) / args.steps)
     os.environ["MMB_FUSED_DIAG"] = "0"
     os.environ["MMB_FUSED_UNR"] = "8"
+    os.environ.pop("MMB_FUSED_PIPE", None)
     for name in kt:
         print(f"kernel {name}: median {statistics.median(kt[name]):.3f} ms  min {min(kt[name]):.3f}")
 
