@@ -1555,11 +1555,12 @@ __global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict
   }
 }
 
-// pc_remove1_kernel rows per wave (2, 4, 8); 0 = pc_remove_kernel (default
-// until measured)
+// pc_remove1_kernel rows per wave (2, 4, 8); 0 = pc_remove_kernel.  Measured
+// (tools/remove_ab.py, 1M x 300, r02q): R = 0 / 2 / 4 / 8 = 0.529 / 0.455 /
+// 0.435 / 0.444 ms, all bit-identical
 static int remove_rows() {
   const char* e = getenv("MMB_PC_REMOVE_R");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 4;
 }
 
 template <int VEC, int PER, typename TX = float>

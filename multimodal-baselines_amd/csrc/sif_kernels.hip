@@ -831,6 +831,7 @@ struct FusedArgs {
   float* out;              // mmb2 [N][D]
   int64_t nb;              // batches = ceil(N / 48)
   int kq[3];               // padded piece widths (multiples of 32)
+  int balanced;            // rows past the last full round split evenly over the workgroups
   int psleep;              // projector: s_sleep 1 (64 clk) x psleep after each K chunk
   int sprio;               // streamer waves at s_setprio 3
 };
@@ -1012,6 +1013,27 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   const int64_t N = a.N;
   const int G = gridDim.x;
   const int D = a.D;
+  // This workgroup's batches of 48 rows: batch blockIdx.x + j G of the row
+  // space (round robin: the CUs stream neighbouring rows -- contiguous
+  // per-CU ranges measured 23.07 vs 22.32 ms).  With f.balanced the rows
+  // past the last full round (N mod 48 G) are split evenly over the
+  // workgroups instead of being whole batches of a few of them (a CU with
+  // one batch more than another runs ~0.28 ms longer).
+  const int64_t full = N / (static_cast<int64_t>(kGR) * G);  // full rounds
+  auto batch = [&](int64_t j, int64_t& row0, int64_t& rend) -> bool {
+    if (f.balanced && j >= full) {
+      if (j > full) return false;
+      const int64_t t0 = full * kGR * G, tail = N - t0, b = blockIdx.x;
+      const int64_t per = tail / G, rem = tail % G;
+      row0 = t0 + b * per + (b < rem ? b : rem);
+      rend = row0 + per + (b < rem ? 1 : 0);
+      return row0 < rend;
+    }
+    const int64_t Bj = blockIdx.x + j * G;
+    row0 = Bj * kGR;
+    rend = min<int64_t>(N, row0 + kGR);
+    return Bj < f.nb;
+  };
 
   if (wave < 4) {
     // ------------------------------------------------------------ streamer
@@ -1094,16 +1116,16 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 
     if constexpr (!PIPE) {
       for (int64_t j = 0;; ++j) {
-        const int64_t B = blockIdx.x + j * G;
-        if (B >= f.nb) break;
+        int64_t row0, rend;
+        if (!batch(j, row0, rend)) break;
 #pragma unroll 1
         for (int m = 0; m < 3; ++m) {
           const int W = wdt[m];
 #pragma unroll 1
           for (int r = 0; r < kGR / 4; ++r) {
             const int q = wave + 4 * r;
-            const int64_t i = B * kGR + q;
-            if (i >= N) break;
+            const int64_t i = row0 + q;
+            if (i >= rend) break;
             float4 num[2], sx[2], sxx[2];
             float cnt = 0.f, sw = 0.f;
             if constexpr ((DIAG & 8) != 0) {
@@ -1290,10 +1312,10 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
       };
       for (int64_t j = 0;; ++j) {
-        const int64_t B = blockIdx.x + j * G;
-        if (B >= f.nb) break;
-        const int64_t i0 = B * kGR + uw;
-        const int nrows = i0 < N ? static_cast<int>(min<int64_t>(kGR / 4, (N - i0 + 3) / 4)) : 0;
+        int64_t row0, rend;
+        if (!batch(j, row0, rend)) break;
+        const int64_t i0 = row0 + uw;
+        const int nrows = i0 < rend ? static_cast<int>(min<int64_t>(kGR / 4, (rend - i0 + 3) / 4)) : 0;
         if (nrows == 0) continue;
         piece(std::true_type{}, j, 0, i0, nrows);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x / aux stores before the audio increments
@@ -1336,9 +1358,9 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   const int ntiles = max(kFTiles - 1, min(kFTiles, tD + 1 - kFTiles * pw));
   int ep = 0;  // projector exchange points passed
   for (int64_t j = 0;; ++j) {
-    const int64_t B = blockIdx.x + j * G;
-    if (B >= f.nb) break;
-    const int nvalid = static_cast<int>(N - B * kGR < kGR ? N - B * kGR : kGR);
+    int64_t row0, rend;
+    if (!batch(j, row0, rend)) break;
+    const int nvalid = static_cast<int>(rend - row0);
     f32x4 acc[kGRT][kFTiles];
 #pragma unroll
     for (int rt = 0; rt < kGRT; ++rt)
@@ -1440,7 +1462,6 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
     }
 
     // epilogue: lane value (rt, t, jj) = row 16 rt + 4 g + jj, column 16 (5 pw + t) + q
-    const int64_t row0 = B * kGR;
     const float* cntb = s_cnt + (j & 1) * kGR;
     const float* twb = s_tw + (j & 1) * kGR;
     float* tot = s_tot + (j & 1) * kGR;
@@ -1872,6 +1893,8 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
     f.psleep = e ? atoi(e) : 0;
     e = getenv("MMB_FUSED_SPRIO");
     f.sprio = e ? atoi(e) : 0;
+    e = getenv("MMB_FUSED_BALANCED");  // default on: 22.35 -> 22.26 ms (r02s)
+    f.balanced = e ? atoi(e) : 1;
   }
   int parts = 0;
   const int rc = launch_fused(f, stream, &parts);

@@ -638,9 +638,10 @@ def test_stream_project_repeatable_and_unit_rows(gpu):
     assert (norms - 1).abs().max().item() < 1e-5
 
 
-def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False):
+def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False, balanced=False):
     """One mmb_mm2_stream_project launch with the streamer selected by
-    MMB_FUSED_PIPE (read per launch by the library); every output cloned."""
+    MMB_FUSED_PIPE and the row assignment by MMB_FUSED_BALANCED (read per
+    launch by the library); every output cloned."""
     import os
 
     dev = inp["audio"].device
@@ -653,17 +654,19 @@ def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False):
         ids = inp["ids"].long()
         kw = dict(text_dense=inp["table"][ids.clamp(min=0)].contiguous(),
                   w_dense=inp["wtab"][ids.clamp(min=0)] * (ids >= 0))
-    old = os.environ.get("MMB_FUSED_PIPE")
-    os.environ["MMB_FUSED_PIPE"] = "1" if pipe else "0"
+    knobs = {"MMB_FUSED_PIPE": "1" if pipe else "0", "MMB_FUSED_BALANCED": "1" if balanced else "0"}
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
     try:
         x, aux, m = P.mm2_stream_project(n, t, d, a, vd, inp["audio"], inp["visual"], proj,
                                          flag=flag, colmax=colmax, colmax_ws=ws, **kw)
         torch.cuda.synchronize()
     finally:
-        if old is None:
-            del os.environ["MMB_FUSED_PIPE"]
-        else:
-            os.environ["MMB_FUSED_PIPE"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return [v.clone() for v in (x, aux, m, colmax, flag)]
 
 
@@ -683,7 +686,8 @@ def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
     against the group-at-a-time streamer: x, aux, MMB2 rows, column bounds
     and the flag word bit-identical -- partial batches, partial last groups
     (T = 33, 17), the 3-group minimum (T = 24; T = 16 falls back), narrow
-    frames, dense text, negative and out-of-range ids."""
+    frames, dense text, negative and out-of-range ids -- and with balanced
+    per-workgroup row ranges (MMB_FUSED_BALANCED) instead of round robin."""
     inp = synth.device_workload(N, T, 20_000, A=A, Vd=Vd, seed=71, device=gpu)
     if bad:  # negative ids wrap; ids >= V are flagged and contribute zero rows
         inp["ids"][3, 5] = -7
@@ -693,8 +697,9 @@ def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
     gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
     proj = P.MMB2Projection(gen.networks(), 300, A, Vd, T, gpu)
     ref = _fused_outputs(inp, proj, N, T, A, Vd, pipe=False, dense=dense)
-    got = _fused_outputs(inp, proj, N, T, A, Vd, pipe=True, dense=dense)
     names = ["x", "aux", "mmb2", "colmax", "flag"]
-    for nm, r, g in zip(names, ref, got):
-        assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), nm
+    for pipe, bal in [(True, False), (True, True), (False, True)]:
+        got = _fused_outputs(inp, proj, N, T, A, Vd, pipe=pipe, dense=dense, balanced=bal)
+        for nm, r, g in zip(names, ref, got):
+            assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), (nm, pipe, bal)
     assert (int(ref[4].item()) != 0) == bad

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""In-process A/B of the PC removal (mmb_pc_remove, one PC, 1M x 300 f32
+rows): pc_remove_kernel (MMB_PC_REMOVE_R=0) against pc_remove1_kernel with
+R = 2 / 4 / 8 rows per wave, interleaved rounds, median per variant, outputs
+checked bit-identical.
+
+    python tools/remove_ab.py [--n 1000000] [--rounds 5]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-baselines_amd"))
+
+import torch  # noqa: E402
+
+import pipeline as P  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(args.n, 300, generator=g, device=dev)
+    pc = torch.randn(1, 300, generator=g, device=dev, dtype=torch.float64)
+    pc /= torch.linalg.norm(pc)
+    out = torch.empty_like(x)
+    rs = ["0", "2", "4", "8"]
+    ref = None
+    times = {r: [] for r in rs}
+    for k in range(args.rounds):
+        for r in rs:
+            os.environ["MMB_PC_REMOVE_R"] = r
+            P.remove_pc(x, None, pc, out=out)
+            torch.cuda.synchronize()
+            if k == 0:
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    print(f"R={r}: bit-identical to R=0: {torch.equal(out, ref)}", flush=True)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(args.reps):
+                P.remove_pc(x, None, pc, out=out)
+            b.record()
+            torch.cuda.synchronize()
+            times[r].append(a.elapsed_time(b) / args.reps)
+    for r in rs:
+        ms = statistics.median(times[r])
+        print(f"R={r}: {ms:.4f} ms  ({2400 * args.n / ms / 1e6:.0f} GB/s on 2400 B/row)")
+
+
+if __name__ == "__main__":
+    main()
