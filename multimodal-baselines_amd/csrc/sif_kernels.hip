@@ -808,18 +808,19 @@ static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nul
 // hand-over ends the kernel (wrong rows, flagged) instead of hanging the GPU.
 constexpr int kGR = 48;                 // rows per batch
 constexpr int kGRT = kGR / 16;          // MFMA row tiles per batch
-constexpr int kGSlots = 60;             // ring slots (piece-rows)
+constexpr int kGSlots = 62;             // ring slots (piece-rows), at most (fused_lds_bytes)
 constexpr int kGUnits = 80;             // 16-byte units per plane (piece <= 640 sums; XOR-16 headroom)
 constexpr int kGPlane = kGUnits * 8;    // halves per plane
 constexpr int kGSlot = 2 * kGPlane;     // halves per slot (hi | lo)
 constexpr int kFTiles = 5;              // 16-column tiles per projector (ldw = 320)
 constexpr int kFLdw = 320;
 constexpr int kFThreads = 512;
-constexpr size_t kGRingBytes = static_cast<size_t>(kGSlots) * kGSlot * sizeof(_Float16);
-// ring | irs [60] | counters [8] | cnt, tw [2][48] each | tot [2][48] | ssq [2][4][48]
-constexpr size_t kGLdsBytes =
-    kGRingBytes + kGSlots * 4 + 8 * 4 + 2 * 2 * kGR * 4 + 2 * kGR * 4 + 2 * 4 * kGR * 4;
-static_assert(kGLdsBytes <= 160 * 1024, "fused ring exceeds LDS");
+// ring [SL slots] | irs [SL] | counters [8] | cnt, tw [2][48] each | tot [2][48] | ssq [2][4][48]
+__host__ __device__ constexpr size_t fused_lds_bytes(int sl) {
+  return static_cast<size_t>(sl) * kGSlot * sizeof(_Float16) + sl * 4 + 8 * 4 + 2 * 2 * kGR * 4 +
+         2 * kGR * 4 + 2 * 4 * kGR * 4;
+}
+static_assert(fused_lds_bytes(kGSlots) <= 160 * 1024, "fused ring exceeds LDS");
 static_assert((kGSlot * 2) % 256 == 0 && (kGPlane * 2) % 256 == 0,
               "slot and plane strides keep the XOR swizzle conflict-free");
 
@@ -991,14 +992,14 @@ __device__ __forceinline__ void frame_piece(const float* base, int W, int L, int
 // projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
 // no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
 // the frames (constant sums: the projectors alone)
-template <int UNR, bool NT, int DIAG = 0, bool PIPE = false>
+template <int UNR, bool NT, int DIAG = 0, bool PIPE = false, int SL = kGSlots>
 __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_fused_kernel(
     FusedArgs f) {
   const StreamArgs& a = f.s;
   extern __shared__ __attribute__((aligned(16))) _Float16 flds[];
   _Float16* ring = flds;
-  float* s_irs = reinterpret_cast<float*>(flds + kGSlots * kGSlot);
-  int* ctr = reinterpret_cast<int*>(s_irs + kGSlots);   // fill[4], consumed, pbar, abort, -
+  float* s_irs = reinterpret_cast<float*>(flds + SL * kGSlot);
+  int* ctr = reinterpret_cast<int*>(s_irs + SL);   // fill[4], consumed, pbar, abort, -
   float* s_cnt = reinterpret_cast<float*>(ctr + 8);     // [2][48]
   float* s_tw = s_cnt + 2 * kGR;                        // [2][48]
   float* s_tot = s_tw + 2 * kGR;                        // [2][48]
@@ -1079,10 +1080,10 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
       // the slot's previous piece-row (pos - 60) must have been read by every projector
       const int pos = p * kGR + q;
-      const int slot = pos % kGSlots;
+      const int slot = pos % SL;
       // (DIAG 64, timing only: never wait -- the ring's back-pressure removed)
-      if ((DIAG & 64) == 0 && pos >= kGSlots)
-        fused_wait(consumed, ((pos - kGSlots) / kGR + 1) * 4, abort_flag, a.flag);
+      if ((DIAG & 64) == 0 && pos >= SL)
+        fused_wait(consumed, ((pos - SL) / kGR + 1) * 4, abort_flag, a.flag);
       _Float16* srow = ring + slot * kGSlot;
       const int qx = q & 15;  // row within its MFMA row tile: the XOR swizzle key
       auto put = [&](int k, float4 v) {
@@ -1384,7 +1385,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
       for (int rt = 0; rt < kGRT; ++rt)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const float v = s_irs[(p * kGR + 16 * rt + 4 * g + jj) % kGSlots];
+          const float v = s_irs[(p * kGR + 16 * rt + 4 * g + jj) % SL];
           if (m > 0) {
             const float ratio = irs[rt][jj] / v;
 #pragma unroll
@@ -1394,7 +1395,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
       const _Float16* arow[kGRT];
 #pragma unroll
-      for (int rt = 0; rt < kGRT; ++rt) arow[rt] = ring + ((p * kGR + 16 * rt + q) % kGSlots) * kGSlot;
+      for (int rt = 0; rt < kGRT; ++rt) arow[rt] = ring + ((p * kGR + 16 * rt + q) % SL) * kGSlot;
       const int npc = f.kq[m] / 32, c0g = cb[m];
       // the K loop for NT live column tiles (tiles past column D hold zero
       // padding: projector 3 at D = 300 skips their loads and MFMAs)
@@ -1538,15 +1539,16 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   }
 }
 
-template <int DIAG, int UNR = 8, bool PIPE = false>
+template <int DIAG, int UNR = 8, bool PIPE = false, int SL = kGSlots>
 static void launch_fused_v(const FusedArgs& f, int grid, hipStream_t stream) {
+  constexpr size_t lds = fused_lds_bytes(SL);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_fused_kernel<UNR, true, DIAG, PIPE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kGLdsBytes));
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_fused_kernel<UNR, true, DIAG, PIPE, SL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr = true;
   }
-  utt_fused_kernel<UNR, true, DIAG, PIPE><<<grid, kFThreads, kGLdsBytes, stream>>>(f);
+  utt_fused_kernel<UNR, true, DIAG, PIPE, SL><<<grid, kFThreads, lds, stream>>>(f);
 }
 static int fused_unr() {  // streamer frames per load group (in-process sweeps)
   const char* e = getenv("MMB_FUSED_UNR");
@@ -1566,6 +1568,11 @@ static int fused_pipe() {
   return e ? atoi(e) : 1;
 }
 
+static int fused_slots() {  // ring slots: 62 (default) or 60 (in-process A/B)
+  const char* e = getenv("MMB_FUSED_SLOTS");
+  return e ? atoi(e) : kGSlots;
+}
+
 static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
   if (parts) *parts = grid * 4;
@@ -1583,7 +1590,13 @@ static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
       case 16: launch_fused_v<16, 8, true>(f, grid, stream); break;
       case 32: launch_fused_v<32, 8, true>(f, grid, stream); break;
       case 64: launch_fused_v<64, 8, true>(f, grid, stream); break;
-      default: launch_fused_v<0, 8, true>(f, grid, stream); break;
+      default:
+        if (fused_slots() == 60) {
+          launch_fused_v<0, 8, true, 60>(f, grid, stream);
+        } else {
+          launch_fused_v<0, 8, true>(f, grid, stream);
+        }
+        break;
     }
   } else if (pipe && dg == 0 && un == 6) {
     launch_fused_v<0, 6, true>(f, grid, stream);

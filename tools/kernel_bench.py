@@ -81,10 +81,14 @@ def main():
         G64 = P.gram(step.x, None, ws=step.gws)
         torch.cuda.synchronize()
         print(f"gram_i8 vs f64 Gram: max rel {((Gi - G64).abs().max() / G64.abs().max()).item():.3e}")
+        Gref = Gi.clone()
         for dg in os.environ.get("GRAM_DIAGS", "").split(","):  # timing-only ablations
             if dg:
                 os.environ["MMB_GRAM_DIAG"] = dg
                 res[f"gram_i8 diag {dg}"] = timed(lambda: P.gram_i8(step.x, cm, Gi, ws=step.gws), args.reps)
+                if int(dg) & 15 == 0:  # schedule variants: the same Gram
+                    torch.cuda.synchronize()
+                    print(f"gram_i8 diag {dg} bit-identical: {torch.equal(Gi, Gref)}")
         os.environ.pop("MMB_GRAM_DIAG", None)
     if "pcsolve" in which:
         res["pcsolve"] = timed(lambda: P.pc_solve(step.G, z0, 1, False), args.reps)
