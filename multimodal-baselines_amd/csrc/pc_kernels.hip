@@ -523,30 +523,38 @@ __global__ void colmax_kernel(const float* __restrict__ x, int64_t N, int D, int
   }
 }
 
+// Fixed-order sum of the R range partials of every upper-triangle tile
+// element (consecutive threads read consecutive partial elements: coalesced;
+// the former element-of-G order read the lower half transposed, 8x the bytes),
+// written to G[p][q] and mirrored to G[q][p] for off-diagonal tiles (diagonal
+// tiles hold both halves themselves).  Same sums in the same order as before.
 __global__ void gram_tri_reduce_kernel(const double* __restrict__ part, int D, int nt, int R,
                                        int accumulate, double* __restrict__ g) {
   const int T = nt * (nt + 1) / 2;
-  const int64_t total = static_cast<int64_t>(D) * D;
+  const int64_t total = static_cast<int64_t>(T) * 256;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
-    int p = static_cast<int>(e / D), q = static_cast<int>(e % D);
-    if (p / 16 > q / 16) {
-      const int t = p; p = q; q = t;
-    }
-    const int bi = p / 16, bj = q / 16;
-    const int tau = bi * nt - bi * (bi - 1) / 2 + (bj - bi);
-    const int64_t off = static_cast<int64_t>(tau) * 256 + (p % 16) * 16 + (q % 16);
+    const int tau = static_cast<int>(e >> 8), w = static_cast<int>(e & 255);
+    int bi, bj;
+    tri_tile(tau, nt, bi, bj);
+    const int p = 16 * bi + (w >> 4), q = 16 * bj + (w & 15);
+    if (p >= D || q >= D) continue;
     // eight independent partial sums (eight loads in flight; a single chain
     // waited on every load), combined in a fixed order: deterministic
     double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     int r = 0;
     for (; r + 8 <= R; r += 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s8[u] += part[static_cast<int64_t>(r + u) * T * 256 + off];
+      for (int u = 0; u < 8; ++u) s8[u] += part[static_cast<int64_t>(r + u) * total + e];
     }
-    for (; r < R; ++r) s8[0] += part[static_cast<int64_t>(r) * T * 256 + off];
+    for (; r < R; ++r) s8[0] += part[static_cast<int64_t>(r) * total + e];
     const double sum = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-    g[e] = accumulate ? g[e] + sum : sum;
+    const int64_t e1 = static_cast<int64_t>(p) * D + q;
+    g[e1] = accumulate ? g[e1] + sum : sum;
+    if (bi != bj) {
+      const int64_t e2 = static_cast<int64_t>(q) * D + p;
+      g[e2] = accumulate ? g[e2] + sum : sum;
+    }
   }
 }
 
