@@ -1002,6 +1002,10 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve_kernel(const double* __rest
 //              share of the rows, the 16 partials summed in a fixed order.
 // Everything k x k (Cholesky, triangular inverse, Jacobi) stays on one wave.
 constexpr int kP16MaxD = 320;
+// 16 waves.  (8 waves with a software-pipelined G.Z product -- two 16-deep
+// batches of G per lane in flight, which 128 VGPRs cannot hold -- measured
+// slower: 0.340 vs 0.310 ms per solve; the products are not what bounds it.)
+constexpr int kP16NT = 1024;
 constexpr int kP16W = 16;  // block width (k <= 16)
 
 struct P16Lds {
@@ -1011,10 +1015,10 @@ struct P16Lds {
 };
 
 // M (k x k, compact) = X^T Y over the Dp rows of two [Dp][16] blocks.
-__device__ void p16_gram(const double* X, const double* Y, int Dp, int k, double* part, double* M) {
+__device__ __forceinline__ void p16_gram(const double* X, const double* Y, int Dp, int k, double* part, double* M) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   f64x4 acc = {0, 0, 0, 0};
-  for (int p = 4 * wave; p < Dp; p += 4 * (kSolveNT / kWave)) {
+  for (int p = 4 * wave; p < Dp; p += 4 * (kP16NT / kWave)) {
     const int o = (p + (lane >> 4)) * kP16W + (lane & 15);
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[o], Y[o], acc, 0, 0, 0);
   }
@@ -1025,7 +1029,7 @@ __device__ void p16_gram(const double* X, const double* Y, int Dp, int k, double
     const int i = tid >> 4, j = tid & 15;
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < kSolveNT / kWave; ++w) s += part[w * 256 + tid];
+    for (int w = 0; w < kP16NT / kWave; ++w) s += part[w * 256 + tid];
     if (i < k && j < k) M[i * k + j] = s;
   }
   __syncthreads();
@@ -1034,23 +1038,31 @@ __device__ void p16_gram(const double* X, const double* Y, int Dp, int k, double
 // GZ = G Z (G symmetric [D][D] in global memory / L2).  16 k-steps of loads
 // are issued before their MFMAs (one L2 latency per batch, not per step);
 // two accumulators alternate so consecutive MFMAs are independent.  (32-step
-// batches measured slower on MI355X: 24.3 vs 19.5 us per product.)
+// batches measured slower on MI355X: 24.3 vs 19.5 us per product.)  The p16
+// helpers are force-inlined: as called functions they were compiled with
+// flat loads and spilled their operands to scratch around every call
+// (pc_solve 0.316 -> 0.310 ms).
 constexpr int kGzBatch = 16;
-__device__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double* Z, double* GZ) {
+__device__ __forceinline__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double* Z, double* GZ) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int mt = Dp / 16;
-  for (int t = wave; t < mt; t += kSolveNT / kWave) {
+  const int nbat = (Dp + 4 * kGzBatch - 1) / (4 * kGzBatch);
+  for (int t = wave; t < mt; t += kP16NT / kWave) {
     const int p = t * 16 + (lane & 15);
     const int pc = min(p, D - 1);
     f64x4 acc0 = {0, 0, 0, 0}, acc1 = acc0;
-    for (int q0 = 0; q0 < Dp; q0 += 4 * kGzBatch) {
-      double g[kGzBatch];
+    // clamped addresses, unconditional loads, selected after (keeps loads in
+    // flight; a batch index past the last re-reads it, an L2 hit)
+    auto load = [&](int bt, double (&g)[kGzBatch]) {
+      const int q0 = 4 * kGzBatch * min(bt, nbat - 1);
 #pragma unroll
       for (int s = 0; s < kGzBatch; ++s) {
         const int q = q0 + 4 * s + (lane >> 4);
-        // clamped address, unconditional load, selected after (keeps loads in flight)
         g[s] = G[static_cast<int64_t>(min(q, D - 1)) * D + pc];
       }
+    };
+    auto comp = [&](int bt, const double (&g)[kGzBatch]) {
+      const int q0 = 4 * kGzBatch * bt;
 #pragma unroll
       for (int s = 0; s < kGzBatch; ++s) {
         const int q = q0 + 4 * s + (lane >> 4);
@@ -1062,6 +1074,11 @@ __device__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double
           acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc0, 0, 0, 0);
         }
       }
+    };
+    double g0[kGzBatch];
+    for (int bt = 0; bt < nbat; ++bt) {
+      load(bt, g0);
+      comp(bt, g0);
     }
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg)
@@ -1073,7 +1090,7 @@ __device__ void p16_gz(const double* __restrict__ G, int D, int Dp, const double
 // keeps row i of the trailing matrix in registers (right-looking, column j's
 // multipliers broadcast by shuffles); lane c then solves L x = e_c.  *fail is
 // set if a pivot is not positive (the pivot is then replaced by 1).
-__device__ void p16_chol(const double* sW, double* sL, double* sLi, int k, int lane, int* fail) {
+__device__ __forceinline__ void p16_chol(const double* sW, double* sL, double* sLi, int k, int lane, int* fail) {
   double w[kMaxK], l[kMaxK];
 #pragma unroll
   for (int m = 0; m < kMaxK; ++m) {
@@ -1198,7 +1215,7 @@ __device__ double p16_top_eig(const double* A, int k, int lane, double* u) {
 // 2: equilibration + one CholeskyQR -- a well-conditioned basis of the same
 // span, all the subspace iteration needs between products (the span, not the
 // basis, fixes the result: span(Q) = span(G^q Omega)).
-__device__ void p16_orth(double* Z, int D, int Dp, int k, double* part, double* sW, double* sL,
+__device__ __forceinline__ void p16_orth(double* Z, int D, int Dp, int k, double* part, double* sW, double* sL,
                          double* sLi, int* s_fail, int npass = 3) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   for (int pass = 0; pass < npass; ++pass) {
@@ -1243,7 +1260,7 @@ __device__ void p16_orth(double* Z, int D, int Dp, int k, double* part, double* 
   }
 }
 
-__global__ __launch_bounds__(kSolveNT) void pc_solve16_kernel(const double* __restrict__ G, int D,
+__global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __restrict__ G, int D,
                                                               const double* __restrict__ z0, int k,
                                                               int npc, int n_iter, int transposed,
                                                               double* __restrict__ pc_out) {
@@ -1255,15 +1272,15 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve16_kernel(const double* __re
   __shared__ double sA[kMaxK * kMaxK], sV[kMaxK * kMaxK], sW[kMaxK * kMaxK];
   __shared__ double sL[kMaxK * kMaxK], sLi[kMaxK * kMaxK], sT[kMaxK * kMaxK];
   __shared__ double sy[kMaxK];
-  __shared__ double s_rd[kSolveNT / kWave];
-  __shared__ double s_rv[kSolveNT / kWave];
-  __shared__ int s_ri[kSolveNT / kWave];
+  __shared__ double s_rd[kP16NT / kWave];
+  __shared__ double s_rv[kP16NT / kWave];
+  __shared__ int s_ri[kP16NT / kWave];
   __shared__ double sU[kMaxK * kMaxK];  // eigenvectors of A, largest first
   __shared__ int s_fail;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
 
   PC_MARK(0);
-  for (int e = tid; e < Dp * kP16W; e += kSolveNT) {
+  for (int e = tid; e < Dp * kP16W; e += kP16NT) {
     const int p = e / kP16W, j = e % kP16W;
     sZ[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
     sGZ[e] = 0.0;
@@ -1379,7 +1396,7 @@ __global__ __launch_bounds__(kSolveNT) void pc_solve16_kernel(const double* __re
     double tot = 0.0, bb = -1.0;
     int bi = 0x7fffffff;
     double vbest = 0.0;
-    for (int w = 0; w < kSolveNT / kWave; ++w) {
+    for (int w = 0; w < kP16NT / kWave; ++w) {
       tot += s_rd[w];
       if (s_rv[w] > bb || (s_rv[w] == bb && s_ri[w] < bi)) {
         bb = s_rv[w];
@@ -1801,7 +1818,7 @@ extern "C" int mmb_pc_solve(const double* g, int d, const double* z0, int k, int
                                 static_cast<int>(p16_lds_bytes(kP16MaxD)));
       attr = true;
     }
-    pc_solve16_kernel<<<1, kSolveNT, lds, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
+    pc_solve16_kernel<<<1, kP16NT, lds, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
   } else {
     pc_solve_kernel<<<1, kSolveNT, 0, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
   }

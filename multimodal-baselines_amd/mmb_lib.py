@@ -18,7 +18,8 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmmb.so")
+# MMB_LIB_PATH: another build of the library (same-box A/B of kernel builds)
+LIB_PATH = os.environ.get("MMB_LIB_PATH") or os.path.join(HERE, "libmmb.so")
 
 MMB_FLAG_ID_RANGE = 1
 MMB_FLAG_ZERO_WEIGHTS = 2
