@@ -315,7 +315,8 @@ def dominant_kernel(step, T, D, text_rows=None):
     if step.stream_project:
         return (fused_kernel_bytes(T, D, step.a, step.vd, text_rows=text_rows),
                 "utt_fused_kernel (mmb_mm2_stream_project: 4 streaming waves, one per "
-                "utterance, + 4 projecting waves per CU, sums in an LDS ring)")
+                "utterance, two 8-frame load groups in flight, + 4 projecting waves per CU, "
+                "sums in an LDS ring)")
     kname = ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
              else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)")
     return stream_kernel_bytes(T, D, step.a, step.vd, text_rows=text_rows), kname
