@@ -14,6 +14,9 @@
 // so the SGD update W1 -= lr dW1 is a lane-local FMA on the fragment with no
 // shuffles.  Each tile is owned by one wave for the whole run (its own
 // stores are re-read only by itself).  Bias, output layer and loss are VALU on LDS.
+#include <algorithm>
+#include <cstdlib>
+
 #include "mmb_common.h"
 
 namespace mmb {
@@ -60,7 +63,13 @@ __device__ __forceinline__ void store_frag(float* p, const f32x16& v) {
   for (int i = 0; i < 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
 }
 
-__global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
+// NT threads; REGT > 0: each wave's W1^T tiles (<= REGT) held in registers for
+// the whole run (8 waves x 256 VGPRs), so neither the forward nor the SGD
+// update touches L2 for W1; REGT = 0: tiles re-read from the L2-resident
+// tiled copy every step (16 waves x 128 VGPRs, where the tiles spilled).
+template <int NT, int REGT>
+__global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
+  constexpr int kNW = NT / kWave;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int DP = a.DP, HP = a.HP, O = a.O;
   int64_t* s_perm = reinterpret_cast<int64_t*>(smem);  // [2][32] row indices (prefetch)
@@ -72,7 +81,7 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
   float* sb2 = sb1 + HP;                              // [O]
   float* sg = sb2 + O;                                // [32][O]
   float* sy = sg + kBatchMax * O;                     // [32][O]
-  float* s_red = sy + kBatchMax * O;                  // [kMaxWaves]
+  float* s_red = sy + kBatchMax * O;                  // [kNW]
   float* sdh = spart;                                 // [32][HP]
   const int SX = DP + 1;
 
@@ -86,21 +95,27 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
   float* wt = a.w1t + (static_cast<int64_t>(Th) * a.nTd * kWave + lane) * 16;  // + td*64*16
 
   // W1 -> tiled W1^T workspace (zero outside [H) x [D))
-  for (int64_t e = tid; e < static_cast<int64_t>(a.nTh) * a.nTd * kWave * 16; e += kMlpNT) {
+  for (int64_t e = tid; e < static_cast<int64_t>(a.nTh) * a.nTd * kWave * 16; e += NT) {
     const int r = static_cast<int>(e & 15), l = static_cast<int>((e >> 4) & 63);
     const int64_t tile = e >> 10;
     const int th = static_cast<int>(tile / a.nTd), td = static_cast<int>(tile % a.nTd);
     const int h = 32 * th + (l & 31), d = 32 * td + c_row(r, l);
     a.w1t[e] = (h < a.H && d < a.D) ? a.w1[static_cast<int64_t>(h) * a.D + d] : 0.f;
   }
-  for (int e = tid; e < O * HP; e += kMlpNT) {
+  for (int e = tid; e < O * HP; e += NT) {
     const int o = e / HP, h = e % HP;
     sW2[e] = h < a.H ? a.w2[o * a.H + h] : 0.f;
   }
-  for (int h = tid; h < HP; h += kMlpNT) sb1[h] = h < a.H ? a.b1[h] : 0.f;
-  for (int o = tid; o < O; o += kMlpNT) sb2[o] = a.b2[o];
+  for (int h = tid; h < HP; h += NT) sb1[h] = h < a.H ? a.b1[h] : 0.f;
+  for (int o = tid; o < O; o += NT) sb2[o] = a.b2[o];
   __threadfence_block();
   __syncthreads();
+  f32x16 wreg[REGT > 0 ? REGT : 1];
+  if constexpr (REGT > 0) {
+#pragma unroll
+    for (int t = 0; t < REGT; ++t)
+      if (t < ntiles) wreg[t] = load_frag(wt + static_cast<int64_t>(td0 + t) * kWave * 16);
+  }
 
   const int64_t spe = (a.n_per_epoch + a.B - 1) / a.B;
   const int64_t nsteps = spe * a.n_epochs;
@@ -132,7 +147,7 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
     // 1. gather the batch rows (DataLoader order) into LDS
     if (v4) {
       const int U = DP >> 2;  // float4 units of a padded row
-      for (int e = tid; e < kBatchMax * U; e += kMlpNT) {
+      for (int e = tid; e < kBatchMax * U; e += NT) {
         const int b = e / U, u = e - b * U;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (b < Bc && 4 * u < a.D) v = *reinterpret_cast<const float4*>(a.lat + pp[b] * a.D + 4 * u);
@@ -140,14 +155,14 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
         dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
       }
     } else {
-      for (int e = tid; e < kBatchMax * DP; e += kMlpNT) {
+      for (int e = tid; e < kBatchMax * DP; e += NT) {
         const int b = e / DP, d = e % DP;
         float v = 0.f;
         if (b < Bc && d < a.D) v = a.lat[pp[b] * a.D + d];
         sx[b * SX + d] = v;
       }
     }
-    for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
+    for (int e = tid; e < kBatchMax * O; e += NT) {
       const int b = e / O, o = e % O;
       sy[e] = (b < Bc) ? a.lab[pp[b] * O + o] : 0.f;
     }
@@ -159,21 +174,28 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
       const float* xb = sx + (lane & 31) * SX + 4 * (lane >> 5);
-      for (int t = 0; t < ntiles; ++t) {
+      auto fwd_tile = [&](int t, const f32x16& w) {
         const int td = td0 + t;
-        const f32x16 w = load_frag(wt + static_cast<int64_t>(td) * kWave * 16);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float xa = xb[32 * td + (r & 3) + 8 * (r >> 2)];
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, w[r], acc, 0, 0, 0);
         }
+      };
+      if constexpr (REGT > 0) {
+#pragma unroll
+        for (int t = 0; t < REGT; ++t)
+          if (t < ntiles) fwd_tile(t, wreg[t]);
+      } else {
+        for (int t = 0; t < ntiles; ++t)
+          fwd_tile(t, load_frag(wt + static_cast<int64_t>(td0 + t) * kWave * 16));
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) spart[(grp * kBatchMax + c_row(r, lane)) * HP + hcol] = acc[r];
     }
     __syncthreads();
     // 3. hidden = relu(sum_g partial + b1)  (fixed group order)
-    for (int e = tid; e < kBatchMax * HP; e += kMlpNT) {
+    for (int e = tid; e < kBatchMax * HP; e += NT) {
       const int b = e / HP, h = e % HP;
       float p = sb1[h];
       for (int g = 0; g < a.G; ++g) p += spart[(g * kBatchMax + b) * HP + h];
@@ -186,19 +208,22 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
     //    100-long serial chain per row
     float lsum = 0.f;
     if (O == 1) {
-      const int b = 2 * wave + (lane >> 5), l32 = lane & 31;
-      float part = 0.f;
-      for (int h = l32; h < a.H; h += 32) part = fmaf(sW2[h], shid[b * HP + h], part);
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
-      const float diff = (sb2[0] + part) - sy[b];
-      const bool valid = b < Bc;
-      if (l32 == 0) {
-        sg[b] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc) : 0.f;
-        if (valid) lsum = fabsf(diff);
+      for (int k = 0; k < kBatchMax / (2 * kNW); ++k) {
+        const int b = 2 * (wave + kNW * k) + (lane >> 5), l32 = lane & 31;
+        float part = 0.f;
+        for (int h = l32; h < a.H; h += 32) part = fmaf(sW2[h], shid[b * HP + h], part);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
+        const float diff = (sb2[0] + part) - sy[b];
+        const bool valid = b < Bc;
+        if (l32 == 0) {
+          sg[b] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc) : 0.f;
+          if (valid) lsum += fabsf(diff);
+        }
       }
     } else {
-      for (int e = tid; e < kBatchMax * O; e += kMlpNT) {
+      for (int e = tid; e < kBatchMax * O; e += NT) {
         const int b = e / O, o = e % O;
         float out = sb2[o];
         for (int h = 0; h < a.H; ++h) out = fmaf(sW2[o * HP + h], shid[b * HP + h], out);
@@ -212,7 +237,7 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
     if (lane == 0) s_red[wave] = lsum;
     __syncthreads();
     // 5. dH = relu'(.) * g W2 ; then W2/b2 gradients (old W2 already consumed)
-    for (int e = tid; e < kBatchMax * HP; e += kMlpNT) {
+    for (int e = tid; e < kBatchMax * HP; e += NT) {
       const int b = e / HP, h = e % HP;
       float s = 0.f;
       if (shid[e] > 0.f)
@@ -223,7 +248,7 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
     // 6. dW1^T = X^T dH (MFMA, K = batch) and the SGD step on the owned tiles;
     //    VALU updates of b1/W2/b2
     if (mw) {
-      for (int t = 0; t < ntiles; ++t) {
+      auto grad_tile = [&](int t) {
         const int td = td0 + t;
         f32x16 acc;
 #pragma unroll
@@ -235,14 +260,29 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
           const float db = sdh[b * HP + hcol];
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, db, acc, 0, 0, 0);
         }
-        float* p = wt + static_cast<int64_t>(td) * kWave * 16;
-        f32x16 w = load_frag(p);
+        return acc;
+      };
+      if constexpr (REGT > 0) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) w[r] = fmaf(-a.lr, acc[r], w[r]);
-        store_frag(p, w);
+        for (int t = 0; t < REGT; ++t) {
+          if (t < ntiles) {
+            const f32x16 g = grad_tile(t);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) wreg[t][r] = fmaf(-a.lr, g[r], wreg[t][r]);
+          }
+        }
+      } else {
+        for (int t = 0; t < ntiles; ++t) {
+          const f32x16 g = grad_tile(t);
+          float* p = wt + static_cast<int64_t>(td0 + t) * kWave * 16;
+          f32x16 w = load_frag(p);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) w[r] = fmaf(-a.lr, g[r], w[r]);
+          store_frag(p, w);
+        }
       }
     }
-    for (int e = tid; e < O * HP; e += kMlpNT) {
+    for (int e = tid; e < O * HP; e += NT) {
       const int o = e / HP, h = e % HP;
       if (h < a.H) {
         float gsum = 0.f;
@@ -250,28 +290,33 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
         sW2[e] = fmaf(-a.lr, gsum, sW2[e]);
       }
     }
-    for (int h = tid; h < a.H; h += kMlpNT) {
+    for (int h = tid; h < a.H; h += NT) {
       float gsum = 0.f;
       for (int b = 0; b < kBatchMax; ++b) gsum += sdh[b * HP + h];
       sb1[h] = fmaf(-a.lr, gsum, sb1[h]);
     }
-    for (int o = tid; o < O; o += kMlpNT) {
+    for (int o = tid; o < O; o += NT) {
       float gsum = 0.f;
       for (int b = 0; b < kBatchMax; ++b) gsum += sg[b * O + o];
       sb2[o] = fmaf(-a.lr, gsum, sb2[o]);
     }
     if (tid == 0) {
       float l = 0.f;
-      for (int w = 0; w < kMaxWaves; ++w) l += s_red[w];
+      for (int w = 0; w < kNW; ++w) l += s_red[w];
       a.step_loss[step] = l / static_cast<float>(Bc * O);
     }
     __syncthreads();
   }
 
   // write the parameters back
+  if constexpr (REGT > 0) {
+#pragma unroll
+    for (int t = 0; t < REGT; ++t)
+      if (t < ntiles) store_frag(wt + static_cast<int64_t>(td0 + t) * kWave * 16, wreg[t]);
+  }
   __threadfence_block();
   __syncthreads();
-  for (int64_t e = tid; e < static_cast<int64_t>(a.H) * a.D; e += kMlpNT) {
+  for (int64_t e = tid; e < static_cast<int64_t>(a.H) * a.D; e += NT) {
     const int h = static_cast<int>(e / a.D), d = static_cast<int>(e % a.D);
     const int th = h >> 5, td = d >> 5, dr = d & 31;
     // invert c_row: dr = (r&3) + 8*(r>>2) + 4*(lane>>5)
@@ -279,9 +324,9 @@ __global__ __launch_bounds__(kMlpNT) void mlp_train_kernel(MlpArgs a) {
     const int l = (h & 31) + 32 * hl;
     a.w1[e] = a.w1t[((static_cast<int64_t>(th) * a.nTd + td) * kWave + l) * 16 + r];
   }
-  for (int e = tid; e < O * a.H; e += kMlpNT) a.w2[e] = sW2[(e / a.H) * HP + e % a.H];
-  for (int h = tid; h < a.H; h += kMlpNT) a.b1[h] = sb1[h];
-  for (int o = tid; o < O; o += kMlpNT) a.b2[o] = sb2[o];
+  for (int e = tid; e < O * a.H; e += NT) a.w2[e] = sW2[(e / a.H) * HP + e % a.H];
+  for (int h = tid; h < a.H; h += NT) a.b1[h] = sb1[h];
+  for (int o = tid; o < O; o += NT) a.b2[o] = sb2[o];
 }
 
 // Forward (+ optional L1 per batch) — one workgroup per batch of rows.
@@ -460,16 +505,25 @@ __global__ __launch_bounds__(256) void mlp_bwd_params_kernel(const float* __rest
   }
 }
 
+template <int NT, int REGT>
 static int launch_train(const MlpArgs& a, size_t lds, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<NT, REGT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  mlp_train_kernel<<<1, kMlpNT, lds, stream>>>(a);
+  mlp_train_kernel<NT, REGT><<<1, NT, lds, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
+}
+
+// W1 tiles in registers (8 waves, <= 5 tiles each) where they fit; 0 keeps
+// the L2-tile kernel (MMB_MLP_REG, read per launch)
+constexpr int kRegWaves = 8, kRegTiles = 5;
+static int mlp_reg() {
+  const char* e = getenv("MMB_MLP_REG");
+  return e ? atoi(e) : 1;
 }
 
 }  // namespace mmb
@@ -521,7 +575,12 @@ extern "C" int mmb_mlp_train(const float* latents, const float* labels, const in
   a.nTh = static_cast<int>(ceil_div(h, 32));
   a.nTd = static_cast<int>(ceil_div(d, 32));
   MMB_REQUIRE(a.nTh <= kMaxWaves);
-  a.G = kMaxWaves / a.nTh;
+  bool reg = false;
+  if (mlp_reg() && a.nTh <= kRegWaves) {
+    const int g = std::min(kRegWaves / a.nTh, a.nTd);
+    reg = ceil_div(a.nTd, g) <= kRegTiles;
+  }
+  a.G = (reg ? kRegWaves : kMaxWaves) / a.nTh;
   if (a.G > a.nTd) a.G = a.nTd;
   a.DP = a.nTd * 32;
   a.HP = a.nTh * 32;
@@ -530,7 +589,8 @@ extern "C" int mmb_mlp_train(const float* latents, const float* labels, const in
                                       static_cast<size_t>(kBatchMax) * a.HP + o * a.HP + a.HP +
                                       o + 2 * kBatchMax * o + kMaxWaves);
   MMB_REQUIRE(lds <= 160 * 1024);
-  return launch_train(a, lds, stream);
+  return reg ? launch_train<kRegWaves * kWave, kRegTiles>(a, lds, stream)
+             : launch_train<kMlpNT, 0>(a, lds, stream);
 }
 
 extern "C" int mmb_mlp_forward_train(const float* x, int64_t b, int d, int h, int o,
