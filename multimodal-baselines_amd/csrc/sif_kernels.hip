@@ -992,7 +992,7 @@ __device__ __forceinline__ void frame_piece(const float* base, int W, int L, int
 // projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
 // no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
 // the frames (constant sums: the projectors alone)
-template <int UNR, bool NT, int DIAG = 0, bool PIPE = false, int SL = kGSlots>
+template <int UNR, bool NT, int DIAG = 0, int PIPE = 0, int SL = kGSlots>
 __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_fused_kernel(
     FusedArgs f) {
   const StreamArgs& a = f.s;
@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
     };
 
-    if constexpr (!PIPE) {
+    if constexpr (PIPE == 0) {
       for (int64_t j = 0;; ++j) {
         int64_t row0, rend;
         if (!batch(j, row0, rend)) break;
@@ -1315,16 +1315,202 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
           consume(g, b0);
         }
       };
-      for (int64_t j = 0;; ++j) {
+      // PIPE == 2: the same pipeline, and each piece's tail also issues the
+      // NEXT piece's first group (text -> audio -> visual -> the next batch's
+      // text) once its own next-to-last group is summed, so loads stay in
+      // flight across piece and batch boundaries too; the next batch's first
+      // text row is staged during the visual piece's last groups.  Pieces with
+      // an odd group count drain as before.
+      float4 pb0[UNR][2], pb1[UNR][2];
+      bool pre = false;  // pb0 holds this piece's group 0 (issued by the previous piece)
+      int rid_pre = -1, raw_p = -1;
+      float w_pre = 0.f, wd_p = 0.f;
+      auto piece2 = [&](auto m_c, int64_t j, int64_t i0, int nrows, int64_t ni0, int nnr) {
+        constexpr int M = decltype(m_c)::value;
+        constexpr bool TEXT = M == 0;
+        const int W = wdt[M], UW = W >> 2;
+        const int ngr = (L + UNR - 1) / UNR, ng = nrows * ngr;
+        const float* src = TEXT ? (gather ? a.table : a.text_dense) : (M == 1 ? a.audio : a.visual);
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool has_next = M < 2 || nnr > 0;
+        if constexpr (M == 2) {
+          // the text piece's x / aux stores complete before any visual
+          // increment (the projectors read x after the visual piece): with
+          // group 0 in flight the 16 newest operations are its loads
+          if (pre) {
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        }
+        int cur = 0;
+        int rid_c = -1, rid_n = -1, raw_n = -1;
+        float w_c = 0.f, w_n = 0.f, wd_n = 0.f;
+        float4 num[2], sx[2], sxx[2];
+        float cnt = 0.f, sw = 0.f;
+        if constexpr (TEXT) {
+          if (pre) {
+            rid_c = rid_pre;
+            w_c = w_pre;
+          } else {
+            int raw;
+            float wd;
+            tok_issue(i0, raw, wd);
+            tok_resolve(raw, wd, rid_c, w_c);
+          }
+        }
+        const int vo0 = 16 * min(lane, UW - 1), vo1 = 16 * min(lane + kWave, UW - 1);
+        // group g of this piece (or, NX, group 0 of the next piece) into v
+        auto load_group = [&](auto nx_c, int g, float4 (&v)[UNR][2]) {
+          constexpr bool NX = decltype(nx_c)::value;
+          constexpr int MM = NX ? (M + 1) % 3 : M;
+          constexpr bool T2 = MM == 0;
+          const int rr = NX ? 0 : g / ngr, t0 = NX ? 0 : (g - rr * ngr) * UNR;
+          const int64_t i = NX ? (M == 2 ? ni0 : i0) : i0 + 4 * rr;
+          const int W2 = wdt[MM], U2 = W2 >> 2;
+          const float* s2 = T2 ? (gather ? a.table : a.text_dense) : (MM == 1 ? a.audio : a.visual);
+          const int o0 = NX ? 16 * min(lane, U2 - 1) : vo0, o1 = NX ? 16 * min(lane + kWave, U2 - 1) : vo1;
+          int rid = 0;
+          if constexpr (T2) rid = NX ? rid_pre : (rr == cur ? rid_c : rid_n);
+          const bool rowbase = !T2 || !gather;
+          const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<float*>(rowbase ? s2 + i * L * W2 : s2), 0,
+              rowbase ? L * W2 * 4 : static_cast<int>(a.V * D * 4), 0x00020000);
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const int t = min(t0 + u, L - 1);
+            int so;
+            if constexpr (T2) {
+              const int r = __builtin_amdgcn_readlane(rid, t);
+              so = gather ? (r >= 0 ? r : 0) * D * 4 : t * W2 * 4;
+            } else {
+              so = t * W2 * 4;
+            }
+            constexpr int pol = (!T2 && NT) ? 2 : 0;  // non-temporal frame streams
+            v[u][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o0, so, pol));
+            v[u][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o1, so, pol));
+          }
+        };
+        auto issue = [&](int g, float4 (&v)[UNR][2]) { load_group(std::false_type{}, g, v); };
+        auto sum_frame = [&](int t, const float4 (&v)[2]) {
+          if constexpr (TEXT) {
+            const int r = __builtin_amdgcn_readlane(rid_c, t);
+            const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w_c), t));
+            const bool ok = r >= 0;  // an out-of-range id (flagged) contributes a zero row
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const float4 x = ok ? v[c] : z4;
+              fma4(num[c], wt, x);
+              add4(sx[c], x);
+              sq4(sxx[c], x);
+            }
+          } else {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              add4(sx[c], v[c]);
+              sq4(sxx[c], v[c]);
+            }
+          }
+        };
+        auto consume = [&](int g, const float4 (&v)[UNR][2]) {
+          const int rr = g / ngr, gg = g - rr * ngr, t0 = gg * UNR;
+          if (gg == 0) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
+            if constexpr (TEXT) {
+              cnt = wave_sum((w_c != 0.f) ? 1.f : 0.f);
+              sw = wave_sum(w_c);
+              // every weight 0: x is 0/0 = NaN (numpy's answer); TruncatedSVD
+              // would reject the split -- report it through the flag word
+              if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+              if (rr + 1 < nrows) tok_issue(i0 + 4 * (rr + 1), raw_n, wd_n);
+            }
+          }
+          if constexpr (TEXT) {
+            if (gg == 1 && rr + 1 < nrows) tok_resolve(raw_n, wd_n, rid_n, w_n);
+          }
+          if constexpr (M == 2) {  // the next batch's first text row
+            if (has_next && ng >= 4 && g == ng - 4) tok_issue(ni0, raw_p, wd_p);
+            if (has_next && ng >= 4 && g == ng - 3) tok_resolve(raw_p, wd_p, rid_pre, w_pre);
+          }
+          if (t0 + UNR <= L) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) sum_frame(t0 + u, v[u]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u)
+              if (t0 + u < L) sum_frame(t0 + u, v[u]);
+          }
+          if (gg == ngr - 1) {
+            const int q = uw + 4 * rr;
+            finish_row(std::false_type{}, j, M, q, i0 + 4 * rr, num, sx, sxx, cnt, sw);
+            cur = rr + 1;
+            if constexpr (TEXT) {
+              rid_c = rid_n;
+              w_c = w_n;
+            }
+          }
+        };
+        if (!pre) issue(0, pb0);
+        int g = 0;
+#pragma unroll 1
+        for (; g + 2 < ng; g += 2) {
+          issue(g + 1, pb1);
+          consume(g, pb0);
+          issue(g + 2, pb0);
+          consume(g + 1, pb1);
+        }
+        if (g + 1 < ng) {
+          issue(g + 1, pb1);
+          consume(g, pb0);
+          if (has_next) {
+            if constexpr (M == 2) {
+              if (ng < 4) {  // too few groups to stage the tokens on the way
+                tok_issue(ni0, raw_p, wd_p);
+                tok_resolve(raw_p, wd_p, rid_pre, w_pre);
+              }
+            }
+            load_group(std::true_type{}, 0, pb0);
+          }
+          consume(g + 1, pb1);
+          pre = has_next;
+        } else {
+          consume(g, pb0);
+          pre = false;
+        }
+      };
+      auto rows_of = [&](int64_t jb, int64_t& i0) -> int {
         int64_t row0, rend;
-        if (!batch(j, row0, rend)) break;
-        const int64_t i0 = row0 + uw;
-        const int nrows = i0 < rend ? static_cast<int>(min<int64_t>(kGR / 4, (rend - i0 + 3) / 4)) : 0;
-        if (nrows == 0) continue;
-        piece(std::true_type{}, j, 0, i0, nrows);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x / aux stores before the audio increments
-        piece(std::false_type{}, j, 1, i0, nrows);
-        piece(std::false_type{}, j, 2, i0, nrows);
+        if (!batch(jb, row0, rend)) {
+          i0 = 0;
+          return 0;
+        }
+        i0 = row0 + uw;
+        return i0 < rend ? static_cast<int>(min<int64_t>(kGR / 4, (rend - i0 + 3) / 4)) : 0;
+      };
+      if constexpr (PIPE == 2) {
+        int64_t i0, ni0;
+        int nrows = rows_of(0, i0);
+        for (int64_t j = 0; nrows > 0; ++j) {
+          const int nnr = rows_of(j + 1, ni0);
+          piece2(std::integral_constant<int, 0>{}, j, i0, nrows, ni0, nnr);
+          piece2(std::integral_constant<int, 1>{}, j, i0, nrows, ni0, nnr);
+          piece2(std::integral_constant<int, 2>{}, j, i0, nrows, ni0, nnr);
+          i0 = ni0;
+          nrows = nnr;
+        }
+      } else {
+        for (int64_t j = 0;; ++j) {
+          int64_t row0, rend;
+          if (!batch(j, row0, rend)) break;
+          const int64_t i0 = row0 + uw;
+          const int nrows = i0 < rend ? static_cast<int>(min<int64_t>(kGR / 4, (rend - i0 + 3) / 4)) : 0;
+          if (nrows == 0) continue;
+          piece(std::true_type{}, j, 0, i0, nrows);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // x / aux stores before the audio increments
+          piece(std::false_type{}, j, 1, i0, nrows);
+          piece(std::false_type{}, j, 2, i0, nrows);
+        }
       }
     }
     if (a.cmax_part) {  // this wave's column bounds (mmb_gram_i8)
@@ -1539,7 +1725,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   }
 }
 
-template <int DIAG, int UNR = 8, bool PIPE = false, int SL = kGSlots>
+template <int DIAG, int UNR = 8, int PIPE = 0, int SL = kGSlots>
 static void launch_fused_v(const FusedArgs& f, int grid, hipStream_t stream) {
   constexpr size_t lds = fused_lds_bytes(SL);
   static bool attr = false;
@@ -1560,12 +1746,13 @@ static int fused_diag() {  // re-read per launch (in-process timing sweeps)
   return e ? atoi(e) : 0;
 }
 
-// streamer: 1 = pipelined (two groups in flight; default: kernel 23.35 ->
-// 22.49 ms, step 25.14 -> 24.41 ms in a same-process A/B, r02k), 0 = one group
-// at a time (the bit-identical reference of the tests)
+// streamer: 1 = pipelined (two groups in flight: kernel 23.35 -> 22.49 ms,
+// step 25.14 -> 24.41 ms in a same-process A/B, r02k); 2 (default) = also
+// prefetching across piece and batch boundaries (22.32 -> 22.14 ms, r02y);
+// 0 = one group at a time (the bit-identical reference of the tests)
 static int fused_pipe() {
   const char* e = getenv("MMB_FUSED_PIPE");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 2;
 }
 
 static int fused_slots() {  // ring slots: 62 (default) or 60 (in-process A/B)
@@ -1582,7 +1769,13 @@ static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   // and addresses the word table through one buffer descriptor (< 2^31 bytes)
   const bool pipe = fused_pipe() != 0 && (f.s.L + un - 1) / un >= 3 &&
                     (f.s.ids == nullptr || f.s.V * f.s.D * 4 < (int64_t{1} << 31));
-  if (pipe && un == 8) {
+  if (pipe && un == 8 && fused_pipe() == 2 && (dg == 0 || dg == 1)) {
+    if (dg == 1) {
+      launch_fused_v<1, 8, 2>(f, grid, stream);
+    } else {
+      launch_fused_v<0, 8, 2>(f, grid, stream);
+    }
+  } else if (pipe && un == 8) {
     switch (dg) {
       case 1: launch_fused_v<1, 8, true>(f, grid, stream); break;
       case 2: launch_fused_v<2, 8, true>(f, grid, stream); break;

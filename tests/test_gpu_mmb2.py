@@ -654,7 +654,7 @@ def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False, balanced=False):
         ids = inp["ids"].long()
         kw = dict(text_dense=inp["table"][ids.clamp(min=0)].contiguous(),
                   w_dense=inp["wtab"][ids.clamp(min=0)] * (ids >= 0))
-    knobs = {"MMB_FUSED_PIPE": "1" if pipe else "0", "MMB_FUSED_BALANCED": "1" if balanced else "0"}
+    knobs = {"MMB_FUSED_PIPE": str(int(pipe)), "MMB_FUSED_BALANCED": "1" if balanced else "0"}
     old = {k: os.environ.get(k) for k in knobs}
     os.environ.update(knobs)
     try:
@@ -683,6 +683,7 @@ def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False, balanced=False):
 def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
     """The pipelined streamer of utt_fused_kernel (two frame groups in flight
     across group, row and text-token boundaries; buffer-descriptor loads)
+    (MMB_FUSED_PIPE=1; =2 also prefetching across piece and batch boundaries)
     against the group-at-a-time streamer: x, aux, MMB2 rows, column bounds
     and the flag word bit-identical -- partial batches, partial last groups
     (T = 33, 17), the 3-group minimum (T = 24; T = 16 falls back), narrow
@@ -698,7 +699,7 @@ def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
     proj = P.MMB2Projection(gen.networks(), 300, A, Vd, T, gpu)
     ref = _fused_outputs(inp, proj, N, T, A, Vd, pipe=False, dense=dense)
     names = ["x", "aux", "mmb2", "colmax", "flag"]
-    for pipe, bal in [(True, False), (True, True), (False, True)]:
+    for pipe, bal in [(1, False), (1, True), (0, True), (2, True), (2, False)]:
         got = _fused_outputs(inp, proj, N, T, A, Vd, pipe=pipe, dense=dense, balanced=bal)
         for nm, r, g in zip(names, ref, got):
             assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), (nm, pipe, bal)
