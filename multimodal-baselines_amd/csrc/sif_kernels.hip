@@ -833,8 +833,6 @@ struct FusedArgs {
   int64_t nb;              // batches = ceil(N / 48)
   int kq[3];               // padded piece widths (multiples of 32)
   int balanced;            // rows past the last full round split evenly over the workgroups
-  int psleep;              // projector: s_sleep 1 (64 clk) x psleep after each K chunk
-  int sprio;               // streamer waves at s_setprio 3
 };
 
 // bounded wait for *p >= target (workgroup scope); false once anything timed out
@@ -1038,7 +1036,6 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 
   if (wave < 4) {
     // ------------------------------------------------------------ streamer
-    if (f.sprio) __builtin_amdgcn_s_setprio(3);
     const int wdt[3] = {a.D, a.A, a.Vd};
     float4 cmx[2];
     cmx[0] = cmx[1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1623,15 +1620,12 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         };
         ld_b(0, bh[0], bl[0]);
         ld_b(1, bh[1], bl[1]);
-        const int ps = f.psleep;
 #pragma unroll 1
         for (int c = 0; c < npc; c += 2) {
           chunk(c, bh[0], bl[0]);
-          for (int k = 0; k < ps; ++k) __builtin_amdgcn_s_sleep(1);
           ld_b(c + 2, bh[0], bl[0]);
           if (c + 1 < npc) {
             chunk(c + 1, bh[1], bl[1]);
-            for (int k = 0; k < ps; ++k) __builtin_amdgcn_s_sleep(1);
             ld_b(c + 3, bh[1], bl[1]);
           }
         }
@@ -2097,12 +2091,8 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   f.c0 = c0;
   f.out = mmb2_out;
   f.nb = ceil_div(n, kGR);
-  {  // measurement knobs (in-process sweeps): projector throttle, streamer priority
-    const char* e = getenv("MMB_FUSED_PSLEEP");
-    f.psleep = e ? atoi(e) : 0;
-    e = getenv("MMB_FUSED_SPRIO");
-    f.sprio = e ? atoi(e) : 0;
-    e = getenv("MMB_FUSED_BALANCED");  // default on: 22.35 -> 22.26 ms (r02s)
+  {  // balanced tail (in-process A/B switch)
+    const char* e = getenv("MMB_FUSED_BALANCED");  // default on: 22.35 -> 22.26 ms (r02s)
     f.balanced = e ? atoi(e) : 1;
   }
   int parts = 0;
