@@ -679,7 +679,8 @@ def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False, balanced=False):
                                                 (5003, 24, 300, 300, False, True),
                                                 (50, 16, 300, 300, False, False),
                                                 (500, 40, 300, 300, True, False),
-                                                (49, 40, 100, 300, False, False)])
+                                                (49, 40, 100, 300, False, False),
+                                                (30011, 40, 300, 300, False, False)])
 def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
     """The pipelined streamer of utt_fused_kernel (two frame groups in flight
     across group, row and text-token boundaries; buffer-descriptor loads)
@@ -687,8 +688,10 @@ def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
     against the group-at-a-time streamer: x, aux, MMB2 rows, column bounds
     and the flag word bit-identical -- partial batches, partial last groups
     (T = 33, 17), the 3-group minimum (T = 24; T = 16 falls back), narrow
-    frames, dense text, negative and out-of-range ids -- and with balanced
-    per-workgroup row ranges (MMB_FUSED_BALANCED) instead of round robin."""
+    frames, dense text, negative and out-of-range ids -- and with the rows
+    past the last full round of batches split evenly over the workgroups
+    (MMB_FUSED_BALANCED; N = 30011: two full rounds of 256 x 48 rows and a
+    5,435-row tail) instead of left as whole batches."""
     inp = synth.device_workload(N, T, 20_000, A=A, Vd=Vd, seed=71, device=gpu)
     if bad:  # negative ids wrap; ids >= V are flagged and contribute zero rows
         inp["ids"][3, 5] = -7
