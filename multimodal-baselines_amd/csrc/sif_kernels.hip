@@ -985,7 +985,8 @@ __device__ __forceinline__ void frame_piece(const float* base, int W, int L, int
   }
 }
 
-// DIAG (timing-only builds, MMB_FUSED_DIAG; wrong MMB2 rows): bit 4 every B
+// DIAG (timing-only builds, MMB_FUSED_DIAG; wrong MMB2 rows): bit 7 the
+// epilogue without its x re-read, bit 8 without its MMB2 stores; bit 4 every B
 // chunk read from the piece's first chunk, bit 5 no B loads; bit 0 the
 // projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
 // no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
@@ -1635,7 +1636,10 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
       } else {
         kloop(std::integral_constant<int, kFTiles - 1>{});
       }
-      fused_signal(consumed);  // this projector's reads of the piece's slots are done
+      // this projector's LDS reads of the piece's slots are done (lgkmcnt
+      // only: its weight-image loads in flight and the previous epilogue's
+      // MMB2 stores do not guard the slots; 22.48 -> 22.45 ms, r02z)
+      fused_signal_lds(consumed);
     }
     if constexpr ((DIAG & 5) != 0) {
 #pragma unroll
@@ -1659,7 +1663,11 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
         for (int t = 0; t < kFTiles; ++t) {
           const int col = 16 * (kFTiles * pw + t) + q;
-          xv[t][jj] = a.num_out[rowc * D + min(col, D - 1)];
+          if constexpr ((DIAG & 128) != 0) {  // timing only: no x re-read
+            xv[t][jj] = static_cast<float>(col);
+          } else {
+            xv[t][jj] = a.num_out[rowc * D + min(col, D - 1)];
+          }
         }
       }
 #pragma unroll
@@ -1679,7 +1687,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         }
       }
     }
-    fused_signal(pbar);
+    fused_signal_lds(pbar);  // the row totals exchanged through LDS only
     fused_wait(pbar, 4 * ++ep, abort_flag, a.flag);
 #pragma unroll
     for (int rt = 0; rt < kGRT; ++rt) {
@@ -1698,7 +1706,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         if (q == 0) ssq[pw * kGR + r] = ss;
       }
     }
-    fused_signal(pbar);
+    fused_signal_lds(pbar);
     fused_wait(pbar, 4 * ++ep, abort_flag, a.flag);
 #pragma unroll
     for (int rt = 0; rt < kGRT; ++rt) {
@@ -1711,7 +1719,11 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
           for (int t = 0; t < kFTiles; ++t) {
             const int col = 16 * (kFTiles * pw + t) + q;
-            if (col < D) orow[col] = acc[rt][t][jj] * inv;
+            if constexpr ((DIAG & 256) != 0) {  // timing only: no MMB2 stores
+              asm volatile("" ::"v"(acc[rt][t][jj] * inv));
+            } else {
+              if (col < D) orow[col] = acc[rt][t][jj] * inv;
+            }
           }
         }
       }
@@ -1763,9 +1775,15 @@ static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   // and addresses the word table through one buffer descriptor (< 2^31 bytes)
   const bool pipe = fused_pipe() != 0 && (f.s.L + un - 1) / un >= 3 &&
                     (f.s.ids == nullptr || f.s.V * f.s.D * 4 < (int64_t{1} << 31));
-  if (pipe && un == 8 && fused_pipe() == 2 && (dg == 0 || dg == 1)) {
+  if (pipe && un == 8 && fused_pipe() == 2 && (dg == 0 || dg == 1 || dg == 4 || dg == 128 || dg == 256)) {
     if (dg == 1) {
       launch_fused_v<1, 8, 2>(f, grid, stream);
+    } else if (dg == 4) {
+      launch_fused_v<4, 8, 2>(f, grid, stream);
+    } else if (dg == 128) {
+      launch_fused_v<128, 8, 2>(f, grid, stream);
+    } else if (dg == 256) {
+      launch_fused_v<256, 8, 2>(f, grid, stream);
     } else {
       launch_fused_v<0, 8, 2>(f, grid, stream);
     }
