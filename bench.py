@@ -8,21 +8,39 @@ ids): for every utterance both its SIF text embedding (weighted average +
 first-PC removal, a1-a5) and its closed-form MMB2 embedding (a6-a8) are
 produced in device memory.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--utts-per-gpu U]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+                    [--utts U] [--dist-backend nccl|gloo] [--share-device]
 
-N > 1 runs one process per GPU with RCCL: each rank owns its own U utterances
-(weak scaling: fixed work per GPU) and the ranks all-reduce the 300x300 fp64
-Gram once per step -- the only collective on the path.  Launched without a
-torchrun environment (no WORLD_SIZE), `--gpus N` starts the N ranks itself
+Scaling (configs[3]: "1M utterances ... utterance-sharded across 8 x MI355X
+... 1/2/4/8-GPU scaling curve"): STRONG by default -- one 1M-utterance split,
+rank r owns the contiguous rows distributed.shard_range(1M, N, r) (1M / N
+each), generated identically for every N (synth.device_shard: the same word
+table on every rank, the utterances from seeded 62.5k-row blocks), so the N
+lines of the curve process the same split.  `--scaling weak` (or
+--utts-per-gpu) gives every rank its own U rows instead.  The ranks all-reduce
+the 300x300 fp64 Gram once per step -- the only collective on the path --
+and every rank runs the identical PC solve.  `value` = utterances of the
+whole split / the slowest rank's time.
+
+N > 1 runs one process per GPU over RCCL.  Launched without a torchrun
+environment (no WORLD_SIZE), `--gpus N` starts the N ranks itself
 (torch.distributed.run as a child process, before anything touches the GPU)
-and exits with its status.  Rank 0 prints ONE JSON line.
+and exits with its status.  `--dist-backend gloo --share-device` runs the
+same multi-rank branch with every rank on GPU 0 and the collectives on gloo
+(the one-GPU test of this branch, tests/test_gpu_bench_dist.py; with
+`--dump-rows DIR` each rank saves its PC and a sample of its rows).  Rank 0
+prints ONE JSON line.
 
-At N = 1 the line also carries `configs_measured` -- the other BASELINE
-configs measured in the same run: the ragged configs[3] variant (Poisson(40)
-lengths in [1, 64]), configs[2] (POM transcript length 1357),
-configs[4] (the regressor's 400-epoch SGD loop at MOSI size) -- plus the
-fp32-MFMA projection timed beside the bench path's fp16x3 one, and the CPU
-baselines.  `--only-main` skips them (profiling passes).
+At N = 1 the line also carries `per_rank_steps` -- the step at the per-rank
+sizes of the 2/4/8-GPU strong-scaling runs (500k / 250k / 125k rows of the
+same split) -- and `configs_measured`, the other BASELINE configs measured in
+the same run: configs[0] (MMB1 text SIF at MOSI shape, GPU and the reference
+CPU path), configs[1] (MMB2 at MOSI shape), the ragged configs[3] variant
+(Poisson(40) lengths in [1, 64]), configs[2] (POM transcript
+length 1357), configs[4] (the regressor's 400-epoch SGD loop at MOSI size)
+and the e2e latent step -- plus the fp32-MFMA projection
+timed beside the bench path's fp16x3 one, and the CPU baselines.
+`--only-main` skips them (profiling passes).
 """
 from __future__ import annotations
 
@@ -585,6 +603,199 @@ def launch_check():
         dist.destroy_process_group()
 
 
+def per_rank_steps(P, inp, gen, steps, warmup, sizes):
+    """The step on the first U rows of the split, for U = the per-rank sizes
+    of the strong-scaling curve (1M / N): the curve each rank follows, minus
+    the all-reduce (720 KB over xGMI) and the rank skew, which one GPU cannot
+    show."""
+    import torch
+
+    out = {}
+    for u in sizes:
+        sl = {k: (v[:u] if k in ("ids", "audio", "visual") else v) for k, v in inp.items()}
+        step, elapsed, traces = run_workload(P, sl, gen, steps, warmup)
+        ph = phase_times(traces, steps)
+        out[str(u)] = {"utts": u, "ms_per_step": round(elapsed * 1e3 / steps, 4),
+                       "value": round(u * steps / elapsed, 1),
+                       "phase_ms": {k: round(v, 4) for k, v in ph.items()}}
+        del step
+        torch.cuda.empty_cache()
+    return out
+
+
+def mosi_mmb2_config(P, models, synth, dev, steps, warmup, U=1_000_000):
+    """configs[1]: MMB2 at MOSI shape -- T = 20 aligned frames, COVAREP 74 + 2
+    positional dims = 76, FACET 46 + 2 = 48 (make_configs.py:28),
+    V = 3016 (sif_functions.py:48) -- on 1M synthetic utterances, the fused
+    step (SIF + MMB2).  The 3.6 MB word table sits in L2 / Infinity Cache, so
+    the roofline is given on algorithmic bytes (text rows counted) and on the
+    bytes that must come from HBM (text rows excluded)."""
+    import torch
+
+    T, V, D, A, Vd = 20, 3016, 300, 76, 48
+    inp = synth.device_workload(U, T, V, D=D, A=A, Vd=Vd, seed=4000, device=dev)
+    torch.manual_seed(0)
+    g = models.AudioVisualGeneratorMultimodal(D, A, Vd, norm=None).to(dev)
+    step, elapsed, traces = run_workload(P, inp, g, steps, warmup)
+    ph = phase_times(traces, steps)
+    kb, kname = dominant_kernel(step, T, D)
+    roof = stream_roofline(ph, traces, steps, kb, U, kname + f", T = {T}, A = {A}, Vd = {Vd}",
+                           "mosi", T)
+    hbm_b = kb - 4 * D * T
+    roof["hbm_bytes_per_utt_excl_table"] = hbm_b
+    roof["hbm_frac_excl_table"] = round(hbm_b * U / (roof["avg_launch_ms"] / 1e3) / 1e9
+                                        / HBM_PEAK_GBS, 4)
+    out = {"workload": f"configs[1] MOSI-shaped: T = {T}, A = {A} (COVAREP 74 + 2 pos), Vd = {Vd} "
+                       f"(FACET 46 + 2 pos), V = {V}, Zipf(1.1) ids, U(-1, 1) frames, SIF(+PC "
+                       "removal) + closed-form MMB2",
+           "utts": U, "value": round(U * steps / elapsed, 1), "unit": "utterance-embeds/s",
+           "ms_per_step": round(elapsed * 1e3 / steps, 4), "roofline": roof,
+           "phase_ms": {k: round(v, 4) for k, v in ph.items()}}
+    n_cpu = 20_000
+    sample = host_sample(inp, n_cpu)
+    gen_cpu = models.AudioVisualGeneratorMultimodal(D, A, Vd, norm=None)
+    gen_cpu.load_state_dict({k: v.cpu() for k, v in g.state_dict().items()})
+    del step, inp
+    torch.cuda.empty_cache()
+    try:
+        out["cpu_baseline"] = cpu_baseline(sample, gen_cpu, n_cpu)
+    except Exception as exc:  # keep the GPU numbers if the host leg fails
+        out["cpu_baseline"] = {"error": repr(exc)}
+    return out
+
+
+def mmb1_sif_mosi_config(dev, reps=50):
+    """configs[0]: MMB1 text-only SIF (--unimodal) at MOSI shape -- N = 2199
+    utterances (1284 + 229 + 686, one split-sized batch), L = 20, V = 3016 --
+    a1-a5 on the GPU (pipeline.sif_embeddings: device-resident inputs, one
+    launch chain + the flag check's sync) against the reference's CPU path
+    restated in oracle/ (its seq2weight / get_weighted_average row loops and
+    sklearn's TruncatedSVD, sif.py:84-94 -> sif_functions.py:8-96) on the
+    host cores, same inputs, results compared."""
+    import numpy as np
+    import torch
+
+    import pipeline as P
+    import synth
+    from oracle import mmb2_oracle as M
+    from oracle import sif_oracle as O
+
+    N, L, V = 2199, 20, 3016
+    E = synth.word_table(V, 300, seed=21)
+    wt = synth.sif_weights(V, w0=0.0)
+    ids = synth.token_ids(N, L, V, seed=22, ragged=True)
+    table = torch.tensor(E, device=dev)
+    wt32 = torch.tensor(wt, device=dev, dtype=torch.float32)
+    ids32 = torch.as_tensor(ids, dtype=torch.int32, device=dev)
+    out, _ = P.sif_embeddings(table, ids32, wtab32=wt32)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out, _ = P.sif_embeddings(table, ids32, wtab32=wt32)
+    torch.cuda.synchronize()
+    gpu_s = (time.perf_counter() - t0) / reps
+    cores, aff = host_threads()
+    with cpu_threads(cores):
+        t0 = time.perf_counter()
+        ref = O.get_sentence_embeddings(E, wt, ids)
+        cpu_s = time.perf_counter() - t0
+    err = M.row_rel_err(out.cpu().numpy(), ref)
+    return {"workload": f"configs[0] MMB1 text SIF at MOSI shape: N = {N}, L = {L}, V = {V}, "
+                        "ragged ids (id-0 pads, w0 = 0)",
+            "gpu": {"ms_per_call": round(gpu_s * 1e3, 4), "value": round(N / gpu_s, 1),
+                    "unit": "utterance-embeds/s",
+                    "note": "pipeline.sif_embeddings on device-resident inputs (a1-a5, PC over "
+                            "the batch), incl. the flag / finite-PC check's host sync"},
+            "cpu_baseline": {"ms_per_call": round(cpu_s * 1e3, 3), "value": round(N / cpu_s, 1),
+                             "cores": cores, "kind": "port",
+                             "sample": "the whole batch through oracle/sif_oracle."
+                                       "get_sentence_embeddings (the reference's loops + sklearn "
+                                       "TruncatedSVD)"},
+            "row_rel_err_vs_cpu": err, "speedup_vs_cpu": round(cpu_s / gpu_s, 1)}
+
+
+def latent_step_config(dev, steps=50, cpu_steps=3):
+    """one e2e latent-optimisation step at MOSI shape
+    (batch 64, V = 3016, T = 20; simplesif.py:712-790: generator forward, word
+    + Gaussian objective, regressor, backward, SGD) -- the CLI's default (HIP
+    graph of the step's device work, tools/latent_bench.py), the same kernels
+    launched eagerly, the reference's torch arithmetic on the GPU and on the
+    host cores -- plus word_zsum_kernel (the [B, V] cosine / acos objective
+    on fp32 MFMA, losses.py:68-95) timed alone with HIP events."""
+    import copy
+
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import latent as LT
+    import latent_bench as LB
+
+    class A:
+        n, t, vocab, a, vd, batch = 1284, 20, 3016, 75, 46, 64
+
+    args = A()
+    cfg, obj, gen, senti, lat0, label, data = LB.build(args, dev)
+    ms_graph = LB.run(cfg, None, copy.deepcopy(gen), copy.deepcopy(senti), lat0, label, dev,
+                      steps, args.batch, graph_obj=obj)
+    ms_eager = LB.run(cfg, obj.log_prob, copy.deepcopy(gen), copy.deepcopy(senti), lat0, label,
+                      dev, steps, args.batch)
+    ms_torch = LB.run(cfg, LB.eager_objective(cfg, data, dev), copy.deepcopy(gen).float(),
+                      copy.deepcopy(senti), lat0, label, dev, steps, args.batch)
+    # the word objective's forward kernel alone: B = 64 latents x V = 3016 words
+    lat = (torch.randn(args.batch, 300, device=dev) * 0.5)
+    j = torch.arange(args.batch, device=dev)
+    wfn = lambda: LT.word_log_prob(lat, obj.table, obj.w[j], obj.m[j], 1e-3, ids=obj.ids[j])
+    wfn()
+    evs = []
+    for _ in range(20):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        wfn()
+        b.record()
+        evs.append((a, b))
+    torch.cuda.synchronize()
+    w_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    flop = 2 * args.batch * args.vocab * 304 * 2  # C = Wn U^T and G += R Wn (K = 304)
+    tf = flop / (w_ms / 1e3) / 1e12
+    cores, aff = host_threads()
+    with cpu_threads(cores):
+        cpu = torch.device("cpu")
+        ms_cpu = LB.run(cfg, LB.eager_objective(cfg, data, cpu), copy.deepcopy(gen).cpu(),
+                        LB.CpuSenti(senti), lat0, label, cpu, cpu_steps, args.batch, warm=1)
+    return {"workload": "e2e latent step at MOSI shape: batch 64, V = 3016, T = 20, audio 75+2, "
+                        "visual 46+2 (simplesif.py:712-790)",
+            "ms_per_step": {"libmmb_graph": round(ms_graph, 4),
+                            "libmmb_eager_launches": round(ms_eager, 4),
+                            "torch_reference_arith_gpu": round(ms_torch, 4),
+                            "reference_arith_cpu": round(ms_cpu, 2)},
+            "word_forward": {"kernel": "word_zsum_kernel + word_finish_kernel "
+                                       "(mmb_word_logprob_fwd: fp32 MFMA 16x16x4)",
+                             "ms": round(w_ms, 5), "flop": flop, "achieved": round(tf, 3),
+                             "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                             "frac": round(tf / F32_MFMA_PEAK_TFS, 5),
+                             "bound": "latency: 0.24 GFLOP over 4 x 189 workgroups, a few us"},
+            "cpu_baseline": {"ms_per_step": round(ms_cpu, 2), "cores": cores, "kind": "port",
+                             "sample": f"{cpu_steps} steps of the reference's torch arithmetic "
+                                       "(oracle/latent_oracle) on the host"},
+            "speedup_vs_torch_gpu": round(ms_torch / ms_graph, 2),
+            "speedup_vs_cpu": round(ms_cpu / ms_graph, 1)}
+
+
+def dump_rows(path, rank, row0, step):
+    """--dump-rows: this rank's PC and every 97th of its SIF / MMB2 rows (plus
+    its last), for tests/test_gpu_bench_dist.py to compare with the unsharded
+    step."""
+    import numpy as np
+    import torch
+
+    os.makedirs(path, exist_ok=True)
+    n = step.n
+    idx = torch.tensor(sorted(set(range(0, n, 97)) | {n - 1}), device=step.sif.device)
+    np.savez(os.path.join(path, f"rank{rank}.npz"), row0=row0, n=n, pc=step.pc.cpu().numpy(),
+             idx=idx.cpu().numpy(), sif=step.sif[idx].cpu().numpy(),
+             mmb2=step.mmb2[idx].cpu().numpy(), flag=int(step.flag.item()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -594,9 +805,23 @@ def main():
                     help="synthetic: BASELINE configs[3] (the metric's workload); pom: configs[2] "
                          "shape (V=7763, transcripts padded to 1357, ~370 tokens); ragged: "
                          "configs[3] with Poisson(40) lengths in [1, 64]")
-    ap.add_argument("--utts-per-gpu", type=int, default=None)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                    help="strong (default): one split of --utts utterances sharded over the "
+                         "ranks; weak: --utts (or --utts-per-gpu) utterances per rank")
+    ap.add_argument("--utts", type=int, default=None,
+                    help="utterances of the split (strong) or per rank (weak); default 1M "
+                         "(POM: 10k)")
+    ap.add_argument("--utts-per-gpu", type=int, default=None,
+                    help="utterances per rank; implies --scaling weak (at N = 1 the same as --utts)")
     ap.add_argument("--tokens", type=int, default=None)
     ap.add_argument("--vocab", type=int, default=None)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI (the product); gloo: the collectives on the host "
+                         "(with --share-device: the multi-rank branch on one GPU)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="every rank on GPU 0 (tests of the N > 1 branch on a one-GPU box)")
+    ap.add_argument("--dump-rows", default=None,
+                    help="directory: each rank saves its PC and a sample of its rows")
     ap.add_argument("--chunks", type=int, default=None,
                     help="row chunks per step (stream of chunk c+1 overlaps projection of c); "
                          "default 1")
@@ -606,14 +831,14 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--only-main", action="store_true",
-                    help="skip configs_measured (the other BASELINE configs) and the fp32 "
-                         "projection timing")
+                    help="skip per_rank_steps, configs_measured (the other BASELINE configs) and "
+                         "the fp32 projection timing")
     ap.add_argument("--launch-check", action="store_true",
                     help="only start the ranks and all-reduce a one (tests the launcher)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        if not args.launch_check:
+        if not args.launch_check and not args.share_device:
             import torch  # device_count() does not initialise the GPU
 
             have = torch.cuda.device_count()
@@ -629,20 +854,24 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         ranks_seen = dist.get_world_size()
         one = torch.ones(1, device=dev)
-        dist.all_reduce(one)  # every rank is live on RCCL before the timed steps
+        dist.all_reduce(one)  # every rank is live on the backend before the timed steps
         assert int(one.item()) == ranks_seen == world
     else:
         ranks_seen = 1
 
+    import distributed as Dist
     import mmb_lib
     import models
     import pipeline as P
@@ -652,14 +881,23 @@ def main():
     kind = args.workload
     dflt = {"synthetic": (1_000_000, 40, 400_000), "pom": (10_000, 1357, 7763),
             "ragged": (1_000_000, 64, 400_000)}[kind]
-    U = args.utts_per_gpu or dflt[0]
+    scaling = args.scaling or ("weak" if args.utts_per_gpu else "strong")
     T = args.tokens or dflt[1]
     V = args.vocab or dflt[2]
     D = 300
-    inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev,
-                                mean_len=370.0 if kind == "pom" else None,
-                                poisson_len=40.0 if kind == "ragged" else None)
-    inp.pop("lengths", None)
+    if scaling == "strong":
+        U_total = args.utts or args.utts_per_gpu or dflt[0]
+        row0, U = Dist.shard_range(U_total, world, rank)
+    else:
+        U = args.utts_per_gpu or args.utts or dflt[0]
+        U_total, row0 = U * world, U * rank
+    if kind == "synthetic":
+        inp = synth.device_shard(row0, U, T, V, D=D, A=300, Vd=300, seed=1000, device=dev)
+    else:  # N = 1 configs (their own generators: ragged lengths, POM transcripts)
+        inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev,
+                                    mean_len=370.0 if kind == "pom" else None,
+                                    poisson_len=40.0 if kind == "ragged" else None)
+        inp.pop("lengths", None)
     ids = inp["ids"]
     text_rows = None
     if kind != "synthetic":
@@ -670,9 +908,9 @@ def main():
     def allreduce(t):
         dist.all_reduce(t)
 
-    assert U * world >= D  # sklearn's direct (non-transposed) randomized-SVD branch
+    assert U_total >= D  # sklearn's direct (non-transposed) randomized-SVD branch
     step = P.FusedStep(inp, gen.networks(), allreduce=allreduce if world > 1 else None,
-                       n_total=U * world, row0=rank * U, chunks=args.chunks,
+                       n_total=U_total, row0=row0, chunks=args.chunks,
                        side_cus=args.side_cus, side_layout=args.side_layout)
     torch.cuda.synchronize()
     for _ in range(args.warmup):
@@ -696,11 +934,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    step.check()  # ids in range, no all-zero-weight utterance, finite PC
+    step.check()  # ids in range, no all-zero-weight utterance, finite PC (every rank)
+    if args.dump_rows:
+        dump_rows(args.dump_rows, rank, row0, step)
 
     phase_ms = phase_times(traces, args.steps)
     ms_per_step = elapsed * 1e3 / args.steps
-    value = U * world * args.steps / elapsed
+    value = U_total * args.steps / elapsed
     if rank != 0:
         dist.destroy_process_group()
         return 0
@@ -726,14 +966,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": DTYPE,
         "data": "synthetic (seeded, generated in HBM; no dataset or checkpoint)",
-        "config": {"workload": wl, "utts_per_gpu": U, "tokens": T, "vocab": V,
-                   "dims": [D, 300, 300],
-                   "parallelism": f"dp{world} (utterance shards) + RCCL all-reduce of the "
-                                  f"300x300 fp64 Gram"},
+        "config": {"workload": wl, "utts_total": U_total, "utts_rank0": U, "tokens": T,
+                   "vocab": V, "dims": [D, 300, 300],
+                   "parallelism": f"dp{world} (contiguous utterance shards of one split, "
+                                  f"{scaling} scaling) + one all-reduce of the 300x300 fp64 Gram "
+                                  f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
+                                  + (", all ranks on GPU 0" if args.share_device else "")},
         "roofline": roof,
         "path_roofline": {"bytes_per_utt": round(pb, 1),
                           "achieved": round(pb * U / (ms_per_step / 1e3) / 1e9, 1),
@@ -752,9 +994,25 @@ def main():
                                      "ms": round(phase_ms["pc_remove"], 4)}
     if world > 1:
         out["phase_ms"].setdefault("allreduce", None)
+    if args.dump_rows:
+        out["dump_rows"] = args.dump_rows
     cpu = None
     extras = world == 1 and not args.only_main and kind == "synthetic"
     if extras:
+        sizes = [u for u in (500_000, 250_000, 125_000) if u < U]
+        prs = per_rank_steps(P, inp, gen, args.steps, args.warmup, sizes)
+        prs[str(U)] = {"utts": U, "ms_per_step": round(ms_per_step, 4), "value": round(value, 1),
+                       "phase_ms": out["phase_ms"]}
+        out["per_rank_steps"] = prs
+        proj = {}
+        for n_r in (2, 4, 8):
+            key = str(U // n_r)
+            if key in prs:
+                proj[str(n_r)] = round(ms_per_step / prs[key]["ms_per_step"], 3)
+        out["strong_scaling_projection"] = {
+            "speedup": proj, "note": "t(1M) / t(1M / N) on one GPU: the per-rank step of the "
+                                     "N-GPU strong-scaling run without the Gram all-reduce "
+                                     "and the rank skew"}
         if step.stream_project:
             out["step_two_kernels"] = two_kernel_step(P, step, gen)
         out["projection_fp32_mfma"] = time_fp32_projection(P, step)
@@ -769,9 +1027,12 @@ def main():
     torch.cuda.empty_cache()
     if extras:
         cm = {}
-        for name, fn in (("ragged", lambda: ragged_config(P, models, synth, dev, 5, 2, U)),
+        for name, fn in (("mmb1_sif_mosi", lambda: mmb1_sif_mosi_config(dev)),
+                         ("mosi_mmb2", lambda: mosi_mmb2_config(P, models, synth, dev, 5, 2)),
+                         ("ragged", lambda: ragged_config(P, models, synth, dev, 5, 2, U)),
                          ("pom", lambda: pom_config(P, models, synth, dev, 5, 2)),
-                         ("regressor", lambda: regressor_config(dev))):
+                         ("regressor", lambda: regressor_config(dev)),
+                         ("latent_step", lambda: latent_step_config(dev))):
             try:
                 cm[name] = fn()
             except Exception as exc:  # keep the headline line even if an extra leg fails

@@ -121,6 +121,20 @@ int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d, const dou
 int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n_iter,
                  int transposed, double* pc_out, hipStream_t stream);
 
+/* The same solve on ceil(d/16) workgroups (d <= 320, k <= 16): each keeps
+ * 16 rows of G in registers, the tiles of every power-iteration product are
+ * exchanged in-launch (write-through stores + an arrival counter), and every
+ * workgroup runs the identical CholeskyQR; workgroup 0 runs the final
+ * Rayleigh-Ritz step.  ws: mmb_pc_solve_mc_ws_bytes(d) bytes, 16-byte
+ * aligned, owned by the call until it completes (its first 16 bytes are
+ * zeroed by a memset the call enqueues).  A workgroup that waits ~1 s for the
+ * others gives up and sets MMB_FLAG_SYNC_TIMEOUT in *flag (nullable); pc_out
+ * is then invalid.
+ * replaces: sif_functions.compute_pc /root/reference/sif_functions.py:58-67 */
+size_t mmb_pc_solve_mc_ws_bytes(int d);
+int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
+                    int transposed, double* pc_out, void* ws, int32_t* flag, hipStream_t stream);
+
 /* ---------------------------------------------------------------- a4
  * out[i] = x_i - sum_c (x_i . pc_c) pc_c   in float64, x_i = num[i]/cnt[i]
  * (cnt nullable).  Exactly one of out32 / out64 non-null.

@@ -518,12 +518,16 @@ static int launch_train(const MlpArgs& a, size_t lds, hipStream_t stream) {
   return MMB_OK;
 }
 
-// W1 tiles in registers (8 waves, <= 5 tiles each) where they fit; 0 keeps
-// the L2-tile kernel (MMB_MLP_REG, read per launch)
+// W1 tiles in registers (8 waves, <= 5 tiles each) where they fit, else the
+// L2-tile kernel (the tools build's MMB_MLP_REG=0 forces the latter)
 constexpr int kRegWaves = 8, kRegTiles = 5;
 static int mlp_reg() {
+#ifdef MMB_DIAG
   const char* e = getenv("MMB_MLP_REG");
   return e ? atoi(e) : 1;
+#else
+  return 1;
+#endif
 }
 
 }  // namespace mmb
@@ -612,7 +616,17 @@ extern "C" int mmb_mlp_backward(const float* x, const float* hid, int64_t b, int
                                 float* dx, float* dw1, float* db1, float* dw2, float* db2,
                                 hipStream_t stream) {
   MMB_REQUIRE(x && hid && w1 && w2 && dy && dh_ws && b >= 0 && d > 0 && h > 0 && o > 0);
-  if (b == 0) return MMB_OK;
+  if (b == 0) {  // an empty batch: zero gradients (the sums over no rows)
+    const size_t nbytes[4] = {sizeof(float) * h * d, sizeof(float) * h, sizeof(float) * o * h,
+                              sizeof(float) * o};
+    float* outs[4] = {dw1, db1, dw2, db2};
+    for (int q = 0; q < 4; ++q) {
+      if (!outs[q]) continue;
+      const hipError_t e = hipMemsetAsync(outs[q], 0, nbytes[q], stream);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return MMB_OK;
+  }
   const size_t lds = sizeof(float) * kMlpRows * h;
   MMB_REQUIRE(lds <= 64 * 1024);
   mlp_bwd_rows_kernel<<<static_cast<int>(ceil_div(b, kMlpRows)), 256, lds, stream>>>(

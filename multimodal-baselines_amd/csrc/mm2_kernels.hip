@@ -1554,13 +1554,11 @@ constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(
 // 24 fragment reads per chunk), 2 = the 16x16x32 kernel with the
 // software-pipelined K loop.  MMB_PROJ_VARIANT overrides (read once).
 // Row-wise projection epilogue (1, default) or the MFMA-tile-layout one (0);
-// MMB_PROJ_ROWEPI overrides (read once).
-static bool proj_row_epilogue() {
-  static const bool v = [] {
-    const char* e = getenv("MMB_PROJ_ROWEPI");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
+// MMB_PROJ_ROWEPI overrides (tools build, read per launch).
+#ifdef MMB_DIAG
+static bool proj_row_epilogue() {  // re-read per launch (in-process A/B)
+  const char* e = getenv("MMB_PROJ_ROWEPI");
+  return e ? atoi(e) != 0 : true;
 }
 
 static int proj_diag() {  // re-read per launch: timing sweeps flip it in one process
@@ -1572,7 +1570,14 @@ static int proj_variant() {  // re-read per launch (in-process A/B sweeps)
   const char* e = getenv("MMB_PROJ_VARIANT");
   return e ? atoi(e) : 2;
 }
+#else
+// the product library: variant 2 with the row-wise epilogue, no knobs
+constexpr bool proj_row_epilogue() { return true; }
+constexpr int proj_diag() { return 0; }
+constexpr int proj_variant() { return 2; }
+#endif
 
+#ifdef MMB_DIAG
 template <int CT, int D_>
 static void launch_diag1(int grid, size_t ldsb, const _Float16* s, const float* num, const float* aux,
                          const _Float16* img, const float* ci, const float* c0, int64_t n, int kp,
@@ -1605,6 +1610,46 @@ static void launch_diag(int v, int grid, size_t ldsb, const _Float16* s, const f
 #undef MMB_DIAG_CASE
 }
 
+#endif
+
+#ifndef MMB_DIAG
+// The product dispatch: the 16x16x32 kernel with the software-pipelined K
+// loop (variant 2), row-wise epilogue where the shape allows it.
+template <int CT>
+static int launch_project_x3(const _Float16* s, const float* num, const float* aux,
+                             const _Float16* img, const float* ci, const float* c0, int64_t n,
+                             int kp, int d, float* out, const double* pc, float* sif,
+                             hipStream_t stream) {
+  const int grid = static_cast<int>(ceil_div(n, kXM));
+  constexpr size_t ldsb = x3b_lds_bytes<CT>();
+  static_assert(ldsb <= 160 * 1024, "x3b chunk rings exceed LDS");
+  static bool attr_b = false;
+  if (!attr_b) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, false, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+    if constexpr (CT == 5)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+    attr_b = true;
+  }
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  // the row-wise epilogue: D in [256, 320) (column D in a lane's second
+  // unit), whole float4 units, 16-byte aligned rows
+  const bool rowepi = d >= 256 && d % 4 == 0 && a16(num) && a16(out) && (sif == nullptr || a16(sif));
+  if constexpr (CT == 5) {
+    if (rowepi) {
+      mm2_project_x3b_kernel<CT, true, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
+                                                                          n, kp, d, out, pc, sif);
+      MMB_LAUNCH_CHECK();
+      return MMB_OK;
+    }
+  }
+  mm2_project_x3b_kernel<CT, false, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
+                                                                       n, kp, d, out, pc, sif);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+#else
 template <int CT>
 static int launch_project_x3(const _Float16* s, const float* num, const float* aux,
                              const _Float16* img, const float* ci, const float* c0, int64_t n,
@@ -1736,6 +1781,8 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
+
+#endif
 
 template <int CT>
 static int launch_project(const float* s, const float* num, const float* aux, const float* wm,

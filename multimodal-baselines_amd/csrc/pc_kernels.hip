@@ -500,26 +500,32 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
     if (q < ntl) {
       const int fj = tj[q] * 16 + lc;
       const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
+      const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int fi = ti[q] * 16 + lr + e;
         const int ei = fi < D ? gi_exp(colmax[fi]) : 0;
-        pr[static_cast<int64_t>(q0 + q) * 256 + (lr + e) * 16 + lc] = ldexp(acc[q][e], ei + ej);
+        // a non-finite column bound (NaN / inf in x) makes its Gram rows and
+        // columns NaN, as the f64 Gram of such rows would be
+        const bool bad = (fi < D && !isfinite(__uint_as_float(colmax[fi]))) || !okj;
+        pr[static_cast<int64_t>(q0 + q) * 256 + (lr + e) * 16 + lc] =
+            bad ? __builtin_nan("") : ldexp(acc[q][e], ei + ej);
       }
     }
   }
 }
 
 // colmax[j] = max_i |x[i, j]| as float bits (atomicMax on the bits of a
-// non-negative float orders like the float); NaNs are skipped.
+// non-negative float orders like the float); a NaN bound wins (non-finite x
+// then reaches G through mmb_gram_i8).
 __global__ void colmax_kernel(const float* __restrict__ x, int64_t N, int D, int64_t rows_per_block,
                               unsigned* __restrict__ colmax) {
   const int64_t r0 = blockIdx.x * rows_per_block;
   const int64_t r1 = min(N, r0 + rows_per_block);
   for (int j = threadIdx.x; j < D; j += blockDim.x) {
-    float m = 0.f;
-    for (int64_t r = r0; r < r1; ++r) m = fmaxf(m, fabsf(x[r * D + j]));
-    if (m > 0.f) atomicMax(colmax + j, __float_as_uint(m));
+    unsigned m = 0u;  // bits of max |x|: NaN (0x7fc00000..) ranks above inf, so it propagates
+    for (int64_t r = r0; r < r1; ++r) m = max(m, __float_as_uint(fabsf(x[r * D + j])));
+    if (m > 0u) atomicMax(colmax + j, m);
   }
 }
 
@@ -528,34 +534,60 @@ __global__ void colmax_kernel(const float* __restrict__ x, int64_t N, int D, int
 // the former element-of-G order read the lower half transposed, 8x the bytes),
 // written to G[p][q] and mirrored to G[q][p] for off-diagonal tiles (diagonal
 // tiles hold both halves themselves).  Same sums in the same order as before.
-__global__ void gram_tri_reduce_kernel(const double* __restrict__ part, int D, int nt, int R,
-                                       int accumulate, double* __restrict__ g) {
+// r03: 8 threads per element (thread group u sums the ranges r = u (mod 8) in
+// increasing r, all of its <= 16 loads in flight at once; the 8 sums are
+// combined in LDS) -- the same eight partial sums and the same combine order
+// as the one-thread-per-element kernel, so G is bit-identical, but 8x the
+// loads in flight: the reduction of 128 ranges (49.8 MB of partials at
+// D = 300) was latency-bound at ~57 us.
+constexpr int kRedEl = 32;      // elements per block
+constexpr int kRedMaxPer = 16;  // ranges per thread (R <= 128)
+__global__ __launch_bounds__(256) void gram_tri_reduce_kernel(const double* __restrict__ part, int D,
+                                                              int nt, int R, int accumulate,
+                                                              double* __restrict__ g) {
+  __shared__ double s_p[8][kRedEl];
   const int T = nt * (nt + 1) / 2;
   const int64_t total = static_cast<int64_t>(T) * 256;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int tau = static_cast<int>(e >> 8), w = static_cast<int>(e & 255);
-    int bi, bj;
-    tri_tile(tau, nt, bi, bj);
-    const int p = 16 * bi + (w >> 4), q = 16 * bj + (w & 15);
-    if (p >= D || q >= D) continue;
-    // eight independent partial sums (eight loads in flight; a single chain
-    // waited on every load), combined in a fixed order: deterministic
-    double s8[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    int r = 0;
-    for (; r + 8 <= R; r += 8) {
+  const int el = threadIdx.x % kRedEl, u = threadIdx.x / kRedEl;
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kRedEl + el;
+  double s = 0.0;
+  if (e < total) {
+    if (R >= 8) {  // R is a multiple of 8 here (gram2_plan / gram_i8_plan)
+      double v[kRedMaxPer];
+      const int per = R / 8;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s8[u] += part[static_cast<int64_t>(r + u) * total + e];
-    }
-    for (; r < R; ++r) s8[0] += part[static_cast<int64_t>(r) * total + e];
-    const double sum = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
-    const int64_t e1 = static_cast<int64_t>(p) * D + q;
-    g[e1] = accumulate ? g[e1] + sum : sum;
-    if (bi != bj) {
-      const int64_t e2 = static_cast<int64_t>(q) * D + p;
-      g[e2] = accumulate ? g[e2] + sum : sum;
+      for (int j = 0; j < kRedMaxPer; ++j)
+        v[j] = j < per ? part[static_cast<int64_t>(u + 8 * j) * total + e] : 0.0;
+#pragma unroll
+      for (int j = 0; j < kRedMaxPer; ++j)
+        if (j < per) s += v[j];
+    } else if (u == 0) {
+      for (int r = 0; r < R; ++r) s += part[static_cast<int64_t>(r) * total + e];
     }
   }
+  s_p[u][el] = s;
+  __syncthreads();
+  if (u != 0 || e >= total) return;
+  const int tau = static_cast<int>(e >> 8), w = static_cast<int>(e & 255);
+  int bi, bj;
+  tri_tile(tau, nt, bi, bj);
+  const int p = 16 * bi + (w >> 4), q = 16 * bj + (w & 15);
+  if (p >= D || q >= D) return;
+  const double sum = ((s_p[0][el] + s_p[1][el]) + (s_p[2][el] + s_p[3][el])) +
+                     ((s_p[4][el] + s_p[5][el]) + (s_p[6][el] + s_p[7][el]));
+  const int64_t e1 = static_cast<int64_t>(p) * D + q;
+  g[e1] = accumulate ? g[e1] + sum : sum;
+  if (bi != bj) {
+    const int64_t e2 = static_cast<int64_t>(q) * D + p;
+    g[e2] = accumulate ? g[e2] + sum : sum;
+  }
+}
+
+static void launch_tri_reduce(const double* part, int d, int nt, int R, int accumulate, double* g,
+                              hipStream_t stream) {
+  const int64_t total = static_cast<int64_t>(nt) * (nt + 1) / 2 * 256;
+  gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, kRedEl)), 256, 0, stream>>>(
+      part, d, nt, R, accumulate, g);
 }
 
 // Fixed-order sum over the S row chunks (deterministic), mirrored to both halves.
@@ -592,10 +624,10 @@ __global__ void xt_omega_kernel(const TX* __restrict__ num, const float* __restr
 // ------------------------------------------------------------------ pc_solve
 #ifdef MMB_PC_PROBE  // phase timestamps for tools/pc_probe.hip (never in libmmb)
 __device__ unsigned long long g_pc_probe[64];
-#define PC_MARK(i)                                      \
-  do {                                                  \
-    __syncthreads();                                    \
-    if (threadIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
+#define PC_MARK(i)                                                         \
+  do {                                                                     \
+    __syncthreads();                                                       \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
   } while (0)
 #else
 #define PC_MARK(i) \
@@ -1260,6 +1292,142 @@ __device__ __forceinline__ void p16_orth(double* Z, int D, int Dp, int k, double
   }
 }
 
+// The k x k scratch of the solve's tail (LDS, one set per workgroup).
+struct P16Small {
+  double *A, *V, *W, *L, *Li, *T, *y, *U;  // [16 x 16] each (y: [16]; U: npc x 16)
+  double *rd, *rv;                         // [16 waves]
+  int *ri, *fail;
+};
+
+// The Rayleigh-Ritz tail of the solve (every thread of a 16-wave workgroup):
+// from the final block Z and its product GZ = G Z (both [Dp][16] in LDS) to
+// the npc components in pc_out -- sklearn's randomized_svd after its range
+// finder: W = Z^T G Z, H = (GZ)^T (GZ), the k x k generalised eigenproblem
+// H y = s^2 W y (Cholesky of W, A = L^-1 H L^-T), v = GZ L^-T u, svd_flip
+// (extmath.py:537-566); the transposed branch takes A = Q^T G Q, v = Q u.
+__device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int D, int Dp, int k,
+                                         int npc, int transposed, double* part, const P16Small& sm,
+                                         double* __restrict__ pc_out) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  if (transposed) {
+    p16_gram(Z, GZ, Dp, k, part, sm.A);  // Q^T G Q
+    symmetrize(sm.A, k);
+    __syncthreads();
+  } else {
+    p16_gram(Z, GZ, Dp, k, part, sm.W);   // W = Z^T G Z
+    p16_gram(GZ, GZ, Dp, k, part, sm.T);  // H = (GZ)^T (GZ)
+    symmetrize(sm.W, k);
+    symmetrize(sm.T, k);
+    __syncthreads();
+    if (wave == 0) {
+      p16_chol(sm.W, sm.L, sm.Li, k, lane, sm.fail);  // a failed pivot is clamped (W is SPD here)
+      for (int e = lane; e < k * k; e += kWave) {  // Linv H
+        const int i = e / k, j = e % k;
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sm.Li[i * k + m] * sm.T[m * k + j];
+        sm.V[e] = s;
+      }
+      wave_lds_sync();
+      for (int e = lane; e < k * k; e += kWave) {  // (Linv H) Linv^T
+        const int i = e / k, j = e % k;
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sm.V[i * k + m] * sm.Li[j * k + m];
+        sm.A[e] = s;
+      }
+      wave_lds_sync();
+      for (int e = lane; e < k * k; e += kWave) {
+        const int i = e / k, j = e % k;
+        if (i < j) {
+          const double m = 0.5 * (sm.A[i * k + j] + sm.A[j * k + i]);
+          sm.A[i * k + j] = m;
+          sm.A[j * k + i] = m;
+        }
+      }
+      wave_lds_sync();
+    }
+    __syncthreads();
+  }
+  PC_MARK(41);
+  if (wave == 0) {  // top npc eigenvectors of A, largest first (deflation)
+    for (int c = 0; c < npc; ++c) {
+      double* u = sm.U + c * kMaxK;
+      const double lam = p16_top_eig(sm.A, k, lane, u);
+      if (c + 1 < npc) {
+        for (int e = lane; e < k * k; e += kWave) sm.A[e] -= lam * u[e / k] * u[e % k];
+        wave_lds_sync();
+      }
+    }
+  }
+  __syncthreads();
+  PC_MARK(42);
+
+  for (int c = 0; c < npc; ++c) {
+    const double* u = sm.U + c * kMaxK;
+    if (!transposed) {
+      if (tid < k) {  // y = Linv^T u
+        double s = 0.0;
+        for (int m = 0; m < k; ++m) s += sm.Li[m * k + tid] * u[m];
+        sm.y[tid] = s;
+      }
+      __syncthreads();
+    }
+    double v = 0.0;
+    if (tid < D) {
+      if (transposed) {
+        for (int j = 0; j < k; ++j) v += Z[tid * kP16W + j] * u[j];
+      } else {
+        for (int j = 0; j < k; ++j) v += GZ[tid * kP16W + j] * sm.y[j];
+      }
+    }
+    // norm and first argmax |v|
+    double nn = wave_sum(v * v);
+    double best = (tid < D) ? fabs(v) : -1.0;
+    int bidx = (tid < D) ? tid : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best, o, kWave);
+      const int oi = __shfl_xor(bidx, o, kWave);
+      if (ob > best || (ob == best && oi < bidx)) {
+        best = ob;
+        bidx = oi;
+      }
+    }
+    if (lane == 0) {
+      sm.rd[wave] = nn;
+      sm.rv[wave] = best;
+      sm.ri[wave] = bidx;
+    }
+    __syncthreads();
+    double tot = 0.0, bb = -1.0;
+    int bi = 0x7fffffff;
+    for (int w = 0; w < kP16NT / kWave; ++w) {
+      tot += sm.rd[w];
+      if (sm.rv[w] > bb || (sm.rv[w] == bb && sm.ri[w] < bi)) {
+        bb = sm.rv[w];
+        bi = sm.ri[w];
+      }
+    }
+    if (tid == bi) part[0] = v;  // sign of the largest-|.| entry (svd_flip)
+    __syncthreads();
+    const double vbest = part[0];
+    const double scale = (vbest < 0.0 ? -1.0 : 1.0) / sqrt(tot);
+    if (tid < D) pc_out[c * D + tid] = v * scale;
+    __syncthreads();
+  }
+  PC_MARK(43);
+}
+
+#define P16_SMALL_DECL                                                                      \
+  __shared__ double sA[kMaxK * kMaxK], sV[kMaxK * kMaxK], sW[kMaxK * kMaxK];                 \
+  __shared__ double sL[kMaxK * kMaxK], sLi[kMaxK * kMaxK], sT[kMaxK * kMaxK];                \
+  __shared__ double sy[kMaxK];                                                               \
+  __shared__ double s_rd[kP16NT / kWave];                                                    \
+  __shared__ double s_rv[kP16NT / kWave];                                                    \
+  __shared__ int s_ri[kP16NT / kWave];                                                       \
+  __shared__ double sU[kMaxK * kMaxK]; /* eigenvectors of A, largest first */               \
+  __shared__ int s_fail;                                                                     \
+  const P16Small sm{sA, sV, sW, sL, sLi, sT, sy, sU, s_rd, s_rv, s_ri, &s_fail};
+
 __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __restrict__ G, int D,
                                                               const double* __restrict__ z0, int k,
                                                               int npc, int n_iter, int transposed,
@@ -1269,15 +1437,8 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
   double* sZ = p16_lds;
   double* sGZ = sZ + Dp * kP16W;
   double* part = sGZ + Dp * kP16W;  // max(16 x 256, Dp x 16): partials / fallback copy
-  __shared__ double sA[kMaxK * kMaxK], sV[kMaxK * kMaxK], sW[kMaxK * kMaxK];
-  __shared__ double sL[kMaxK * kMaxK], sLi[kMaxK * kMaxK], sT[kMaxK * kMaxK];
-  __shared__ double sy[kMaxK];
-  __shared__ double s_rd[kP16NT / kWave];
-  __shared__ double s_rv[kP16NT / kWave];
-  __shared__ int s_ri[kP16NT / kWave];
-  __shared__ double sU[kMaxK * kMaxK];  // eigenvectors of A, largest first
-  __shared__ int s_fail;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  P16_SMALL_DECL
+  const int tid = threadIdx.x;
 
   PC_MARK(0);
   for (int e = tid; e < Dp * kP16W; e += kP16NT) {
@@ -1303,114 +1464,254 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
   p16_gz(G, D, Dp, Z, GZ);
   __syncthreads();
   PC_MARK(40);
+  p16_tail(Z, GZ, D, Dp, k, npc, transposed, part, sm, pc_out);
+}
 
-  if (transposed) {
-    p16_gram(Z, GZ, Dp, k, part, sA);  // Q^T G Q
-    symmetrize(sA, k);
+// ------------------------------------------------------------------ pc_solve, multi-workgroup (r03)
+// The same randomized-SVD replay with the D-long products spread over
+// T = Dp / 16 workgroups (19 at D = 300), one per 16-row tile of G.  The
+// single-workgroup solve spent ~20 us per G Z product (76 dependent MFMA
+// k-steps per tile, two rounds of tiles over 16 waves, G re-read from L2)
+// and ~16 us per orthonormalisation; here each workgroup keeps its 16 rows of
+// G in registers for the whole solve (wave w: k-steps w, w + 16, ..), so a
+// product is <= 5 MFMAs per wave plus a 16-way LDS sum, and the
+// orthonormalisation needs only the block's k x k Gram, which the tiles
+// contribute as partials.  Per power iteration ONE exchange: every workgroup
+// publishes its tile Y_t = G_t Z (16 x 16) and P_t = Y_t^T Y_t with
+// write-through (sc1) stores, drains them and adds one to an arrival counter
+// (agent scope, relaxed); each polls the counter for T (it + 1) arrivals
+// (bounded), acquires, and gathers all tiles with sc1 loads (CDNA guide
+// Guideline 16, R1).  Then EVERY workgroup runs the identical equilibrated
+// CholeskyQR on the identical data (W = sum_t P_t in tile order), so the next
+// block Z is the same in all of them with no second exchange.  After the
+// n_iter-th block, one more exchange gives the final product, and workgroup 0
+// runs the Rayleigh-Ritz tail (p16_tail).  Between products the
+// equilibration scales W itself (W' = d W d) instead of recomputing the Gram
+// of the scaled block; the block entering the tail still gets CholeskyQR2.
+// ws: [2][T][512] doubles of tiles (double-buffered by round parity: a round
+// r + 2 write needs every workgroup past round r + 1's wait, hence done
+// reading round r), then the arrival counter and the abort word (zeroed by
+// the launcher before every launch).
+constexpr int kPmKs = 5;  // k-steps of G per wave: ceil(kP16MaxD / 4 / 16)
+constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
+
+__device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned* abort_w,
+                                        int32_t* flag) {
+  for (int it = 0; it < (1 << 20); ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  // ~0.5-1 s without the other workgroups: give up, release every waiter
+  __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (flag) atomicOr(flag, MMB_FLAG_SYNC_TIMEOUT);
+  return false;
+}
+
+__global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,
+                                                               const double* __restrict__ z0, int k,
+                                                               int npc, int n_iter, int transposed,
+                                                               double* __restrict__ pc_out,
+                                                               double* xbuf, unsigned* ctl,
+                                                               int32_t* flag) {
+  extern __shared__ __attribute__((aligned(16))) double p16_lds[];
+  const int Dp = (D + 15) / 16 * 16;
+  const int T = Dp / 16;
+  double* sZ = p16_lds;
+  double* sY = sZ + Dp * kP16W;
+  double* part = sY + Dp * kP16W;  // max(16 x 256, Dp x 16)
+  P16_SMALL_DECL
+  __shared__ double sYt[256], sPt[256], sd[kMaxK];
+  __shared__ int s_abort;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int t = blockIdx.x;
+  unsigned* ctr = ctl;
+  unsigned* abort_w = ctl + 1;
+
+  // this workgroup's 16 rows of G as MFMA A fragments (G symmetric: row p of
+  // the tile = column p, 16 consecutive doubles per k-row: coalesced)
+  double ga[kPmKs];
+  {
+    const int p = t * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < kPmKs; ++j) {
+      const int q = 4 * (wave + 16 * j) + (lane >> 4);
+      ga[j] = (p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
+    }
+  }
+  for (int e = tid; e < Dp * kP16W; e += kP16NT) {
+    const int p = e / kP16W, j = e % kP16W;
+    sZ[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
+    sY[e] = 0.0;
+  }
+  if (tid == 0) s_abort = 0;
+  __syncthreads();
+  PC_MARK(0);
+  // every workgroup orthonormalises the same start block: identical Z
+  p16_orth(sZ, D, Dp, k, part, sW, sL, sLi, &s_fail, n_iter > 0 ? 2 : 3);
+  PC_MARK(1);
+
+  for (int r = 0; r <= n_iter; ++r) {
+    // Y_t = G_t Z: this wave's k-steps, then a fixed-order sum over the waves
+    f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kPmKs; ++j) {
+      const int q = 4 * (wave + 16 * j) + (lane >> 4);
+      if (4 * (wave + 16 * j) < Dp)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], sZ[q * kP16W + (lane & 15)], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
     __syncthreads();
-  } else {
-    p16_gram(Z, GZ, Dp, k, part, sW);   // W = Z^T G Z
-    p16_gram(GZ, GZ, Dp, k, part, sT);  // H = (GZ)^T (GZ)
-    symmetrize(sW, k);
-    symmetrize(sT, k);
+    if (tid < 256) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < kP16NT / kWave; ++w) s += part[w * 256 + tid];
+      sYt[tid] = s;
+    }
     __syncthreads();
-    if (wave == 0) {
-      p16_chol(sW, sL, sLi, k, lane, &s_fail);  // a failed pivot is clamped (W is SPD here)
-      for (int e = lane; e < k * k; e += kWave) {  // Linv H
-        const int i = e / k, j = e % k;
-        double s = 0.0;
-        for (int m = 0; m < k; ++m) s += sLi[i * k + m] * sT[m * k + j];
-        sV[e] = s;
+    if (wave == 0) {  // P_t = Y_t^T Y_t (16 rows, 4 k-steps)
+      f64x4 pa = {0, 0, 0, 0};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const double y = sYt[(4 * st + (lane >> 4)) * 16 + (lane & 15)];
+        pa = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, pa, 0, 0, 0);
       }
-      wave_lds_sync();
-      for (int e = lane; e < k * k; e += kWave) {  // (Linv H) Linv^T
-        const int i = e / k, j = e % k;
-        double s = 0.0;
-        for (int m = 0; m < k; ++m) s += sV[i * k + m] * sLi[j * k + m];
-        sA[e] = s;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) sPt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = pa[reg];
+    }
+    __syncthreads();
+    // publish: write-through 8-byte stores, every storing wave drains, one arrival
+    double* xb = xbuf + static_cast<int64_t>(r & 1) * T * 512;
+    if (tid < 512) {
+      const double v = tid < 256 ? sYt[tid] : sPt[tid - 256];
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(xb + t * 512 + tid),
+                         __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r == n_iter && t != 0) return;  // the tail runs on workgroup 0 only
+    PC_MARK(2 + 3 * r);
+    if (tid == 0) {
+      if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) s_abort = 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (s_abort) return;
+    PC_MARK(3 + 3 * r);
+    // gather every tile into sY and the partial Grams: all of a thread's
+    // loads (sc1, 8 B: the table's first row) issued before any is used
+    // (a load-then-store loop waited ~1.5 us per load), then W = sum_t P_t
+    // as four strided partial sums combined in a fixed order
+    {
+      const int e = tid & 255, g = tid >> 8;  // element, tile group (tiles g, g + 4, ..)
+      double yv[kPmMaxT / 4], pv[kPmMaxT / 4];
+#pragma unroll
+      for (int u = 0; u < kPmMaxT / 4; ++u) {
+        const int tt = g + 4 * u;
+        unsigned long long* src = reinterpret_cast<unsigned long long*>(xb + tt * 512 + e);
+        yv[u] = tt < T ? __builtin_bit_cast(double, __hip_atomic_load(src, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT))
+                       : 0.0;
+        pv[u] = (tt < T && r < n_iter)
+                    ? __builtin_bit_cast(double, __hip_atomic_load(src + 256, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT))
+                    : 0.0;
       }
-      wave_lds_sync();
-      for (int e = lane; e < k * k; e += kWave) {
-        const int i = e / k, j = e % k;
-        if (i < j) {
-          const double m = 0.5 * (sA[i * k + j] + sA[j * k + i]);
-          sA[i * k + j] = m;
-          sA[j * k + i] = m;
+      double ps = 0.0;
+#pragma unroll
+      for (int u = 0; u < kPmMaxT / 4; ++u) {
+        const int tt = g + 4 * u;
+        if (tt < T) {
+          sY[(tt * 16 + (e >> 4)) * kP16W + (e & 15)] = yv[u];
+          ps += pv[u];
         }
       }
-      wave_lds_sync();
+      part[g * 256 + e] = ps;
     }
     __syncthreads();
-  }
-  PC_MARK(41);
-  if (wave == 0) {  // top npc eigenvectors of A, largest first (deflation)
-    for (int c = 0; c < npc; ++c) {
-      double* u = sU + c * kMaxK;
-      const double lam = p16_top_eig(sA, k, lane, u);
-      if (c + 1 < npc) {
-        for (int e = lane; e < k * k; e += kWave) sA[e] -= lam * u[e / k] * u[e % k];
+    if (r < n_iter && tid < 256) {
+      const double s = (part[tid] + part[256 + tid]) + (part[512 + tid] + part[768 + tid]);
+      const int i = tid >> 4, j = tid & 15;
+      if (i < k && j < k) sW[i * k + j] = s;
+    }
+    __syncthreads();
+    PC_MARK(4 + 3 * r);
+    if (r == n_iter) break;
+    // equilibrated CholeskyQR of the product: d_j = 1 / |y_j|, W' = d W d
+    if (tid < k) sd[tid] = 1.0 / sqrt(sW[tid * k + tid]);
+    __syncthreads();
+    if (tid < k * k) sW[tid] *= sd[tid / k] * sd[tid % k];
+    for (int e = tid; e < D * kP16W; e += kP16NT) {
+      const int j = e % kP16W;
+      if (j < k) sY[e] *= sd[j];
+    }
+    __syncthreads();
+    if (wave == 0) {
+      if (lane == 0) s_fail = 0;
+      wave_lds_sync();
+      p16_chol(sW, sL, sLi, k, lane, &s_fail);
+    }
+    __syncthreads();
+    if (s_fail) {  // extreme ill-conditioning: MGS^2 on wave 0 (the same in every workgroup)
+      if (wave == 0) {
+        for (int e = lane; e < D * k; e += kWave) part[e] = sY[(e / k) * kP16W + e % k];
         wave_lds_sync();
+        orth_wave(part, D, k, lane);
+        for (int e = lane; e < D * k; e += kWave) sY[(e / k) * kP16W + e % k] = part[e];
+      }
+      __syncthreads();
+      for (int e = tid; e < Dp * kP16W; e += kP16NT) sZ[e] = sY[e];
+    } else if (tid < D) {  // row p: z <- y L^{-T}
+      double y[kP16W];
+#pragma unroll
+      for (int m = 0; m < kP16W; ++m) y[m] = sY[tid * kP16W + m];
+      for (int j = 0; j < k; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < kP16W; ++m)
+          if (m <= j) s += y[m] * sLi[j * k + m];
+        sZ[tid * kP16W + j] = s;
       }
     }
-  }
-  __syncthreads();
-  PC_MARK(42);
-
-  for (int c = 0; c < npc; ++c) {
-    const double* u = sU + c * kMaxK;
-    if (!transposed) {
-      if (tid < k) {  // y = Linv^T u
-        double s = 0.0;
-        for (int m = 0; m < k; ++m) s += sLi[m * k + tid] * u[m];
-        sy[tid] = s;
+    __syncthreads();
+    // the block entering the tail: a second CholeskyQR pass (local)
+    if (r == n_iter - 1 && !s_fail) {
+      p16_gram(sZ, sZ, Dp, k, part, sW);
+      if (wave == 0) {
+        if (lane == 0) s_fail = 0;
+        wave_lds_sync();
+        p16_chol(sW, sL, sLi, k, lane, &s_fail);
+      }
+      __syncthreads();
+      if (s_fail) {
+        if (wave == 0) {
+          for (int e = lane; e < D * k; e += kWave) part[e] = sZ[(e / k) * kP16W + e % k];
+          wave_lds_sync();
+          orth_wave(part, D, k, lane);
+          for (int e = lane; e < D * k; e += kWave) sZ[(e / k) * kP16W + e % k] = part[e];
+        }
+      } else if (tid < D) {
+        double z[kP16W];
+#pragma unroll
+        for (int m = 0; m < kP16W; ++m) z[m] = sZ[tid * kP16W + m];
+        for (int j = 0; j < k; ++j) {
+          double s = 0.0;
+#pragma unroll
+          for (int m = 0; m < kP16W; ++m)
+            if (m <= j) s += z[m] * sLi[j * k + m];
+          sZ[tid * kP16W + j] = s;
+        }
       }
       __syncthreads();
     }
-    double v = 0.0;
-    if (tid < D) {
-      if (transposed) {
-        for (int j = 0; j < k; ++j) v += Z[tid * kP16W + j] * u[j];
-      } else {
-        for (int j = 0; j < k; ++j) v += GZ[tid * kP16W + j] * sy[j];
-      }
-    }
-    // norm and first argmax |v|
-    double nn = wave_sum(v * v);
-    double best = (tid < D) ? fabs(v) : -1.0;
-    int bidx = (tid < D) ? tid : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ob = __shfl_xor(best, o, kWave);
-      const int oi = __shfl_xor(bidx, o, kWave);
-      if (ob > best || (ob == best && oi < bidx)) {
-        best = ob;
-        bidx = oi;
-      }
-    }
-    if (lane == 0) {
-      s_rd[wave] = nn;
-      s_rv[wave] = best;
-      s_ri[wave] = bidx;
-    }
-    __syncthreads();
-    double tot = 0.0, bb = -1.0;
-    int bi = 0x7fffffff;
-    double vbest = 0.0;
-    for (int w = 0; w < kP16NT / kWave; ++w) {
-      tot += s_rd[w];
-      if (s_rv[w] > bb || (s_rv[w] == bb && s_ri[w] < bi)) {
-        bb = s_rv[w];
-        bi = s_ri[w];
-      }
-    }
-    if (tid == bi) part[0] = v;  // sign of the largest-|.| entry (svd_flip)
-    __syncthreads();
-    vbest = part[0];
-    const double scale = (vbest < 0.0 ? -1.0 : 1.0) / sqrt(tot);
-    if (tid < D) pc_out[c * D + tid] = v * scale;
-    __syncthreads();
   }
-  PC_MARK(43);
+  // workgroup 0: sY = G Z of the final block
+  PC_MARK(40);
+  p16_tail(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out);
 }
 
 inline size_t p16_lds_bytes(int d) {
@@ -1584,8 +1885,12 @@ __global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict
 // (tools/remove_ab.py, 1M x 300, r02q): R = 0 / 2 / 4 / 8 = 0.529 / 0.455 /
 // 0.435 / 0.444 ms, all bit-identical
 static int remove_rows() {
+#ifdef MMB_DIAG
   const char* e = getenv("MMB_PC_REMOVE_R");
   return e ? atoi(e) : 4;
+#else
+  return 4;
+#endif
 }
 
 template <int VEC, int PER, typename TX = float>
@@ -1691,10 +1996,12 @@ static void launch_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
                                                                         q.chunk, q.xcd, part);
 }
 
+#ifdef MMB_DIAG
 static int gram_i8_diag() {  // timing-only ablations (MMB_GRAM_DIAG), re-read per launch
   const char* e = getenv("MMB_GRAM_DIAG");
   return e ? atoi(e) : 0;
 }
+#endif
 }  // namespace mmb
 
 using namespace mmb;
@@ -1720,7 +2027,7 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
     const size_t lds = gram2_lds();
     gram_tri_kernel<<<2 * q.R, kG2NT, lds, stream>>>(num, cnt, n, d, q.nt, q.R, q.chunk, q.xcd, 0, part);
     MMB_LAUNCH_CHECK();
-    gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, q.nt, q.R, accumulate, g);
+    launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
     MMB_LAUNCH_CHECK();
     return MMB_OK;
   }
@@ -1755,8 +2062,12 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
   MMB_REQUIRE(x && colmax && g && ws && n >= 0 && d > 0 && d <= 304 && d % 4 == 0);
   const Gram2Plan q = gram_i8_plan(n, d);
   MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
+  // the kernel's buffer-descriptor record count and row offsets are 32-bit
+  // byte counts of one range (n above ~229M rows at d = 300: split the call)
+  MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
   // int32 level sums are per 64-row k-step, so any range length is safe
   double* part = static_cast<double*>(ws);
+#ifdef MMB_DIAG
   switch (gram_i8_diag()) {
     case 1: launch_gram_i8<1>(x, colmax, n, d, q, part, stream); break;
     case 2: launch_gram_i8<2>(x, colmax, n, d, q, part, stream); break;
@@ -1767,10 +2078,11 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
     case 7: launch_gram_i8<7>(x, colmax, n, d, q, part, stream); break;
     default: launch_gram_i8<0>(x, colmax, n, d, q, part, stream); break;
   }
+#else
+  launch_gram_i8<0>(x, colmax, n, d, q, part, stream);
+#endif
   MMB_LAUNCH_CHECK();
-  const int64_t total = static_cast<int64_t>(d) * d;
-  gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(part, d, q.nt, q.R,
-                                                                                   accumulate, g);
+  launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1790,9 +2102,7 @@ extern "C" int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate,
                                hipStream_t stream) {
   MMB_REQUIRE(g && ws && n_plan >= 0 && d > 0 && d % 4 == 0 && d <= 320);
   const Gram2Plan q = gram2_plan(n_plan, d);
-  const int64_t total = static_cast<int64_t>(d) * d;
-  gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, 256)), 256, 0, stream>>>(
-      static_cast<const double*>(ws), d, q.nt, q.R, accumulate, g);
+  launch_tri_reduce(static_cast<const double*>(ws), d, q.nt, q.R, accumulate, g, stream);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1826,6 +2136,35 @@ extern "C" int mmb_pc_solve(const double* g, int d, const double* z0, int k, int
   return MMB_OK;
 }
 
+extern "C" size_t mmb_pc_solve_mc_ws_bytes(int d) {
+  const int T = (d > 0 ? d : 0) / 16 + 1;
+  return 16 + static_cast<size_t>(2) * T * 512 * sizeof(double);  // control words | tiles
+}
+
+extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
+                               int transposed, double* pc_out, void* ws, int32_t* flag,
+                               hipStream_t stream) {
+  MMB_REQUIRE(g && z0 && pc_out && ws && d > 1 && d <= kP16MaxD && k >= 1 && k <= kP16W);
+  MMB_REQUIRE(npc >= 1 && npc <= k && n_iter >= 0);
+  MMB_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0);
+  const int T = (d + 15) / 16;
+  unsigned* ctl = static_cast<unsigned*>(ws);  // arrival counter, abort word (16-byte block)
+  double* xbuf = reinterpret_cast<double*>(static_cast<char*>(ws) + 16);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve_mc_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(p16_lds_bytes(kP16MaxD)));
+    attr = true;
+  }
+  const hipError_t e = hipMemsetAsync(ctl, 0, 16, stream);
+  if (e != hipSuccess) return static_cast<int>(e);
+  pc_solve_mc_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
+                                                              pc_out, xbuf, ctl, flag);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
 extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int d,
                              const double* pc, int npc, float* out32, double* out64,
                              hipStream_t stream) {
@@ -1840,11 +2179,14 @@ extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int 
   if (v4 && per == 2 && npc == 1 && out32 && rr > 0) {
     const int64_t waves = ceil_div(n, rr);
     const int grid = static_cast<int>(std::min<int64_t>(ceil_div(waves, 4), 256 * 8));
+#ifdef MMB_DIAG
     if (rr == 2) {
       pc_remove1_kernel<2><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
     } else if (rr == 8) {
       pc_remove1_kernel<8><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
-    } else {
+    } else
+#endif
+    {
       pc_remove1_kernel<4><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
     }
     MMB_LAUNCH_CHECK();

@@ -43,6 +43,18 @@ struct StreamArgs {
   float* cmax_part;  // per-wave (wave kernel) / per-workgroup running max |x| rows [P][D], or null
 };
 
+// max of two column bounds |x| >= 0 on their bits: for non-negative floats the
+// unsigned order is the float order, and a NaN (|NaN| = 0x7fc00000..) ranks
+// above inf -- so a non-finite x reaches the bound (and mmb_gram_i8 then
+// writes NaN into G, as the f64 Gram would), where fmaxf would drop a NaN
+__device__ __forceinline__ float bmax(float a, float b) {
+  return __uint_as_float(max(__float_as_uint(a), __float_as_uint(b)));
+}
+__device__ __forceinline__ float4 bmax4(float4 m, float4 x) {
+  return make_float4(bmax(m.x, fabsf(x.x)), bmax(m.y, fabsf(x.y)), bmax(m.z, fabsf(x.z)),
+                     bmax(m.w, fabsf(x.w)));
+}
+
 template <int VEC>
 __device__ __forceinline__ void ldv(const float* p, float (&v)[VEC]) {
   if constexpr (VEC == 4) {
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         x2 = fmaf(c0 * e0, e0, x2);
         const float xf = n_ / cnt;
         a.num_out[i * a.D + f] = xf;  // x = the a2 row (sif_functions.py:55)
-        if (f < kNT) cmx0 = fmaxf(cmx0, fabsf(xf)); else cmx1 = fmaxf(cmx1, fabsf(xf));
+        if (f < kNT) cmx0 = bmax(cmx0, fabsf(xf)); else cmx1 = bmax(cmx1, fabsf(xf));
         a.s_out[i * a.Kp + f] = x1;
         a.s_out[i * a.Kp + a.D + f] = x2;
         smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
@@ -630,8 +642,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         if (u < UT) {
           const float4 xr = div4(num[c], cnt);
           stnt4<NTS>(a.num_out + i * a.D + 4 * u, xr);  // x = the a2 row
-          cmx[c] = make_float4(fmaxf(cmx[c].x, fabsf(xr.x)), fmaxf(cmx[c].y, fabsf(xr.y)),
-                               fmaxf(cmx[c].z, fabsf(xr.z)), fmaxf(cmx[c].w, fabsf(xr.w)));
+          cmx[c] = bmax4(cmx[c], xr);
           put(4 * u, sx[c]);
           put(a.D + 4 * u, sxx[c]);
         }
@@ -700,16 +711,16 @@ __global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __rest
     int r = g;
     for (; r + 7 * 16 < P; r += 8 * 16) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) mm[u] = fmaxf(mm[u], part[static_cast<int64_t>(r + 16 * u) * D + f]);
+      for (int u = 0; u < 8; ++u) mm[u] = bmax(mm[u], part[static_cast<int64_t>(r + 16 * u) * D + f]);
     }
-    for (; r < P; r += 16) mm[0] = fmaxf(mm[0], part[static_cast<int64_t>(r) * D + f]);
+    for (; r < P; r += 16) mm[0] = bmax(mm[0], part[static_cast<int64_t>(r) * D + f]);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) m = fmaxf(m, mm[u]);
+    for (int u = 0; u < 8; ++u) m = bmax(m, mm[u]);
   }
   s_m[g][c] = m;
   __syncthreads();
   if (g == 0 && f < D) {
-    for (int k = 1; k < 16; ++k) m = fmaxf(m, s_m[k][c]);
+    for (int k = 1; k < 16; ++k) m = bmax(m, s_m[k][c]);
     colmax[f] = __float_as_uint(m);
   }
 }
@@ -723,10 +734,16 @@ __global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __rest
 // once) for such sweeps.
 // Read per launch (in-process A/B sweeps flip it).  Bit 3 (policy 13):
 // the default variant compiled for two waves per SIMD (amdgpu_waves_per_eu).
+// The sweep knobs (this one, MMB_STREAM_GRID_MULT, the fused kernel's
+// MMB_FUSED_*, the projection's MMB_PROJ_*, MMB_GRAM_DIAG, MMB_PC_REMOVE_R)
+// exist only in the tools build (-DMMB_DIAG, libmmb_diag.so): the product
+// library reads no environment variable and carries only the defaults.
+#ifdef MMB_DIAG
 static int stream_policy() {
   const char* e = getenv("MMB_STREAM_POLICY");
   return e ? atoi(e) : 5;
 }
+#endif
 
 template <bool MM2, int CT, int CA, int CV, int UNR, bool NT, bool NTS, int OCC = 1>
 static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
@@ -740,14 +757,15 @@ static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
 // Workgroups per CU of the grid-stride wave kernel: 2 = exactly the resident
 // waves at its occupancy (2 waves / SIMD), one even share of utterances per
 // wave.  Measured (tools/grid_sweep.sh, MI355X): 2/4/8/16/32 = 20.88/20.94/
-// 21.04/21.01/21.18 ms.  MMB_STREAM_GRID_MULT overrides it (read once).
+// 21.04/21.01/21.18 ms.  MMB_STREAM_GRID_MULT overrides it (tools build).
 static int stream_grid_mult() {
-  static const int m = [] {
-    const char* e = getenv("MMB_STREAM_GRID_MULT");
-    const int v = e ? atoi(e) : 2;
-    return v > 0 ? v : 2;
-  }();
-  return m;
+#ifdef MMB_DIAG
+  const char* e = getenv("MMB_STREAM_GRID_MULT");  // re-read per launch (in-process A/B)
+  const int v = e ? atoi(e) : 2;
+  return v > 0 ? v : 2;
+#else
+  return 2;
+#endif
 }
 
 // rows of the column-bound partials (one per wave / workgroup of a launch)
@@ -760,6 +778,7 @@ static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nul
   if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
   if (parts) *parts = grid * 4;
+#ifdef MMB_DIAG
   switch (MM2 ? stream_policy() & 15 : 0) {
     case 13: launch_wave_v<MM2, CT, CA, CV, 4, true, false, 2>(a, grid, stream); break;
     case 1: launch_wave_v<MM2, CT, CA, CV, 2, true, false>(a, grid, stream); break;
@@ -771,6 +790,13 @@ static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nul
     case 7: launch_wave_v<MM2, CT, CA, CV, 4, true, true>(a, grid, stream); break;
     default: launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream); break;
   }
+#else
+  if constexpr (MM2) {  // policy 5: 4-frame groups, non-temporal frame loads
+    launch_wave_v<MM2, CT, CA, CV, 4, true, false>(a, grid, stream);
+  } else {
+    launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream);
+  }
+#endif
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1064,8 +1090,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
           if (uu < U) {
             const float4 xr = div4(num[c], cnt);
             st4(a.num_out + i * D + 4 * uu, xr);  // x = the a2 row
-            cmx[c] = make_float4(fmaxf(cmx[c].x, fabsf(xr.x)), fmaxf(cmx[c].y, fabsf(xr.y)),
-                                 fmaxf(cmx[c].z, fabsf(xr.z)), fmaxf(cmx[c].w, fabsf(xr.w)));
+            cmx[c] = bmax4(cmx[c], xr);
           }
         }
         if (lane == 0) {
@@ -1742,6 +1767,31 @@ static void launch_fused_v(const FusedArgs& f, int grid, hipStream_t stream) {
   }
   utt_fused_kernel<UNR, true, DIAG, PIPE, SL><<<grid, kFThreads, lds, stream>>>(f);
 }
+// streamer: 1 = pipelined (two groups in flight: kernel 23.35 -> 22.49 ms,
+// step 25.14 -> 24.41 ms in a same-process A/B, r02k); 2 (default) = also
+// prefetching across piece and batch boundaries (22.32 -> 22.14 ms, r02y);
+// 0 = one group at a time (the fallback for rows of < 3 frame groups or a
+// word table >= 2 GB, and the bit-identical reference of the tests)
+static bool fused_pipe_ok(const FusedArgs& f, int un) {
+  // the pipelined streamer stages a text row's tokens two groups before its
+  // first group is issued: >= 3 groups per row; it addresses the word table
+  // through one buffer descriptor (< 2^31 bytes)
+  return (f.s.L + un - 1) / un >= 3 && (f.s.ids == nullptr || f.s.V * f.s.D * 4 < (int64_t{1} << 31));
+}
+
+#ifndef MMB_DIAG
+static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
+  const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
+  if (parts) *parts = grid * 4;
+  if (fused_pipe_ok(f, 8)) {
+    launch_fused_v<0, 8, 2>(f, grid, stream);
+  } else {
+    launch_fused_v<0, 8, 0>(f, grid, stream);
+  }
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+#else
 static int fused_unr() {  // streamer frames per load group (in-process sweeps)
   const char* e = getenv("MMB_FUSED_UNR");
   return e ? atoi(e) : 8;
@@ -1752,10 +1802,6 @@ static int fused_diag() {  // re-read per launch (in-process timing sweeps)
   return e ? atoi(e) : 0;
 }
 
-// streamer: 1 = pipelined (two groups in flight: kernel 23.35 -> 22.49 ms,
-// step 25.14 -> 24.41 ms in a same-process A/B, r02k); 2 (default) = also
-// prefetching across piece and batch boundaries (22.32 -> 22.14 ms, r02y);
-// 0 = one group at a time (the bit-identical reference of the tests)
 static int fused_pipe() {
   const char* e = getenv("MMB_FUSED_PIPE");
   return e ? atoi(e) : 2;
@@ -1770,11 +1816,7 @@ static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
   if (parts) *parts = grid * 4;
   const int dg = fused_diag(), un = fused_unr();
-  // the pipelined streamer stages a text row's tokens two groups before its
-  // first group is issued: >= 3 groups per row
-  // and addresses the word table through one buffer descriptor (< 2^31 bytes)
-  const bool pipe = fused_pipe() != 0 && (f.s.L + un - 1) / un >= 3 &&
-                    (f.s.ids == nullptr || f.s.V * f.s.D * 4 < (int64_t{1} << 31));
+  const bool pipe = fused_pipe() != 0 && fused_pipe_ok(f, un);
   if (pipe && un == 8 && fused_pipe() == 2 && (dg == 0 || dg == 1 || dg == 4 || dg == 128 || dg == 256)) {
     if (dg == 1) {
       launch_fused_v<1, 8, 2>(f, grid, stream);
@@ -1822,6 +1864,7 @@ static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
+#endif
 
 __global__ void seq2weight_kernel(const int32_t* __restrict__ seq, const uint8_t* __restrict__ sel,
                                   int64_t total, const double* __restrict__ wtab, int64_t V,
@@ -2109,10 +2152,13 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   f.c0 = c0;
   f.out = mmb2_out;
   f.nb = ceil_div(n, kGR);
-  {  // balanced tail (in-process A/B switch)
-    const char* e = getenv("MMB_FUSED_BALANCED");  // default on: 22.35 -> 22.26 ms (r02s)
+  f.balanced = 1;  // balanced tail: 22.35 -> 22.26 ms (r02s)
+#ifdef MMB_DIAG
+  {  // in-process A/B switch
+    const char* e = getenv("MMB_FUSED_BALANCED");
     f.balanced = e ? atoi(e) : 1;
   }
+#endif
   int parts = 0;
   const int rc = launch_fused(f, stream, &parts);
   if (rc != MMB_OK || !colmax) return rc;

@@ -73,7 +73,13 @@ def sharded_sif_embeddings(table, ids_local, wtab32, n_total: int, row0: int, np
 
 
 def sharded_fused_step(inputs_local: dict, networks: dict, n_total: int, row0: int,
-                       npc: int = 1, group=None) -> P.FusedStep:
-    """The bench step on this rank's shard (SIF + MMB2 of every local utterance)."""
-    return P.FusedStep(inputs_local, networks, npc=npc, allreduce=allreduce_sum(group),
-                       n_total=n_total, row0=row0)
+                       npc: int = 1, group=None, allreduce=None) -> P.FusedStep:
+    """The bench step on this rank's shard (SIF + MMB2 of every local
+    utterance).  Checked: every run() ends with FusedStep.check(), whose flag
+    bits are summed over the ranks, so an id >= V (IndexError, like numpy's
+    fancy index at sif_functions.py:55) or an all-zero-weight utterance
+    (ValueError, TruncatedSVD's input check) on ANY rank raises on every rank.
+    `allreduce` overrides the RCCL sum (tests: a fake all-reduce)."""
+    return P.FusedStep(inputs_local, networks, npc=npc,
+                       allreduce=allreduce if allreduce is not None else allreduce_sum(group),
+                       n_total=n_total, row0=row0, check_each_run=True)

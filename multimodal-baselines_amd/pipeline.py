@@ -70,8 +70,9 @@ def check_flag(flag: torch.Tensor, V: int, zero_weights: bool = False):
     the split (sklearn check_array: "Input X contains NaN")."""
     f = int(flag.item())
     if f & L.MMB_FLAG_SYNC_TIMEOUT:
-        raise RuntimeError("mmb_mm2_stream_project: a hand-over between its streaming and "
-                           "projecting waves timed out; the step's MMB2 rows are invalid")
+        raise RuntimeError("a bounded in-kernel hand-over timed out (mmb_mm2_stream_project's "
+                           "streaming / projecting waves, or mmb_pc_solve_mc's workgroups); "
+                           "the step's MMB2 rows or PC are invalid")
     if f & L.MMB_FLAG_ID_RANGE:
         raise IndexError(f"token id out of bounds for a vocabulary of size {V}")
     if zero_weights and f & L.MMB_FLAG_ZERO_WEIGHTS:
@@ -180,13 +181,41 @@ def pc_start_block(n_total: int, d: int, npc: int, device, num=None, cnt=None, r
     return xt_omega(num, cnt, om), True
 
 
+PC_SOLVE_MC_MAX_D = 320  # mmb_pc_solve_mc: ceil(d / 16) workgroups, k <= 16
+_solve_ws: dict = {}
+
+
+def solve_workspace(d: int, device) -> torch.Tensor:
+    """Scratch of mmb_pc_solve_mc (the tiles exchanged between its
+    workgroups), one per (d, device, current stream): a call owns it until
+    it completes, and calls on one stream are ordered."""
+    key = (d, str(device), L.stream_ptr())
+    ws = _solve_ws.get(key)
+    if ws is None:
+        ws = torch.empty(L.query("mmb_pc_solve_mc_ws_bytes", d), dtype=torch.uint8, device=device)
+        if len(_solve_ws) > 16:
+            _solve_ws.clear()
+        _solve_ws[key] = ws
+    return ws
+
+
 def pc_solve(G: torch.Tensor, z0: torch.Tensor, npc: int, transposed: bool,
-             n_iter: int = N_ITER) -> torch.Tensor:
+             n_iter: int = N_ITER, out: torch.Tensor | None = None,
+             flag: torch.Tensor | None = None, ws: torch.Tensor | None = None) -> torch.Tensor:
+    """sklearn's randomized-SVD components from the Gram (a3's solve).  d <=
+    320: the multi-workgroup solver (mmb_pc_solve_mc; a hand-over timeout
+    sets MMB_FLAG_SYNC_TIMEOUT in `flag`); larger d: one workgroup."""
     d = G.shape[0]
     k = z0.shape[1]
-    pc = torch.empty((npc, d), dtype=torch.float64, device=G.device)
-    L.call("mmb_pc_solve", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed), L.ptr(pc),
-           L.stream_ptr())
+    pc = out if out is not None else torch.empty((npc, d), dtype=torch.float64, device=G.device)
+    if d <= PC_SOLVE_MC_MAX_D and k <= 16:
+        if ws is None:
+            ws = solve_workspace(d, G.device)
+        L.call("mmb_pc_solve_mc", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed),
+               L.ptr(pc), L.ptr(ws), L.ptr(flag), L.stream_ptr())
+    else:
+        L.call("mmb_pc_solve", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed), L.ptr(pc),
+               L.stream_ptr())
     return pc
 
 
@@ -316,17 +345,29 @@ class MMB2Projection:
         self.c0 = torch.empty((self.ldw,), dtype=torch.float32, device=device)
         nbytes = L.query("mmb_mm2_split_bytes", d, a, vd)
         self.wsplit = torch.empty((nbytes + 15) // 16 * 16, dtype=torch.uint8, device=device)
-        self.params = []
-        for k in MMB2_KEYS:  # KeyError for a missing combination, like sif2.py:182
-            mu, ls = networks[k]
-            self.params.append(tuple(p.detach().to(device=device, dtype=torch.float32).contiguous()
-                                     for p in (mu.weight, mu.bias, ls.weight, ls.bias)))
+        self.device = device
+        self.networks = {k: networks[k] for k in MMB2_KEYS}  # KeyError like sif2.py:182
         self.refresh()
 
+    def _live(self):
+        """The generators' current parameter tensors (w_mu, b_mu, w_ls, b_ls per key)."""
+        return [(mu.weight, mu.bias, ls.weight, ls.bias)
+                for mu, ls in (self.networks[k] for k in MMB2_KEYS)]
+
     def _versions(self):
-        return tuple(t._version for ps in self.params for t in ps)
+        # storage address + version counter of every parameter: an optimiser
+        # step (in place) bumps the counter, `p.data = t` moves the address
+        return tuple((t.data_ptr(), t._version) for ps in self._live() for t in ps)
+
+    def invalidate(self):
+        """Force a re-merge at the next refresh_if_changed(): needed after
+        writes that neither bump a parameter's version counter nor move its
+        storage (e.g. `p.data.copy_(...)`, which bypasses autograd's counter)."""
+        self._seen = None
 
     def refresh(self):
+        self.params = [tuple(p.detach().to(device=self.device, dtype=torch.float32).contiguous()
+                             for p in ps) for ps in self._live()]
         arr = lambda i: (ctypes_ptr_array([p[i].data_ptr() for p in self.params]))
         L.call("mmb_mm2_prepare", arr(0), arr(1), arr(2), arr(3), self.d, self.a, self.vd, self.t,
                L.ptr(self.wm), self.ldw, L.ptr(self.c0), L.ptr(self.wsplit), L.stream_ptr())
@@ -346,10 +387,12 @@ class MMB2Projection:
                    L.ptr(self.wpieces), L.stream_ptr())
 
     def refresh_if_changed(self) -> bool:
-        """Re-merge only when a generator parameter changed in place since the
-        last merge (torch's version counters: an optimiser step bumps them), so
-        a step over a new batch with the same weights skips the five prepare
-        launches.  Returns whether it re-merged."""
+        """Re-merge only when a generator parameter changed since the last
+        merge (torch's version counters -- an optimiser step bumps them -- or
+        a parameter's storage moved), so a step over a new batch with the same
+        weights skips the five prepare launches.  Writes through `p.data`
+        bump no counter: call invalidate() after them.  Returns whether it
+        re-merged."""
         if getattr(self, "_seen", None) == self._versions():
             return False
         self.refresh()
@@ -542,8 +585,10 @@ class FusedStep:
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
                  side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True,
-                 gram_kind: str | None = None, stream_project: bool | None = None):
+                 gram_kind: str | None = None, stream_project: bool | None = None,
+                 check_each_run: bool = False):
         self.inp = inputs
+        self.check_each_run = check_each_run
         self.ids = inputs["ids"]
         self.n, self.t = self.ids.shape
         self.table = inputs["table"]
@@ -565,6 +610,9 @@ class FusedStep:
         if self.stream_project:
             self.proj.enable_pieces()
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
+        self.pc_buf = torch.empty((npc, self.d), dtype=torch.float64, device=dev)
+        self.solve_ws = (torch.empty(L.query("mmb_pc_solve_mc_ws_bytes", self.d), dtype=torch.uint8,
+                                     device=dev) if self.d <= PC_SOLVE_MC_MAX_D else None)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         check_npc(npc)
@@ -619,9 +667,23 @@ class FusedStep:
     def check(self):
         """Raise what the reference would have raised for the last step(s):
         IndexError for a token id >= V, ValueError for an utterance whose SIF
-        weights are all 0 (the PC step of the split is then undefined).  Reads
-        the flag word (one device sync); the flag accumulates until `reset()`."""
-        check_flag(self.flag, self.V, zero_weights=True)
+        weights are all 0 (the PC step of the split is then undefined),
+        RuntimeError if the fused kernel's hand-over timed out.  Reads the flag
+        word (one device sync); the flag accumulates until `reset()`.
+
+        Sharded (an `allreduce` given), the three flag bits are summed over
+        the ranks first -- one small all-reduce, only here -- so EVERY rank
+        raises the same error for a bad utterance on any rank (a rank that
+        raised alone would leave the others waiting in the next step's Gram
+        all-reduce).  A NaN row reaches every rank's PC through the Gram anyway
+        (check_pc_finite)."""
+        flag = self.flag
+        if self.allreduce is not None:
+            bits = (L.MMB_FLAG_ID_RANGE, L.MMB_FLAG_ZERO_WEIGHTS, L.MMB_FLAG_SYNC_TIMEOUT)
+            t = torch.stack([(flag[0] & b) != 0 for b in bits]).to(torch.int32)
+            self.allreduce(t)
+            flag = sum((t[i] > 0).to(torch.int32) * b for i, b in enumerate(bits)).reshape(1)
+        check_flag(flag, self.V, zero_weights=True)
         if getattr(self, "pc", None) is not None:
             check_pc_finite(self.pc)
 
@@ -675,11 +737,23 @@ class FusedStep:
                 if transposed:
                     self.allreduce(z0)
         with mark("pc_solve"):
-            return pc_solve(self.G, z0, self.npc, transposed)
+            return pc_solve(self.G, z0, self.npc, transposed, out=self.pc_buf, flag=self.flag,
+                            ws=self.solve_ws)
 
-    def run(self, trace: dict | None = None):
+    def run(self, trace: dict | None = None, check: bool | None = None):
         """One step.  With `trace` (a dict), HIP events are recorded on the
-        stream each phase runs on: trace[phase] gets (start, end) pairs."""
+        stream each phase runs on: trace[phase] gets (start, end) pairs.
+        With `check` (default: the constructor's `check_each_run`) the step
+        ends with check() -- one device sync -- and raises like the
+        reference; without it the step never synchronises and the caller
+        calls check() when it wants the verdict (bench.py: once, after the
+        timed steps)."""
+        out = self._run(trace)
+        if self.check_each_run if check is None else check:
+            self.check()
+        return out
+
+    def _run(self, trace):
         def mark(name):
             if trace is None:
                 return _NullSpan()

@@ -136,6 +136,42 @@ def device_workload(N: int, T: int, V: int, D: int = 300, A: int = 300, Vd: int 
     return out
 
 
+SHARD_BLOCK = 62_500  # rows per seeded block of a sharded workload (1M / 16)
+
+
+def device_shard(row0: int, n: int, T: int, V: int, D: int = 300, A: int = 300, Vd: int = 300,
+                 seed: int = 1000, device="cuda", block: int = SHARD_BLOCK):
+    """Rows [row0, row0 + n) of ONE synthetic config-3 split, generated in
+    device memory the same way whatever the sharding: the word table and
+    weights come from `seed` (replicated on every rank), the utterances from
+    seeded blocks of `block` rows (block b: seed + 1 + b).  So the N shards of
+    bench.py's strong scaling (1M / N rows each) are slices of the same
+    1M-utterance split for every N, and a test can rebuild the union of the
+    ranks' rows in one process.  Same recipe as device_workload (Zipf ids,
+    U(-1, 1) frames); returns the same dict."""
+    import torch
+
+    base = device_workload(1, T, V, D=D, A=1, Vd=1, seed=seed, device=device)
+    ids = torch.empty(n, T, device=device, dtype=torch.int32)
+    audio = torch.empty(n, T, A, device=device, dtype=torch.float32)
+    visual = torch.empty(n, T, Vd, device=device, dtype=torch.float32)
+    r = row0
+    while r < row0 + n:
+        b = r // block
+        b0 = b * block
+        hi = min(row0 + n, b0 + block)
+        # the whole block from its seed (device RNG streams are not
+        # prefix-stable across sizes), then the rows this shard owns
+        blk = device_workload(block, T, V, D=1, A=A, Vd=Vd, seed=seed + 1 + b, device=device)
+        ids[r - row0:hi - row0] = blk["ids"][r - b0:hi - b0]
+        audio[r - row0:hi - row0] = blk["audio"][r - b0:hi - b0]
+        visual[r - row0:hi - row0] = blk["visual"][r - b0:hi - b0]
+        del blk
+        r = hi
+    return {"table": base["table"], "wtab": base["wtab"], "ids": ids, "audio": audio,
+            "visual": visual}
+
+
 # ---------------------------------------------------------------- CLI datasets
 def mm_splits(seed: int = 0, sizes=(96, 32, 32), T: int = 12, V: int = 300, A_raw: int = 20,
               Vd_raw: int = 14, dataset: str = "mosi", n_labels: int = 1):

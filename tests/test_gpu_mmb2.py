@@ -262,28 +262,6 @@ def test_overlapped_step_cu_masked_matches_single_chunk(gpu, side_cus):
     assert M.row_rel_err(s4.cpu().numpy(), s1.cpu().numpy()) < 1e-6
 
 
-@pytest.mark.parametrize("variant", ["3", "4", "6"])
-@pytest.mark.parametrize("N", [700, 128, 129, 1000])
-def test_projection_variants_bit_identical(gpu, N, variant, monkeypatch):
-    """Variant 3 (A fragments straight from HBM into registers, B through a
-    3-slot LDS ring, 4 x 2 waves) and variant 4 (256-row tiles) sum every 16x16
-    tile in the same MFMA order as the default kernel and share its epilogue:
-    MMB2 and PC-removed rows bit-identical, ragged last tiles included."""
-    T, V = 40, 5000
-    inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=41, device=gpu)
-    torch.manual_seed(0)
-    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    step = P.FusedStep(inp, gen.networks(), stream_project=False)
-    s1, m1 = [t.clone() for t in step.run()]
-    monkeypatch.setenv("MMB_PROJ_VARIANT", variant)
-    step.sif.zero_()
-    step.mmb2.zero_()
-    s3, m3 = step.run()
-    torch.cuda.synchronize()
-    assert torch.equal(m1, m3)
-    assert torch.equal(s1, s3)
-
-
 @pytest.mark.parametrize("N,T", [(3000, 40), (129, 40), (40, 300)])
 def test_fused_step_int8_gram_vs_f64(gpu, N, T):
     """The default step's Gram (mmb_gram_i8 on the column bounds the stream
@@ -341,49 +319,6 @@ def test_zero_weight_rows_sif_raises_mmb2_finite(gpu):
                                             M.params_from_module(gen.cpu()), sw, text)
     assert np.isfinite(mm2_out).all()
     assert M.row_rel_err(mm2_out, ref) < TOL
-
-
-_VARIANT_SCRIPT = r"""
-import sys, numpy as np, torch
-sys.path[:0] = [sys.argv[2], sys.argv[2] + "/multimodal-baselines_amd"]
-import models, pipeline as P, synth
-dev = torch.device("cuda", 0)
-inp = synth.device_workload(700, 40, 5000, A=300, Vd=300, seed=31, device=dev)
-torch.manual_seed(0)
-gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
-s, m = P.FusedStep(inp, gen.networks()).run()
-np.savez(sys.argv[1], sif=s.cpu().numpy(), mmb2=m.cpu().numpy())
-"""
-
-
-@pytest.mark.parametrize("env", [{"MMB_PROJ_VARIANT": "0", "MMB_STREAM_POLICY": "0"},
-                                 {"MMB_PROJ_VARIANT": "1"}, {"MMB_PROJ_VARIANT": "3"},
-                                 {"MMB_PROJ_VARIANT": "4"},
-                                 {"MMB_STREAM_POLICY": "7", "MMB_STREAM_GRID_MULT": "8"},
-                                 {"MMB_PROJ_ROWEPI": "0"}])
-def test_non_default_kernel_variants_agree(gpu, tmp_path, env):
-    """The measured-and-kept-selectable variants (32x32x16 projection tiles,
-    the 16x16x32 kernel without the pipelined K loop, every stream-kernel
-    load/store policy, grid size; read once per process,
-    so run in a child process) give the default path's rows: SIF to the
-    removal's dot order, MMB2 within the 1e-5 bar."""
-    import os
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    path = str(tmp_path / "variant.npz")
-    subprocess.run([sys.executable, "-c", _VARIANT_SCRIPT, path, root], check=True, timeout=300,
-                   env={**os.environ, **env})
-    z = np.load(path)
-    inp = synth.device_workload(700, 40, 5000, A=300, Vd=300, seed=31, device=gpu)
-    torch.manual_seed(0)
-    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    s, m = P.FusedStep(inp, gen.networks()).run()
-    # SIF: the same x, Gram and PC; the removal's f64 dot may sum in another
-    # order (the 32x32x16 kernel's tail reduces with shuffles, not DPP)
-    assert M.row_rel_err(z["sif"], s.cpu().numpy()) < 1e-6
-    assert M.row_rel_err(z["mmb2"], m.cpu().numpy()) < TOL
 
 
 def _pom_case(golden, case, n, A, Vd, seed):
@@ -636,74 +571,3 @@ def test_stream_project_repeatable_and_unit_rows(gpu):
     assert torch.equal(s1, s2) and torch.equal(m1, m2)
     norms = torch.linalg.norm(m1.double(), dim=1)
     assert (norms - 1).abs().max().item() < 1e-5
-
-
-def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False, balanced=False):
-    """One mmb_mm2_stream_project launch with the streamer selected by
-    MMB_FUSED_PIPE and the row assignment by MMB_FUSED_BALANCED (read per
-    launch by the library); every output cloned."""
-    import os
-
-    dev = inp["audio"].device
-    d = 300
-    flag = torch.zeros(1, dtype=torch.int32, device=dev)
-    colmax = torch.empty(d, dtype=torch.int32, device=dev)
-    ws = torch.empty((8192, d), dtype=torch.float32, device=dev)
-    kw = dict(ids32=inp["ids"], table=inp["table"], wtab32=inp["wtab"])
-    if dense:
-        ids = inp["ids"].long()
-        kw = dict(text_dense=inp["table"][ids.clamp(min=0)].contiguous(),
-                  w_dense=inp["wtab"][ids.clamp(min=0)] * (ids >= 0))
-    knobs = {"MMB_FUSED_PIPE": str(int(pipe)), "MMB_FUSED_BALANCED": "1" if balanced else "0"}
-    old = {k: os.environ.get(k) for k in knobs}
-    os.environ.update(knobs)
-    try:
-        x, aux, m = P.mm2_stream_project(n, t, d, a, vd, inp["audio"], inp["visual"], proj,
-                                         flag=flag, colmax=colmax, colmax_ws=ws, **kw)
-        torch.cuda.synchronize()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    return [v.clone() for v in (x, aux, m, colmax, flag)]
-
-
-@pytest.mark.parametrize("N,T,A,Vd,dense,bad", [(2048, 40, 300, 300, False, False),
-                                                (15, 40, 300, 300, False, False),
-                                                (700, 64, 300, 300, False, True),
-                                                (999, 33, 260, 292, False, False),
-                                                (97, 40, 300, 20, False, False),
-                                                (300, 17, 300, 256, False, False),
-                                                (5003, 24, 300, 300, False, True),
-                                                (50, 16, 300, 300, False, False),
-                                                (500, 40, 300, 300, True, False),
-                                                (49, 40, 100, 300, False, False),
-                                                (30011, 40, 300, 300, False, False)])
-def test_fused_pipelined_streamer_bit_identical(gpu, N, T, A, Vd, dense, bad):
-    """The pipelined streamer of utt_fused_kernel (two frame groups in flight
-    across group, row and text-token boundaries; buffer-descriptor loads)
-    (MMB_FUSED_PIPE=1; =2 also prefetching across piece and batch boundaries)
-    against the group-at-a-time streamer: x, aux, MMB2 rows, column bounds
-    and the flag word bit-identical -- partial batches, partial last groups
-    (T = 33, 17), the 3-group minimum (T = 24; T = 16 falls back), narrow
-    frames, dense text, negative and out-of-range ids -- and with the rows
-    past the last full round of batches split evenly over the workgroups
-    (MMB_FUSED_BALANCED; N = 30011: two full rounds of 256 x 48 rows and a
-    5,435-row tail) instead of left as whole batches."""
-    inp = synth.device_workload(N, T, 20_000, A=A, Vd=Vd, seed=71, device=gpu)
-    if bad:  # negative ids wrap; ids >= V are flagged and contribute zero rows
-        inp["ids"][3, 5] = -7
-        inp["ids"][N // 2, T - 1] = 20_000 + 11
-        inp["ids"][N - 1, 0] = -20_001
-    torch.manual_seed(0)
-    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
-    proj = P.MMB2Projection(gen.networks(), 300, A, Vd, T, gpu)
-    ref = _fused_outputs(inp, proj, N, T, A, Vd, pipe=False, dense=dense)
-    names = ["x", "aux", "mmb2", "colmax", "flag"]
-    for pipe, bal in [(1, False), (1, True), (0, True), (2, True), (2, False)]:
-        got = _fused_outputs(inp, proj, N, T, A, Vd, pipe=pipe, dense=dense, balanced=bal)
-        for nm, r, g in zip(names, ref, got):
-            assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), (nm, pipe, bal)
-    assert (int(ref[4].item()) != 0) == bad

@@ -284,8 +284,9 @@ def test_fused_step_sharded_with_fake_allreduce(gpu, n_total, shards):
         step = P.FusedStep(sl, gen.networks(), n_total=n_total, row0=row0,
                            allreduce=lambda t, got=got: got.append(t.clone()))
         step.run()
+        step.check()  # sharded: its flag bits cross the ranks too
         local.append(got)
-    n_calls = 2 if n_total < 300 else 1
+    n_calls = (2 if n_total < 300 else 1) + 1
     assert all(len(g) == n_calls for g in local)
 
     # pass 2: the fake all-reduce adds the other shards' tensors in rank order
@@ -311,6 +312,93 @@ def test_fused_step_sharded_with_fake_allreduce(gpu, n_total, shards):
         mm2_parts.append(m.clone())
     assert torch.equal(torch.cat(mm2_parts), m_ref)
     assert M.row_rel_err(torch.cat(sif_parts).cpu().numpy(), s_ref.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("value", [float("inf"), float("nan")])
+@pytest.mark.parametrize("gram_kind", ["i8", "f64"])
+def test_nonfinite_table_row_raises(gpu, value, gram_kind):
+    """A non-finite word-table entry used with a nonzero weight makes that
+    utterance's a2 row non-finite; the reference's TruncatedSVD rejects the
+    split (ValueError, sif_functions.py:65).  The int8 Gram carries it: the
+    column bound keeps NaN / inf (max on the bits), and a non-finite bound
+    writes NaN into G, so the PC is NaN and check() raises -- as with the
+    exact f64 Gram."""
+    import models
+
+    inp = synth.device_workload(2000, 40, 8000, seed=19, device=gpu)
+    inp["table"][11, 17] = value
+    inp["ids"][123, 5] = 11
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks(), gram_kind=gram_kind)
+    step.run()
+    if gram_kind == "i8":
+        cm = step.colmax.cpu().numpy().view(np.float32)
+        assert not np.isfinite(cm[17]) and np.isfinite(np.delete(cm, 17)).all()
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        step.check()
+
+
+@pytest.mark.parametrize("bad,err", [("id_range", IndexError), ("zero_weight", ValueError),
+                                     ("none", None)])
+def test_sharded_checked_step_raises_on_every_rank(gpu, bad, err):
+    """distributed.sharded_fused_step returns a checked step: a token id >= V
+    (numpy's IndexError, sif_functions.py:55) or an all-zero-weight utterance
+    (TruncatedSVD's ValueError on the NaN row, sif_functions.py:65) on ONE
+    shard raises on EVERY shard -- the flag bits are summed by the step's
+    all-reduce, and the zero-weight row's NaN reaches every shard's PC through
+    the int8 Gram (a non-finite column bound makes G NaN) -- so no rank is left
+    waiting in the next all-reduce.  Three shards on one device, RCCL's
+    all-reduce replaced by a fake that adds the other shards' tensors in call
+    order (recorded in a first pass)."""
+    import distributed as D
+    import models
+
+    n_total, shards, V = 3000, 3, 8000
+    inp = synth.device_workload(n_total, 40, V, seed=17, device=gpu)
+    if bad == "id_range":
+        inp["ids"][1500, 3] = V + 5  # shard 1's rows are [1000, 2000)
+    elif bad == "zero_weight":
+        inp["wtab"][7] = 0.0
+        inp["ids"][1500] = 7
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+
+    def shard(r):
+        row0, n = D.shard_range(n_total, shards, r)
+        return row0, {k: (v[row0:row0 + n] if k in ("ids", "audio", "visual") else v)
+                      for k, v in inp.items()}
+
+    local = []
+    for r in range(shards):  # pass 1: each shard's own all-reduce operands, in call order
+        row0, sl = shard(r)
+        got = []
+        step = D.sharded_fused_step(sl, gen.networks(), n_total, row0,
+                                    allreduce=lambda t, got=got: got.append(t.clone()))
+        try:
+            step.run()
+        except (IndexError, ValueError):
+            assert r == 1 and err is not None  # only the shard holding the bad row
+        local.append(got)
+    assert all(len(g) == 2 for g in local)  # the Gram, then check()'s flag bits
+    for r in range(shards):  # pass 2: the fake all-reduce sums over the shards
+        row0, sl = shard(r)
+        calls = iter(range(2))
+
+        def fake(t, r=r, calls=calls):
+            c = next(calls)
+            tot = torch.zeros_like(t)
+            for q in range(shards):
+                tot += t if q == r else local[q][c]
+            t.copy_(tot)
+
+        step = D.sharded_fused_step(sl, gen.networks(), n_total, row0, allreduce=fake)
+        if err is None:
+            step.run()
+            assert bool(torch.isfinite(step.pc).all())
+        else:
+            with pytest.raises(err):
+                step.run()
 
 
 @pytest.mark.parametrize("n,seed,scale", [(320, 0, 1.0), (5000, 1, 1.0), (70_000, 2, 1e-3),
@@ -347,36 +435,3 @@ def test_gram_i8_pc_on_golden_splits(gpu, golden):
         G = P.gram_i8(x, P.colmax(x))
         pc = P.pc_solve(G, P.omega(300, npc + 10, gpu), npc, False).cpu().numpy()
         assert np.abs(pc - z["pc"]).max() < 1e-9, case
-
-
-@pytest.mark.parametrize("n,d,with_cnt", [(1, 300, False), (5, 300, True), (1003, 300, False),
-                                          (4099, 300, True), (777, 260, False), (130, 292, True)])
-def test_remove_multirow_kernel_bit_identical(gpu, n, d, with_cnt):
-    """pc_remove1_kernel (one PC, R rows per wave in flight, the PC in
-    registers) against pc_remove_kernel (MMB_PC_REMOVE_R=0): bit-identical
-    rows -- row counts not multiples of R, narrow rows, a count divisor --
-    and within 1e-6 of the f64 removal of the oracle."""
-    import os
-
-    g = torch.Generator(device=gpu).manual_seed(5)
-    x = torch.randn(n, d, generator=g, device=gpu) * 3 + 0.5
-    cnt = torch.randint(1, 40, (n,), generator=g, device=gpu).float() if with_cnt else None
-    pc = torch.randn(1, d, generator=g, device=gpu, dtype=torch.float64)
-    pc /= torch.linalg.norm(pc)
-    outs = []
-    old = os.environ.get("MMB_PC_REMOVE_R")
-    try:
-        for r in ("0", "4", "2", "8"):
-            os.environ["MMB_PC_REMOVE_R"] = r
-            outs.append(P.remove_pc(x, cnt, pc).clone())
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            os.environ.pop("MMB_PC_REMOVE_R", None)
-        else:
-            os.environ["MMB_PC_REMOVE_R"] = old
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
-    xs = x.double() / (cnt.double()[:, None] if with_cnt else 1.0)
-    ref = xs - (xs @ pc.T) @ pc
-    assert (outs[0].double() - ref).abs().max().item() <= 1e-6 * xs.abs().max().item()

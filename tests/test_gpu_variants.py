@@ -1,0 +1,54 @@
+"""Measured kernel variants against the product defaults (tools build).
+
+The product library carries only the default kernels and reads no
+environment variable (`strings libmmb.so` has no MMB_* knob); the variants
+and timing-only ablations live in libmmb_diag.so (`make diag`).  Each group
+of tests/variant_checks.py runs in ONE child process with MMB_LIB_PATH set to
+that build; the fused-streamer group also dumps the group-at-a-time
+streamer's outputs, which the product library (this process) must reproduce
+bit for bit with its default streamer.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import mmb_lib as L
+import variant_checks as VC
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIAG = os.path.join(ROOT, "multimodal-baselines_amd", "libmmb_diag.so")
+pytestmark = pytest.mark.gpu
+
+
+def _child(group, tmp_path):
+    assert os.path.exists(DIAG), "libmmb_diag.so missing: build() runs `make diag`"
+    env = {**os.environ, "MMB_LIB_PATH": DIAG, "VARIANT_DUMP": str(tmp_path)}
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "variant_checks.py"),
+                        group], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("group", ["projection", "remove_rows", "gram"])
+def test_variants_agree(gpu, tmp_path, group):
+    _child(group, tmp_path)
+
+
+def test_fused_streamers_and_product_default(gpu, tmp_path):
+    """Streamer / tail variants bit-identical in the tools build, and the
+    product library's default launch bit-identical to the group-at-a-time
+    streamer on every case (pipe 2 + balanced tail where rows have >= 3 frame
+    groups, the group-at-a-time fallback below)."""
+    _child("fused_streamer", tmp_path)
+    names = ["x", "aux", "mmb2", "colmax", "flag"]
+    for ci, (N, T, A, Vd, dense, bad) in enumerate(VC.FUSED_CASES):
+        inp, proj = VC.fused_case(gpu, N, T, A, Vd, bad)
+        got = VC.fused_outputs(inp, proj, N, T, A, Vd, dense=dense)
+        ref = np.load(str(tmp_path / f"fused_{ci}.npz"))
+        for nm, g in zip(names, got):
+            r = torch.from_numpy(ref[nm]).to(gpu)
+            assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), (nm, ci)

@@ -45,6 +45,19 @@ def test_exports_are_c_symbols():
     assert set(declared_functions()) <= exported  # unmangled extern "C"
 
 
+def test_product_library_reads_no_knobs():
+    """The product library carries only the default kernels: no getenv, no
+    MMB_* knob string, no timing-only DIAG build (those live in the tools
+    build libmmb_diag.so, `make diag`)."""
+    path = os.path.join(ROOT, "multimodal-baselines_amd", "libmmb.so")
+    blob = open(path, "rb").read()
+    assert b"DIAG" not in blob
+    assert re.search(rb"MMB_[A-Z_]{3,}", blob) is None
+    undef = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True,
+                           check=True).stdout
+    assert "getenv" not in undef
+
+
 def test_library_carries_gfx950_code_objects():
     data = open(mmb_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data

@@ -1,0 +1,215 @@
+"""Cross-checks of the measured kernel variants against the product defaults.
+
+The product library (libmmb.so) carries only the default kernels and reads
+no environment variable.  The variants the design notes measured -- the
+projection's 32x32x16 / un-pipelined / register-A (3) / 256-row (4) /
+register-B (6) kernels and its tile-layout epilogue, the stream kernel's
+load/store policies and grid sizes, the fused kernel's group-at-a-time and
+pipelined streamers and its unbalanced tail, the one-row PC removal -- live in
+the tools build, libmmb_diag.so (`make diag`, -DMMB_DIAG), where MMB_* knobs
+select them per launch.  This script runs in a child process with
+MMB_LIB_PATH pointing at that build (tests/test_gpu_variants.py) and asserts
+that each variant reproduces the default path: bit-identical where the
+variant sums in the same order, within the stated bar otherwise.
+
+    MMB_LIB_PATH=.../libmmb_diag.so python tests/variant_checks.py <group>
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multimodal-baselines_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import mmb_lib as L  # noqa: E402
+import models  # noqa: E402
+import pipeline as P  # noqa: E402
+import synth  # noqa: E402
+from oracle import mmb2_oracle as M  # noqa: E402
+
+TOL = 1e-5
+
+
+@contextlib.contextmanager
+def knobs(**kv):
+    """Set MMB_* knobs of the tools build for the launches inside the block."""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update({k: str(v) for k, v in kv.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _gen(dev, A=300, Vd=300):
+    torch.manual_seed(0)
+    return models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(dev)
+
+
+def check_projection(dev):
+    """Projection variants 3 (A fragments straight from HBM into registers),
+    4 (256-row tiles) and 6 (B straight from L2 into registers) sum every
+    16x16 tile in the default kernel's MFMA order and share its epilogue:
+    MMB2 and PC-removed rows bit-identical, ragged last tiles included.  The
+    32x32x16 kernel (0), the un-pipelined 16x16x32 kernel (1) and the
+    tile-layout epilogue agree to the removal's dot order / the 1e-5 bar."""
+    for N in (700, 128, 129, 1000):
+        inp = synth.device_workload(N, 40, 5000, A=300, Vd=300, seed=41, device=dev)
+        step = P.FusedStep(inp, _gen(dev).networks(), stream_project=False)
+        s1, m1 = [t.clone() for t in step.run()]
+        for variant in ("3", "4", "6"):
+            with knobs(MMB_PROJ_VARIANT=variant):
+                step.sif.zero_()
+                step.mmb2.zero_()
+                s3, m3 = step.run()
+                torch.cuda.synchronize()
+            assert torch.equal(m1, m3), ("mmb2", N, variant)
+            assert torch.equal(s1, s3), ("sif", N, variant)
+        for kv in ({"MMB_PROJ_VARIANT": "0", "MMB_STREAM_POLICY": "0"}, {"MMB_PROJ_VARIANT": "1"},
+                   {"MMB_STREAM_POLICY": "7", "MMB_STREAM_GRID_MULT": "8"},
+                   {"MMB_STREAM_POLICY": "13"}, {"MMB_PROJ_ROWEPI": "0"}):
+            with knobs(**kv):
+                s2, m2 = [t.clone() for t in step.run()]
+                torch.cuda.synchronize()
+            # the 32x32x16 kernel's tail reduces the removal's f64 dot with
+            # shuffles, not DPP: the SIF rows agree to that order
+            assert M.row_rel_err(s2.cpu().numpy(), s1.cpu().numpy()) < 1e-6, (N, kv)
+            assert M.row_rel_err(m2.cpu().numpy(), m1.cpu().numpy()) < TOL, (N, kv)
+    print("projection: variants 0/1/3/4/6, tile epilogue, stream policies 0/7/13 ok")
+
+
+# (N, T, A, Vd, dense text, bad ids)
+FUSED_CASES = [(2048, 40, 300, 300, False, False), (15, 40, 300, 300, False, False),
+               (700, 64, 300, 300, False, True), (999, 33, 260, 292, False, False),
+               (97, 40, 300, 20, False, False), (300, 17, 300, 256, False, False),
+               (5003, 24, 300, 300, False, True), (50, 16, 300, 300, False, False),
+               (500, 40, 300, 300, True, False), (49, 40, 100, 300, False, False),
+               (30011, 40, 300, 300, False, False)]
+
+
+def fused_case(dev, N, T, A, Vd, bad):
+    """Seeded inputs and the merged projection of one FUSED_CASES entry."""
+    inp = synth.device_workload(N, T, 20_000, A=A, Vd=Vd, seed=71, device=dev)
+    if bad:  # negative ids wrap; ids >= V are flagged and contribute zero rows
+        inp["ids"][3, 5] = -7
+        inp["ids"][N // 2, T - 1] = 20_000 + 11
+        inp["ids"][N - 1, 0] = -20_001
+    proj = P.MMB2Projection(_gen(dev, A, Vd).networks(), 300, A, Vd, T, dev)
+    return inp, proj
+
+
+def fused_outputs(inp, proj, n, t, a, vd, dense=False):
+    """One mmb_mm2_stream_project launch (whatever the loaded library's
+    default streamer is); every output cloned."""
+    d = 300
+    flag = torch.zeros(1, dtype=torch.int32, device=inp["audio"].device)
+    colmax = torch.empty(d, dtype=torch.int32, device=flag.device)
+    ws = torch.empty((8192, d), dtype=torch.float32, device=flag.device)
+    kw = dict(ids32=inp["ids"], table=inp["table"], wtab32=inp["wtab"])
+    if dense:
+        ids = inp["ids"].long()
+        kw = dict(text_dense=inp["table"][ids.clamp(min=0)].contiguous(),
+                  w_dense=inp["wtab"][ids.clamp(min=0)] * (ids >= 0))
+    x, aux, m = P.mm2_stream_project(n, t, d, a, vd, inp["audio"], inp["visual"], proj,
+                                     flag=flag, colmax=colmax, colmax_ws=ws, **kw)
+    torch.cuda.synchronize()
+    return [v.clone() for v in (x, aux, m, colmax, flag)]
+
+
+def _fused_outputs(inp, proj, n, t, a, vd, pipe, dense=False, balanced=False):
+    with knobs(MMB_FUSED_PIPE=int(pipe), MMB_FUSED_BALANCED=1 if balanced else 0):
+        return fused_outputs(inp, proj, n, t, a, vd, dense=dense)
+
+
+def check_fused_streamer(dev):
+    """The pipelined streamers of utt_fused_kernel (MMB_FUSED_PIPE=1: two
+    frame groups in flight across group, row and text-token boundaries; =2,
+    the product default: also across piece and batch boundaries) against the
+    group-at-a-time streamer: x, aux, MMB2 rows, column bounds and the flag
+    word bit-identical -- partial batches, partial last groups (T = 33, 17),
+    the 3-group minimum (T = 24; T = 16 falls back), narrow frames, dense
+    text, negative and out-of-range ids -- with and without the balanced tail
+    (N = 30011: two full rounds of 256 x 48 rows and a 5,435-row tail)."""
+    names = ["x", "aux", "mmb2", "colmax", "flag"]
+    dump = os.environ.get("VARIANT_DUMP")
+    for ci, (N, T, A, Vd, dense, bad) in enumerate(FUSED_CASES):
+        inp, proj = fused_case(dev, N, T, A, Vd, bad)
+        ref = _fused_outputs(inp, proj, N, T, A, Vd, pipe=False, dense=dense)
+        if dump:  # the group-at-a-time streamer's outputs, for the product-library comparison
+            np.savez(os.path.join(dump, f"fused_{ci}.npz"),
+                     **{nm: r.cpu().numpy() for nm, r in zip(names, ref)})
+        for pipe, bal in [(1, False), (1, True), (0, True), (2, True), (2, False)]:
+            got = _fused_outputs(inp, proj, N, T, A, Vd, pipe=pipe, dense=dense, balanced=bal)
+            for nm, r, g in zip(names, ref, got):
+                assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), \
+                    (nm, N, T, pipe, bal)
+        assert (int(ref[4].item()) != 0) == bad
+    print(f"fused streamer: {len(FUSED_CASES)} shapes x 5 streamer / tail variants bit-identical")
+
+
+def check_remove_rows(dev):
+    """pc_remove1_kernel (one PC, R = 2 / 4 / 8 rows per wave in flight, the
+    PC in registers) against pc_remove_kernel (MMB_PC_REMOVE_R=0):
+    bit-identical rows -- row counts not multiples of R, narrow rows, a count
+    divisor -- and within 1e-6 of the f64 removal."""
+    for n, d, with_cnt in [(1, 300, False), (5, 300, True), (1003, 300, False),
+                           (4099, 300, True), (777, 260, False), (130, 292, True)]:
+        g = torch.Generator(device=dev).manual_seed(5)
+        x = torch.randn(n, d, generator=g, device=dev) * 3 + 0.5
+        cnt = torch.randint(1, 40, (n,), generator=g, device=dev).float() if with_cnt else None
+        pc = torch.randn(1, d, generator=g, device=dev, dtype=torch.float64)
+        pc /= torch.linalg.norm(pc)
+        outs = []
+        for r in ("0", "4", "2", "8"):
+            with knobs(MMB_PC_REMOVE_R=r):
+                outs.append(P.remove_pc(x, cnt, pc).clone())
+                torch.cuda.synchronize()
+        for o in outs[1:]:
+            assert torch.equal(o, outs[0]), (n, d)
+        xs = x.double() / (cnt.double()[:, None] if with_cnt else 1.0)
+        ref = xs - (xs @ pc.T) @ pc
+        assert (outs[0].double() - ref).abs().max().item() <= 1e-6 * xs.abs().max().item()
+    print("remove rows: R = 0/2/4/8 bit-identical")
+
+
+def check_gram_schedules(dev):
+    """The int8 Gram's timing-only ablations are wrong by design; its product
+    schedule (MMB_GRAM_DIAG unset) must equal the product library's Gram --
+    checked here against the exact f64 Gram to the int8 format's 2e-9."""
+    x = torch.randn(5000, 300, device=dev) * 0.3
+    G8 = P.gram_i8(x, P.colmax(x))
+    G64 = P.gram(x, None)
+    torch.cuda.synchronize()
+    assert (G8 - G64).abs().max().item() <= 2e-9 * G64.abs().max().item()
+    print("gram: int8 schedule within 2e-9 of f64")
+
+
+GROUPS = {"projection": check_projection, "fused_streamer": check_fused_streamer,
+          "remove_rows": check_remove_rows, "gram": check_gram_schedules}
+
+
+def main(argv):
+    want = argv[1:] or list(GROUPS)
+    lib = os.path.basename(L.LIB_PATH)
+    if lib != "libmmb_diag.so":
+        print(f"variant_checks: needs the tools build (MMB_LIB_PATH=.../libmmb_diag.so), "
+              f"got {L.LIB_PATH}", file=sys.stderr)
+        return 2
+    L.require_gpu()
+    dev = torch.device("cuda", 0)
+    for g in want:
+        GROUPS[g](dev)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv))

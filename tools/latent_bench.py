@@ -162,6 +162,19 @@ def run(cfg, objective, gen, senti, lat0, label, dev, steps, batch, warm=2, grap
     return (time.perf_counter() - t0) / steps * 1e3
 
 
+class CpuSenti(torch.nn.Module):  # the reference regressor in plain torch (no libmmb on CPU)
+    def __init__(self, m):
+        super().__init__()
+        self.h = torch.nn.Linear(300, 100)
+        self.o = torch.nn.Linear(100, 1)
+        with torch.no_grad():
+            self.h.weight.copy_(m.hidden1.weight.cpu()), self.h.bias.copy_(m.hidden1.bias.cpu())
+            self.o.weight.copy_(m.out.weight.cpu()), self.o.bias.copy_(m.out.bias.cpu())
+
+    def forward(self, x):
+        return self.o(torch.relu(self.h(x))).squeeze()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
@@ -186,18 +199,6 @@ def main():
                    copy.deepcopy(senti), lat0, label, dev, args.steps, args.batch)
     cpu = torch.device("cpu")
     from oracle import latent_oracle as LO  # noqa: F401  (cpu leg: the reference arithmetic)
-
-    class CpuSenti(torch.nn.Module):  # the reference regressor in plain torch (no libmmb on CPU)
-        def __init__(self, m):
-            super().__init__()
-            self.h = torch.nn.Linear(300, 100)
-            self.o = torch.nn.Linear(100, 1)
-            with torch.no_grad():
-                self.h.weight.copy_(m.hidden1.weight.cpu()), self.h.bias.copy_(m.hidden1.bias.cpu())
-                self.o.weight.copy_(m.out.weight.cpu()), self.o.bias.copy_(m.out.bias.cpu())
-
-        def forward(self, x):
-            return self.o(torch.relu(self.h(x))).squeeze()
 
     ms_cpu = run(cfg, eager_objective(cfg, data, cpu), copy.deepcopy(gen).cpu(), CpuSenti(senti),
                  lat0, label, cpu, args.cpu_steps, args.batch, warm=1)

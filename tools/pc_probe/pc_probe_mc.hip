@@ -1,0 +1,83 @@
+// Phase timing of pc_solve_mc_kernel (wall_clock64 marks of workgroup 0,
+// MMB_PC_PROBE build) and its PC against the one-workgroup solve.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMMB_PC_PROBE -I../../include \
+//     pc_probe_mc.hip ../../multimodal-baselines_amd/csrc/host_rng.cpp -o pc_probe_mc
+#include "../../multimodal-baselines_amd/csrc/pc_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+int main() {
+  const int D = 300, k = 11, n = 4096;
+  std::mt19937_64 rng(1);
+  std::normal_distribution<double> nd;
+  std::vector<double> X(static_cast<size_t>(n) * D), G(D * D, 0.0), z0(D * k);
+  std::vector<double> g(D);
+  for (auto& v : g) v = nd(rng);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < D; ++j) X[i * D + j] = 0.4 * nd(rng) + 0.3 * g[j];
+  for (int i = 0; i < n; ++i)
+    for (int a = 0; a < D; ++a)
+      for (int b = 0; b < D; ++b) G[a * D + b] += X[i * D + a] * X[i * D + b];
+  for (auto& v : z0) v = nd(rng);
+  double *dG, *dz, *dpc;
+  void* ws;
+  int32_t* flag;
+  (void)hipMalloc(&dG, D * D * 8);
+  (void)hipMalloc(&dz, D * k * 8);
+  (void)hipMalloc(&dpc, D * 8);
+  (void)hipMalloc(&ws, mmb_pc_solve_mc_ws_bytes(D));
+  (void)hipMalloc(&flag, 4);
+  (void)hipMemset(flag, 0, 4);
+  (void)hipMemcpy(dG, G.data(), D * D * 8, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dz, z0.data(), D * k * 8, hipMemcpyHostToDevice);
+  int rate = 0;
+  (void)hipDeviceGetAttribute(&rate, hipDeviceAttributeWallClockRate, 0);  // kHz
+  for (int rep = 0; rep < 5; ++rep) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, 0);
+    const int rc = mmb_pc_solve_mc(dG, D, dz, k, 1, 7, 0, dpc, ws, flag, 0);
+    (void)hipEventRecord(b, 0);
+    (void)hipDeviceSynchronize();
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    unsigned long long t[64];
+    (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(mmb::g_pc_probe), sizeof(t));
+    auto us = [&](int i, int j) { return (double)(t[j] - t[i]) * 1e3 / rate; };
+    printf("rep %d rc %d: kernel+memset %.1f us | orth0 %.1f", rep, rc, ms * 1e3, us(0, 1));
+    int prev = 1;
+    for (int r = 0; r <= 7; ++r) {
+      printf(" | r%d prod %.1f wait %.1f gather %.1f", r, us(prev, 2 + 3 * r), us(2 + 3 * r, 3 + 3 * r),
+             us(3 + 3 * r, 4 + 3 * r));
+      if (r < 7) printf(" orth %.1f", us(4 + 3 * r, 2 + 3 * (r + 1)) - 0.0);
+      prev = 4 + 3 * r;
+    }
+    printf(" | tail-rr %.1f eig %.1f out %.1f\n", us(40, 41), us(41, 42), us(42, 43));
+  }
+  int32_t hflag = 0;
+  (void)hipMemcpy(&hflag, flag, 4, hipMemcpyDeviceToHost);
+  std::vector<double> pc(D), pc1(D);
+  (void)hipMemcpy(pc.data(), dpc, D * 8, hipMemcpyDeviceToHost);
+  for (int rep = 0; rep < 3; ++rep) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, 0);
+    mmb_pc_solve(dG, D, dz, k, 1, 7, 0, dpc, 0);
+    (void)hipEventRecord(b, 0);
+    (void)hipDeviceSynchronize();
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    printf("one-workgroup solve %.1f us\n", ms * 1e3);
+  }
+  (void)hipMemcpy(pc1.data(), dpc, D * 8, hipMemcpyDeviceToHost);
+  double md = 0;
+  for (int i = 0; i < D; ++i) md = std::max(md, std::fabs(pc[i] - pc1[i]));
+  printf("flag %d | pc[0..3] %.12f %.12f %.12f | max|mc - one-wg| %.3e\n", hflag, pc[0], pc[1], pc[2], md);
+  return 0;
+}
