@@ -1118,39 +1118,49 @@ __device__ __forceinline__ void p16_gz(const double* __restrict__ G, int D, int 
   }
 }
 
-// Cholesky W = L L^T (k x k, compact) and Linv = L^{-1} by one wave: lane i
-// keeps row i of the trailing matrix in registers (right-looking, column j's
-// multipliers broadcast by shuffles); lane c then solves L x = e_c.  *fail is
-// set if a pivot is not positive (the pivot is then replaced by 1).
-__device__ __forceinline__ void p16_chol(const double* sW, double* sL, double* sLi, int k, int lane, int* fail) {
-  double w[kMaxK], l[kMaxK];
-#pragma unroll
-  for (int m = 0; m < kMaxK; ++m) {
-    w[m] = (lane < k && m < k) ? sW[lane * k + m] : 0.0;
-    l[m] = 0.0;
-  }
+// 1 / sqrt(x) to f64 precision: the v_rsq_f64 estimate + two Newton steps
+// (r03: replaces sqrt + an f64 division per Cholesky pivot)
+__device__ __forceinline__ double rsqrt_f64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  y = y * fma(-h * y, y, 1.5);
+  y = y * fma(-h * y, y, 1.5);
+  return y;
+}
+
+// Cholesky of the k x k SPD matrix whose row `lane` (lane < k) is w[]
+// (registers; zero elsewhere): lane i keeps row i of the trailing matrix,
+// column j's multipliers broadcast by readlane, pivots inverted once
+// (rsqrt_f64).  Writes L (compact, sL) and L^{-1} (compact, sLi; lane c solves
+// L x = e_c with the reciprocal pivots) and returns, in x[], lane c's column
+// of L^{-1}.  *fail is set if a pivot is not positive (the pivot is then
+// replaced by 1).
+__device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, double* sLi, int k,
+                                              int lane, int* fail, double (&x)[kMaxK]) {
+  // L's columns and the reciprocal pivots go to LDS as they are produced
+  // (sLi's storage holds the pivots until the inverse overwrites it): at
+  // 1024 threads a wave has 128 VGPRs, and the arrays of L and 1 / L_jj held
+  // in registers spilled to scratch, one reload per substitution step
+  double* rl = sLi;
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < kMaxK; ++j) {
     if (j < k) {
       const double djj = readlane_f64(w[j], j);  // broadcast: no LDS round trip
       bad = bad || !(djj > 0.0);
-      const double s = sqrt(djj > 0.0 ? djj : 1.0);
-      const double lij = (lane == j) ? s : (lane > j ? w[j] / s : 0.0);
-      l[j] = lij;
+      const double p = djj > 0.0 ? djj : 1.0;
+      const double r = rsqrt_f64(p);
+      const double lij = (lane == j) ? p * r : (lane > j ? w[j] * r : 0.0);
+      if (lane < k) sL[lane * k + j] = lij;
+      if (lane == 0) rl[kMaxK * kMaxK - kMaxK + j] = r;  // the last row of sLi's storage
 #pragma unroll
       for (int m = j + 1; m < kMaxK; ++m) w[m] -= lij * readlane_f64(lij, m);
     }
   }
   if (bad && lane == 0) *fail = 1;
-  if (lane < k) {
-#pragma unroll
-    for (int m = 0; m < kMaxK; ++m)
-      if (m < k) sL[lane * k + m] = l[m];
-  }
   wave_lds_sync();
-  // column c = lane of Linv: forward substitution, L entries read as broadcasts
-  double x[kMaxK];
+  // column c = lane of Linv: forward substitution, L entries and the
+  // reciprocal pivots read as LDS broadcasts
 #pragma unroll
   for (int i = 0; i < kMaxK; ++i) {
     x[i] = 0.0;
@@ -1158,15 +1168,24 @@ __device__ __forceinline__ void p16_chol(const double* sW, double* sL, double* s
       double s = (i == lane) ? 1.0 : 0.0;
 #pragma unroll
       for (int m = 0; m < i; ++m) s -= sL[i * k + m] * x[m];
-      x[i] = s / sL[i * k + i];
+      x[i] = s * rl[kMaxK * kMaxK - kMaxK + i];
     }
   }
+  wave_lds_sync();  // every lane has read the pivots before sLi is written
   if (lane < k) {
 #pragma unroll
     for (int i = 0; i < kMaxK; ++i)
       if (i < k) sLi[i * k + lane] = (i < lane) ? 0.0 : x[i];
   }
   wave_lds_sync();
+}
+
+// Cholesky W = L L^T (k x k, compact, LDS) and Linv = L^{-1} by one wave.
+__device__ __forceinline__ void p16_chol(const double* sW, double* sL, double* sLi, int k, int lane, int* fail) {
+  double w[kMaxK], x[kMaxK];
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m) w[m] = (lane < k && m < k) ? sW[lane * k + m] : 0.0;
+  p16_chol_regs(w, sL, sLi, k, lane, fail, x);
 }
 
 // Top eigenvector of the symmetric positive semi-definite A (k x k, compact,
@@ -1197,6 +1216,10 @@ __device__ double p16_top_eig(const double* A, int k, int lane, double* u) {
     const double inv = tr > 0.0 ? 1.0 / tr : 0.0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) b[r] = acc[r] * inv;
+    // from the second squaring on trace(B) = 1, and trace(B B) = 1 exactly
+    // when B is rank one: B is then v v^T to rounding and more squarings
+    // change nothing (r03: 32 -> ~5 squarings on separated spectra, ~8 us)
+    if (it >= 1 && tr >= 1.0 - 1e-14) break;
   }
   // column with the largest diagonal entry (first index on ties)
   double dg = -1.0;
@@ -1307,7 +1330,7 @@ struct P16Small {
 // (extmath.py:537-566); the transposed branch takes A = Q^T G Q, v = Q u.
 __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int D, int Dp, int k,
                                          int npc, int transposed, double* part, const P16Small& sm,
-                                         double* __restrict__ pc_out) {
+                                         double* __restrict__ pc_out, const double* Hpre = nullptr) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   if (transposed) {
     p16_gram(Z, GZ, Dp, k, part, sm.A);  // Q^T G Q
@@ -1315,7 +1338,12 @@ __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int 
     __syncthreads();
   } else {
     p16_gram(Z, GZ, Dp, k, part, sm.W);   // W = Z^T G Z
-    p16_gram(GZ, GZ, Dp, k, part, sm.T);  // H = (GZ)^T (GZ)
+    if (Hpre) {                           // H = (GZ)^T (GZ), summed by the caller
+      if (threadIdx.x < k * k) sm.T[threadIdx.x] = Hpre[threadIdx.x];
+      __syncthreads();
+    } else {
+      p16_gram(GZ, GZ, Dp, k, part, sm.T);
+    }
     symmetrize(sm.W, k);
     symmetrize(sm.T, k);
     __syncthreads();
@@ -1508,6 +1536,47 @@ __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned
   return false;
 }
 
+// Out [Dp][16] = In [Dp][16] M^T for a 16 x 16 M (row-major, zero past k):
+// the 16-row tiles over the waves, 4 MFMA k-steps each.  In != Out.
+__device__ __forceinline__ void p16_rmul(const double* In, const double* M, double* Out, int Dp) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  for (int t = wave; t < Dp / 16; t += kP16NT / kWave) {
+    f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int m = 4 * st + (lane >> 4);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(In[(t * 16 + (lane & 15)) * kP16W + m],
+                                                 M[(lane & 15) * kP16W + m], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) Out[(t * 16 + (lane >> 4) + 4 * reg) * kP16W + (lane & 15)] = acc[reg];
+  }
+}
+
+// Wave 0: the equilibrated Cholesky factor of a block's Gram W (k x k
+// compact, LDS): d_j = 1 / sqrt(W_jj), d W d = L L^T, and on return
+// M = L^-1 diag(d) (16 x 16, zero past k) is the right factor that
+// orthonormalises the block: Z = B M^T (one CholeskyQR pass after
+// equilibration, from the Gram alone).  d[] = the scales.  All in registers
+// (lane i = row i); *fail as p16_chol.
+__device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* Li, double* M,
+                                            double* d, int k, int lane, int* fail) {
+  double w[kMaxK], x[kMaxK];
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m) w[m] = (lane < k && m < k) ? W[lane * k + m] : 0.0;
+  const double di = rsqrt_f64(lane < k ? W[lane * k + lane] : 1.0);
+#pragma unroll
+  for (int m = 0; m < kMaxK; ++m) w[m] *= di * readlane_f64(di, m);
+  if (lane < kMaxK) d[lane] = lane < k ? di : 0.0;
+  if (lane == 0) *fail = 0;
+  p16_chol_regs(w, L, Li, k, lane, fail, x);
+  if (lane < kP16W) {  // lane c: column c of L^-1 diag(d)
+#pragma unroll
+    for (int i = 0; i < kP16W; ++i) M[i * kP16W + lane] = (lane < k && i < k) ? x[i] * di : 0.0;
+  }
+  wave_lds_sync();
+}
+
 __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,
                                                                const double* __restrict__ z0, int k,
                                                                int npc, int n_iter, int transposed,
@@ -1517,11 +1586,11 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
   extern __shared__ __attribute__((aligned(16))) double p16_lds[];
   const int Dp = (D + 15) / 16 * 16;
   const int T = Dp / 16;
-  double* sZ = p16_lds;
-  double* sY = sZ + Dp * kP16W;
-  double* part = sY + Dp * kP16W;  // max(16 x 256, Dp x 16)
+  double* sZ = p16_lds;               // the orthonormal block (explicit rounds)
+  double* sY = sZ + Dp * kP16W;       // the raw block B_r (z0, then G Z_{r-1})
+  double* part = sY + Dp * kP16W;     // max(16 x 256, Dp x 16)
   P16_SMALL_DECL
-  __shared__ double sYt[256], sPt[256], sd[kMaxK];
+  __shared__ double sHt[256], sYt[256], sPt[256], sM[256], sM2[256], sd[kMaxK];
   __shared__ int s_abort;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -1540,26 +1609,14 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
       ga[j] = (p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
     }
   }
-  for (int e = tid; e < Dp * kP16W; e += kP16NT) {
-    const int p = e / kP16W, j = e % kP16W;
-    sZ[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
-    sY[e] = 0.0;
-  }
-  if (tid == 0) s_abort = 0;
-  __syncthreads();
-  PC_MARK(0);
-  // every workgroup orthonormalises the same start block: identical Z
-  p16_orth(sZ, D, Dp, k, part, sW, sL, sLi, &s_fail, n_iter > 0 ? 2 : 3);
-  PC_MARK(1);
-
-  for (int r = 0; r <= n_iter; ++r) {
-    // Y_t = G_t Z: this wave's k-steps, then a fixed-order sum over the waves
+  // this tile of G times a [Dp][16] block, summed over the waves in a fixed order
+  auto tile_product = [&](const double* B, double* out) {
     f64x4 acc = {0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < kPmKs; ++j) {
       const int q = 4 * (wave + 16 * j) + (lane >> 4);
       if (4 * (wave + 16 * j) < Dp)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], sZ[q * kP16W + (lane & 15)], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], B[q * kP16W + (lane & 15)], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
@@ -1568,10 +1625,99 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
       double s = 0.0;
 #pragma unroll
       for (int w = 0; w < kP16NT / kWave; ++w) s += part[w * 256 + tid];
-      sYt[tid] = s;
+      out[tid] = s;
     }
     __syncthreads();
-    if (wave == 0) {  // P_t = Y_t^T Y_t (16 rows, 4 k-steps)
+  };
+  // MGS^2 of the k columns of a [Dp][16] block on wave 0 (extreme
+  // ill-conditioning: a Cholesky pivot <= 0), in place
+  auto mgs = [&](double* B) {
+    if (wave == 0) {
+      for (int e = lane; e < D * k; e += kWave) part[e] = B[(e / k) * kP16W + e % k];
+      wave_lds_sync();
+      orth_wave(part, D, k, lane);
+      for (int e = lane; e < D * k; e += kWave) B[(e / k) * kP16W + e % k] = part[e];
+    }
+    __syncthreads();
+  };
+
+  for (int e = tid; e < Dp * kP16W; e += kP16NT) {
+    const int p = e / kP16W, j = e % kP16W;
+    sY[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
+    sZ[e] = 0.0;
+  }
+  if (tid == 0) s_abort = 0;
+  __syncthreads();
+  PC_MARK(0);
+  p16_gram(sY, sY, Dp, k, part, sW);  // W_0 = B_0^T B_0 (every workgroup: identical)
+  PC_MARK(1);
+
+  // Round r: the raw block B_r (sY) and its Gram W_r (sW) -> Z_r = orth(B_r)
+  // -> this tile of G Z_r -> exchange -> B_{r+1}, W_{r+1}.  Rounds r <
+  // n_iter orthonormalise implicitly: Z_r = B_r M^T, so G_t Z_r = (G_t B_r)
+  // M^T and no row of Z_r is formed.  Round n_iter (the block entering the
+  // Rayleigh-Ritz tail) forms Z explicitly with CholeskyQR2.
+  for (int r = 0; r <= n_iter; ++r) {
+    const bool last = r == n_iter;
+    if (wave == 0) p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);
+    __syncthreads();
+    PC_MARK(44 + 2 * r);
+    // explicit rows: a failed pivot (MGS^2), or the block entering the
+    // transposed branch's tail (an orthonormal Q: CholeskyQR2).  The direct
+    // branch's tail is a generalised eigenproblem on span(Z), invariant to
+    // the basis, so its last block stays implicit; workgroup 0 forms its
+    // rows for the tail.
+    const bool explicit_z = (last && transposed) || s_fail;
+    if (last && !explicit_z && t == 0) p16_rmul(sY, sM, sZ, Dp);  // Z = B M^T
+    if (explicit_z) {
+      if (s_fail) {  // the equilibrated rows, orthonormalised by MGS^2
+        for (int e = tid; e < D * kP16W; e += kP16NT) sZ[e] = sY[e] * (e % kP16W < k ? sd[e % kP16W] : 0.0);
+        __syncthreads();
+        mgs(sZ);
+      } else {
+        p16_rmul(sY, sM, sZ, Dp);  // Z1 = B M1^T
+        __syncthreads();
+        p16_gram(sZ, sZ, Dp, k, part, sW);  // second CholeskyQR pass on the rows
+        if (wave == 0) {
+          if (lane == 0) s_fail = 0;
+          wave_lds_sync();
+          p16_chol(sW, sL, sLi, k, lane, &s_fail);
+          for (int e = lane; e < 256; e += kWave) {
+            const int j = e / kP16W, m = e % kP16W;
+            sM2[e] = (j < k && m <= j) ? sLi[j * k + m] : 0.0;
+          }
+        }
+        __syncthreads();
+        if (s_fail) {
+          mgs(sZ);
+        } else {
+          p16_rmul(sZ, sM2, sY, Dp);  // Z = Z1 L2^-T (sY free: B is no longer needed)
+          __syncthreads();
+          for (int e = tid; e < Dp * kP16W; e += kP16NT) sZ[e] = sY[e];
+          __syncthreads();
+        }
+      }
+      tile_product(sZ, sYt);  // Y_t = G_t Z
+    } else {
+      tile_product(sY, sHt);  // H_t = G_t B_r
+      if (wave == 0) {        // Y_t = H_t M^T
+        f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const int m = 4 * st + (lane >> 4);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sHt[(lane & 15) * 16 + m], sM[(lane & 15) * 16 + m],
+                                                     acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) sYt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+      }
+    }
+    PC_MARK(45 + 2 * r);
+    // wave 0: P_t = Y_t^T Y_t, then publishes Y_t | P_t with write-through
+    // 8-byte stores, drains them and adds one arrival
+    double* xb = xbuf + static_cast<int64_t>(r & 1) * T * 512;
+    if (wave == 0) {
+      wave_lds_sync();
       f64x4 pa = {0, 0, 0, 0};
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
@@ -1580,25 +1726,25 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
       }
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) sPt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = pa[reg];
+      wave_lds_sync();
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = lane + kWave * u;
+        const double v = e < 256 ? sYt[e] : sPt[e - 256];
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(xb + t * 512 + e),
+                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(last && t != 0)) {
+          if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) s_abort = 1;
+        }
+      }
     }
-    __syncthreads();
-    // publish: write-through 8-byte stores, every storing wave drains, one arrival
-    double* xb = xbuf + static_cast<int64_t>(r & 1) * T * 512;
-    if (tid < 512) {
-      const double v = tid < 256 ? sYt[tid] : sPt[tid - 256];
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(xb + t * 512 + tid),
-                         __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (r == n_iter && t != 0) return;  // the tail runs on workgroup 0 only
+    if (last && t != 0) return;  // the tail runs on workgroup 0 only
     PC_MARK(2 + 3 * r);
-    if (tid == 0) {
-      if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) s_abort = 1;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
     __syncthreads();
     if (s_abort) return;
     PC_MARK(3 + 3 * r);
@@ -1616,10 +1762,9 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
         yv[u] = tt < T ? __builtin_bit_cast(double, __hip_atomic_load(src, __ATOMIC_RELAXED,
                                                                       __HIP_MEMORY_SCOPE_AGENT))
                        : 0.0;
-        pv[u] = (tt < T && r < n_iter)
-                    ? __builtin_bit_cast(double, __hip_atomic_load(src + 256, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT))
-                    : 0.0;
+        pv[u] = tt < T ? __builtin_bit_cast(double, __hip_atomic_load(src + 256, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT))
+                       : 0.0;
       }
       double ps = 0.0;
 #pragma unroll
@@ -1633,85 +1778,19 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
       part[g * 256 + e] = ps;
     }
     __syncthreads();
-    if (r < n_iter && tid < 256) {
+    if (tid < 256) {
       const double s = (part[tid] + part[256 + tid]) + (part[512 + tid] + part[768 + tid]);
       const int i = tid >> 4, j = tid & 15;
-      if (i < k && j < k) sW[i * k + j] = s;
+      if (i < k && j < k) sW[i * k + j] = s;  // W_{r+1}; after the last round H = Y^T Y
     }
     __syncthreads();
     PC_MARK(4 + 3 * r);
-    if (r == n_iter) break;
-    // equilibrated CholeskyQR of the product: d_j = 1 / |y_j|, W' = d W d
-    if (tid < k) sd[tid] = 1.0 / sqrt(sW[tid * k + tid]);
-    __syncthreads();
-    if (tid < k * k) sW[tid] *= sd[tid / k] * sd[tid % k];
-    for (int e = tid; e < D * kP16W; e += kP16NT) {
-      const int j = e % kP16W;
-      if (j < k) sY[e] *= sd[j];
-    }
-    __syncthreads();
-    if (wave == 0) {
-      if (lane == 0) s_fail = 0;
-      wave_lds_sync();
-      p16_chol(sW, sL, sLi, k, lane, &s_fail);
-    }
-    __syncthreads();
-    if (s_fail) {  // extreme ill-conditioning: MGS^2 on wave 0 (the same in every workgroup)
-      if (wave == 0) {
-        for (int e = lane; e < D * k; e += kWave) part[e] = sY[(e / k) * kP16W + e % k];
-        wave_lds_sync();
-        orth_wave(part, D, k, lane);
-        for (int e = lane; e < D * k; e += kWave) sY[(e / k) * kP16W + e % k] = part[e];
-      }
-      __syncthreads();
-      for (int e = tid; e < Dp * kP16W; e += kP16NT) sZ[e] = sY[e];
-    } else if (tid < D) {  // row p: z <- y L^{-T}
-      double y[kP16W];
-#pragma unroll
-      for (int m = 0; m < kP16W; ++m) y[m] = sY[tid * kP16W + m];
-      for (int j = 0; j < k; ++j) {
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m < kP16W; ++m)
-          if (m <= j) s += y[m] * sLi[j * k + m];
-        sZ[tid * kP16W + j] = s;
-      }
-    }
-    __syncthreads();
-    // the block entering the tail: a second CholeskyQR pass (local)
-    if (r == n_iter - 1 && !s_fail) {
-      p16_gram(sZ, sZ, Dp, k, part, sW);
-      if (wave == 0) {
-        if (lane == 0) s_fail = 0;
-        wave_lds_sync();
-        p16_chol(sW, sL, sLi, k, lane, &s_fail);
-      }
-      __syncthreads();
-      if (s_fail) {
-        if (wave == 0) {
-          for (int e = lane; e < D * k; e += kWave) part[e] = sZ[(e / k) * kP16W + e % k];
-          wave_lds_sync();
-          orth_wave(part, D, k, lane);
-          for (int e = lane; e < D * k; e += kWave) sZ[(e / k) * kP16W + e % k] = part[e];
-        }
-      } else if (tid < D) {
-        double z[kP16W];
-#pragma unroll
-        for (int m = 0; m < kP16W; ++m) z[m] = sZ[tid * kP16W + m];
-        for (int j = 0; j < k; ++j) {
-          double s = 0.0;
-#pragma unroll
-          for (int m = 0; m < kP16W; ++m)
-            if (m <= j) s += z[m] * sLi[j * k + m];
-          sZ[tid * kP16W + j] = s;
-        }
-      }
-      __syncthreads();
-    }
   }
-  // workgroup 0: sY = G Z of the final block
+  // workgroup 0: sZ = the final block, sY = G Z, sW = (G Z)^T (G Z)
+  for (int e = tid; e < k * k; e += kP16NT) sT[e] = sW[e];
+  __syncthreads();
   PC_MARK(40);
-  p16_tail(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out);
+  p16_tail(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT);
 }
 
 inline size_t p16_lds_bytes(int d) {

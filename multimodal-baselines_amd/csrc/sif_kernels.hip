@@ -1017,6 +1017,23 @@ __device__ __forceinline__ void frame_piece(const float* base, int W, int L, int
 // projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
 // no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
 // the frames (constant sums: the projectors alone)
+#ifdef MMB_DIAG
+// tools build only: per-workgroup wall-clock marks of the fused kernel
+// (start; each streamer wave's and each projector wave's end), read back with
+// mmb_diag_fused_probe -- the spread of finishing times across the CUs
+constexpr int kFProbe = 9;
+__device__ unsigned long long g_fused_probe[1024 * kFProbe];
+#define FUSED_PROBE(slot)                                                              \
+  do {                                                                                 \
+    if ((threadIdx.x & (kWave - 1)) == 0 && blockIdx.x < 1024)                         \
+      g_fused_probe[blockIdx.x * kFProbe + (slot)] = wall_clock64();                   \
+  } while (0)
+#else
+#define FUSED_PROBE(slot) \
+  do {                    \
+  } while (0)
+#endif
+
 template <int UNR, bool NT, int DIAG = 0, int PIPE = 0, int SL = kGSlots>
 __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_fused_kernel(
     FusedArgs f) {
@@ -1035,6 +1052,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   int* abort_flag = ctr + 6;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
   if (tid < 8) ctr[tid] = 0;
+  if (tid == 0) FUSED_PROBE(0);
   __syncthreads();
   const int64_t N = a.N;
   const int G = gridDim.x;
@@ -1544,6 +1562,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         if (uu < (D >> 2)) st4(a.cmax_part + wid * D + 4 * uu, cmx[c]);
       }
     }
+    FUSED_PROBE(1 + wave);
     return;
   }
 
@@ -1754,6 +1773,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
     }
   }
+  FUSED_PROBE(1 + wave);
 }
 
 template <int DIAG, int UNR = 8, int PIPE = 0, int SL = kGSlots>
@@ -2167,3 +2187,18 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
+
+#ifdef MMB_DIAG
+// tools build: copy the fused kernel's per-workgroup wall-clock marks
+// [1024][9] (start, streamer waves 0-3 end, projector waves 4-7 end) and the
+// wall-clock rate (kHz) to the host
+extern "C" int mmb_diag_fused_probe(unsigned long long* host_out, int* rate_khz) {
+  MMB_REQUIRE(host_out && rate_khz);
+  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_fused_probe), sizeof(g_fused_probe));
+  if (e != hipSuccess) return static_cast<int>(e);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  e = hipDeviceGetAttribute(rate_khz, hipDeviceAttributeWallClockRate, dev);
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+#endif

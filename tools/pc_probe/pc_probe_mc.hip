@@ -49,12 +49,11 @@ int main() {
     unsigned long long t[64];
     (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(mmb::g_pc_probe), sizeof(t));
     auto us = [&](int i, int j) { return (double)(t[j] - t[i]) * 1e3 / rate; };
-    printf("rep %d rc %d: kernel+memset %.1f us | orth0 %.1f", rep, rc, ms * 1e3, us(0, 1));
+    printf("rep %d rc %d: kernel+memset %.1f us | gram0 %.1f", rep, rc, ms * 1e3, us(0, 1));
     int prev = 1;
     for (int r = 0; r <= 7; ++r) {
-      printf(" | r%d prod %.1f wait %.1f gather %.1f", r, us(prev, 2 + 3 * r), us(2 + 3 * r, 3 + 3 * r),
-             us(3 + 3 * r, 4 + 3 * r));
-      if (r < 7) printf(" orth %.1f", us(4 + 3 * r, 2 + 3 * (r + 1)) - 0.0);
+      printf(" | r%d chol %.1f prod %.1f pub+wait %.1f gather %.1f", r, us(prev, 44 + 2 * r),
+             us(44 + 2 * r, 45 + 2 * r), us(45 + 2 * r, 2 + 3 * r), us(3 + 3 * r, 4 + 3 * r));
       prev = 4 + 3 * r;
     }
     printf(" | tail-rr %.1f eig %.1f out %.1f\n", us(40, 41), us(41, 42), us(42, 43));

@@ -17,6 +17,8 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the MMB_* knobs these runs flip live in the tools build (make -C multimodal-baselines_amd/csrc diag)
+os.environ.setdefault("MMB_LIB_PATH", os.path.join(ROOT, "multimodal-baselines_amd", "libmmb_diag.so"))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-baselines_amd"))
 
 import torch  # noqa: E402
