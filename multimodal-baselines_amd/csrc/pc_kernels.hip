@@ -1520,7 +1520,8 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
 // r + 2 write needs every workgroup past round r + 1's wait, hence done
 // reading round r), then the arrival counter and the abort word (zeroed by
 // the launcher before every launch).
-constexpr int kPmKs = 5;  // k-steps of G per wave: ceil(kP16MaxD / 4 / 16)
+constexpr int kPmPw = 15;  // waves holding G (wave 15 runs the Cholesky meanwhile)
+constexpr int kPmKs = 6;   // k-steps of G per wave: ceil(kP16MaxD / 4 / kPmPw)
 constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
 
 __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned* abort_w,
@@ -1598,36 +1599,46 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
   unsigned* ctr = ctl;
   unsigned* abort_w = ctl + 1;
 
-  // this workgroup's 16 rows of G as MFMA A fragments (G symmetric: row p of
-  // the tile = column p, 16 consecutive doubles per k-row: coalesced)
+  // this workgroup's 16 rows of G as MFMA A fragments on waves 0-14 (G
+  // symmetric: row p of the tile = column p, 16 consecutive doubles per k-row:
+  // coalesced); wave 15 is free for the k x k work that overlaps the product
   double ga[kPmKs];
   {
     const int p = t * 16 + (lane & 15);
 #pragma unroll
     for (int j = 0; j < kPmKs; ++j) {
-      const int q = 4 * (wave + 16 * j) + (lane >> 4);
-      ga[j] = (p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
+      const int q = 4 * (wave + kPmPw * j) + (lane >> 4);
+      ga[j] = (wave < kPmPw && p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
     }
   }
-  // this tile of G times a [Dp][16] block, summed over the waves in a fixed order
-  auto tile_product = [&](const double* B, double* out) {
-    f64x4 acc = {0, 0, 0, 0};
+  // waves 0-14: their partial products of this tile of G with a [Dp][16] block
+  auto tile_partials = [&](const double* B) {
+    if (wave < kPmPw) {
+      f64x4 acc = {0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < kPmKs; ++j) {
-      const int q = 4 * (wave + 16 * j) + (lane >> 4);
-      if (4 * (wave + 16 * j) < Dp)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], B[q * kP16W + (lane & 15)], acc, 0, 0, 0);
+      for (int j = 0; j < kPmKs; ++j) {
+        const int q = 4 * (wave + kPmPw * j) + (lane >> 4);
+        if (4 * (wave + kPmPw * j) < Dp)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], B[q * kP16W + (lane & 15)], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
     }
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
-    __syncthreads();
+  };
+  // ... summed over the waves in a fixed order (after a barrier)
+  auto tile_sum = [&](double* out) {
     if (tid < 256) {
       double s = 0.0;
 #pragma unroll
-      for (int w = 0; w < kP16NT / kWave; ++w) s += part[w * 256 + tid];
+      for (int w = 0; w < kPmPw; ++w) s += part[w * 256 + tid];
       out[tid] = s;
     }
     __syncthreads();
+  };
+  auto tile_product = [&](const double* B, double* out) {
+    tile_partials(B);
+    __syncthreads();
+    tile_sum(out);
   };
   // MGS^2 of the k columns of a [Dp][16] block on wave 0 (extreme
   // ill-conditioning: a Cholesky pivot <= 0), in place
@@ -1659,7 +1670,14 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
   // Rayleigh-Ritz tail) forms Z explicitly with CholeskyQR2.
   for (int r = 0; r <= n_iter; ++r) {
     const bool last = r == n_iter;
-    if (wave == 0) p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);
+    // the equilibrated Cholesky of W on wave 15 while waves 0-14 form this
+    // tile's partial products with the raw block B (G_t B: all the implicit
+    // path needs before M)
+    if (wave == kPmPw) {
+      p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);
+    } else {
+      tile_partials(sY);
+    }
     __syncthreads();
     PC_MARK(44 + 2 * r);
     // explicit rows: a failed pivot (MGS^2), or the block entering the
@@ -1699,8 +1717,8 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
       }
       tile_product(sZ, sYt);  // Y_t = G_t Z
     } else {
-      tile_product(sY, sHt);  // H_t = G_t B_r
-      if (wave == 0) {        // Y_t = H_t M^T
+      tile_sum(sHt);    // H_t = G_t B_r (its partials formed beside the Cholesky)
+      if (wave == 0) {  // Y_t = H_t M^T
         f64x4 acc = {0, 0, 0, 0};
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
