@@ -801,10 +801,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="synthetic", choices=["synthetic", "pom", "ragged"],
+    ap.add_argument("--workload", default="synthetic", choices=["synthetic", "pom", "ragged", "mosi"],
                     help="synthetic: BASELINE configs[3] (the metric's workload); pom: configs[2] "
                          "shape (V=7763, transcripts padded to 1357, ~370 tokens); ragged: "
-                         "configs[3] with Poisson(40) lengths in [1, 64]")
+                         "configs[3] with Poisson(40) lengths in [1, 64]; mosi: configs[1] shape "
+                         "(T = 20, A = 76, Vd = 48, V = 3016; also in configs_measured)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
                     help="strong (default): one split of --utts utterances sharded over the "
                          "ranks; weak: --utts (or --utts-per-gpu) utterances per rank")
@@ -880,7 +881,8 @@ def main():
     mmb_lib.require_gpu()
     kind = args.workload
     dflt = {"synthetic": (1_000_000, 40, 400_000), "pom": (10_000, 1357, 7763),
-            "ragged": (1_000_000, 64, 400_000)}[kind]
+            "ragged": (1_000_000, 64, 400_000), "mosi": (1_000_000, 20, 3016)}[kind]
+    A, Vd = (76, 48) if kind == "mosi" else (300, 300)
     scaling = args.scaling or ("weak" if args.utts_per_gpu else "strong")
     T = args.tokens or dflt[1]
     V = args.vocab or dflt[2]
@@ -893,6 +895,8 @@ def main():
         U_total, row0 = U * world, U * rank
     if kind == "synthetic":
         inp = synth.device_shard(row0, U, T, V, D=D, A=300, Vd=300, seed=1000, device=dev)
+    elif kind == "mosi":  # mosi_mmb2_config's inputs
+        inp = synth.device_workload(U, T, V, D=D, A=A, Vd=Vd, seed=4000 + rank, device=dev)
     else:  # N = 1 configs (their own generators: ragged lengths, POM transcripts)
         inp = synth.device_workload(U, T, V, D=D, A=300, Vd=300, seed=1000 + rank, device=dev,
                                     mean_len=370.0 if kind == "pom" else None,
@@ -900,10 +904,10 @@ def main():
         inp.pop("lengths", None)
     ids = inp["ids"]
     text_rows = None
-    if kind != "synthetic":
+    if kind in ("pom", "ragged"):
         text_rows = (ids != 0).sum().item() / U + (ids == 0).any(1).float().mean().item()
     torch.manual_seed(0)
-    gen = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None).to(dev)
+    gen = models.AudioVisualGeneratorMultimodal(D, A, Vd, norm=None).to(dev)
 
     def allreduce(t):
         dist.all_reduce(t)
@@ -948,14 +952,16 @@ def main():
     utts_per_launch = U // len(step.bounds) if len(step.bounds) > 1 else U
     kb, kname = dominant_kernel(step, T, D, text_rows=text_rows)
     roof = stream_roofline(phase_ms, traces, args.steps, kb, utts_per_launch, kname, kind, T)
-    pb = path_bytes(T, D, 300, 300, text_rows=text_rows)
+    pb = path_bytes(T, D, A, Vd, text_rows=text_rows)
     mfma = mfma_rooflines(step, phase_ms, U, D)
     wl = {"synthetic": "configs[3]: synthetic utterances x 40 tokens/frames x 3 modalities x "
                        "300d, V = 400k, Zipf(1.1) ids, SIF(+PC removal) + closed-form MMB2",
           "pom": "configs[2]: POM-shaped (V=7763, w0=1.0, transcripts padded to 1357, ~370 "
                  "tokens, aligned frames) x 3 modalities x 300d, SIF(+PC removal) + MMB2",
           "ragged": "configs[3] ragged: Poisson(40) lengths in [1, 64], padded with id 0 / -10 "
-                    "frames, 3 x 300d, V = 400k, SIF(+PC removal) + MMB2"}[kind]
+                    "frames, 3 x 300d, V = 400k, SIF(+PC removal) + MMB2",
+          "mosi": "configs[1] MOSI-shaped: T = 20, A = 76, Vd = 48, V = 3016, Zipf(1.1) ids, "
+                  "SIF(+PC removal) + closed-form MMB2"}[kind]
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -971,7 +977,7 @@ def main():
         "dtype": DTYPE,
         "data": "synthetic (seeded, generated in HBM; no dataset or checkpoint)",
         "config": {"workload": wl, "utts_total": U_total, "utts_rank0": U, "tokens": T,
-                   "vocab": V, "dims": [D, 300, 300],
+                   "vocab": V, "dims": [D, A, Vd],
                    "parallelism": f"dp{world} (contiguous utterance shards of one split, "
                                   f"{scaling} scaling) + one all-reduce of the 300x300 fp64 Gram "
                                   f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo'})"
@@ -1021,7 +1027,7 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         n_cpu = args.cpu_sample if T <= 64 else max(1, args.cpu_sample * 40 // T)
         sample = host_sample(inp, n_cpu)
-    gen_cpu = models.AudioVisualGeneratorMultimodal(D, 300, 300, norm=None)
+    gen_cpu = models.AudioVisualGeneratorMultimodal(D, A, Vd, norm=None)
     gen_cpu.load_state_dict({k: v.cpu() for k, v in gen.state_dict().items()})
     del step, inp, ids
     torch.cuda.empty_cache()

@@ -55,8 +55,7 @@ def _worker(rank, world, port, case_path, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    z = np.load(case_path)
-    X = z["emb"].astype(np.float32)
+    X = np.load(case_path).astype(np.float32)  # the split's a2 rows
     n_total = X.shape[0]
     row0, n = D.shard_range(n_total, world, rank)
     # num/cnt as the stream kernel leaves them: any split with num/cnt == X works
@@ -70,9 +69,8 @@ def _worker(rank, world, port, case_path, out_path):
 
 @pytest.mark.parametrize("case,world", [("g2_mosi", 2), ("g1_pom_valid", 2), ("g2_mosi", 3)])
 def test_sharded_pc_gloo(golden, tmp_path, case, world):
-    from conftest import GOLDEN
-
-    case_path = os.path.join(GOLDEN, case + ".npz")
+    case_path = str(tmp_path / "emb.npy")
+    np.save(case_path, golden(case)["emb"])
     out = str(tmp_path / "pc_{}.npy")
     mp.start_processes(_worker, args=(world, _free_port(), case_path, out), nprocs=world,
                        join=True, start_method="spawn")
