@@ -4,7 +4,7 @@
 #   PART a: every -m gpu test, smoke(), the default bench line, rocprofv3
 #           --kernel-trace --stats of the headline bench (--only-main) at the
 #           1M split and at the 125k per-rank size of the 8-GPU curve
-#   PART b: per workload (synthetic configs[3], ragged configs[3], POM
+#   PART b: per workload (synthetic configs[3], ragged configs[3], POM configs[2], MOSI configs[1]
 #           configs[2]): separate PMC passes FETCH_SIZE and WRITE_SIZE
 #           (MI355X_MICROARCH.md §HBM: separate passes; gfx950 FETCH_SIZE counts
 #           half of wide reads), and rocprofv3 --kernel-trace --stats of the
@@ -34,7 +34,7 @@ if [ "$PART" = a ]; then
     -- python3 "$REPO/bench.py" --utts 125000 --steps 20 --warmup 3 --only-main --no-cpu-baseline > "$OUT/trace125k_bench.json" 2> "$OUT/trace125k.err"; ok $?
 else
   cd /tmp
-  for W in synthetic ragged pom; do
+  for W in synthetic ragged pom mosi; do
     for C in FETCH_SIZE WRITE_SIZE; do
       timeout -k 10 600 rocprofv3 --kernel-trace --pmc $C -d "$OUT/pmc_${W}_${C}" -o run --output-format csv \
         -- python3 "$REPO/bench.py" --workload $W --steps 2 --warmup 1 --only-main --no-cpu-baseline > "$OUT/pmc_${W}_${C}.json" 2> "$OUT/pmc_${W}_${C}.err"; ok $?
