@@ -626,10 +626,12 @@ def per_rank_steps(P, inp, gen, steps, warmup, sizes):
 def mosi_mmb2_config(P, models, synth, dev, steps, warmup, U=1_000_000):
     """configs[1]: MMB2 at MOSI shape -- T = 20 aligned frames, COVAREP 74 + 2
     positional dims = 76, FACET 46 + 2 = 48 (make_configs.py:28),
-    V = 3016 (sif_functions.py:48) -- on 1M synthetic utterances, the fused
-    step (SIF + MMB2).  The 3.6 MB word table sits in L2 / Infinity Cache, so
-    the roofline is given on algorithmic bytes (text rows counted) and on the
-    bytes that must come from HBM (text rows excluded)."""
+    V = 3016 (sif_functions.py:48) -- on 1M synthetic utterances, the step
+    FusedStep picks for these frame widths (pipeline.fused_pays: the
+    two-kernel step, stream kernel + projection, 1.5x the fused kernel's rate
+    at 76 / 48-float frames).  The 3.6 MB word table sits in L2 / Infinity
+    Cache, so the roofline is given on algorithmic bytes (text rows counted)
+    and on the bytes that must come from HBM (text rows excluded)."""
     import torch
 
     T, V, D, A, Vd = 20, 3016, 300, 76, 48

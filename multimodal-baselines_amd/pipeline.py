@@ -432,6 +432,22 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
     return num, s, aux
 
 
+# Narrowest frame row (floats) for which the fused stream + projection step is
+# the default: its 4 streaming waves per CU load every modality row as 16-B
+# columns on 64 lanes, so a frame row under 256 floats leaves lanes idle and
+# costs as many load round trips as a full one, while the two-kernel step's
+# stream kernel (one wave per utterance, no LDS ring) keeps more loads in
+# flight.  Measured (r03t, tools/step_ab.py, 500k-1M utterances, ms per
+# step fused / two-kernel): A = 76, Vd = 48 at T = 20 / 40 / 64: 12.3 / 8.0,
+# 8.7 / 5.8, 11.9 / 7.8 (V = 3016); 6.6 / 4.2 (V = 400k, T = 20); A = Vd = 300
+# at T = 30 / 40: 10.3 / 11.0, 12.2 / 12.7 (V = 400k).
+FUSED_MIN_FRAME = 256
+
+
+def fused_pays(a: int, vd: int) -> bool:
+    return min(a, vd) >= FUSED_MIN_FRAME
+
+
 def stream_project_supported(t: int, d: int, a: int, vd: int) -> bool:
     """Shapes the fused stream + projection kernel takes (t <= 64 frames,
     256 <= d < 320, widths % 4, k <= 1920): the bench / MOSI-like configs."""
@@ -601,9 +617,11 @@ class FusedStep:
         self.x = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.s_half = x3_supported(self.proj)
         # stream + projection in one kernel (s never in HBM): one chunk, the
-        # shapes the kernel takes; MMB_STREAM_PROJECT=0 keeps the two kernels
+        # shapes the kernel takes, and wide frames (fused_pays);
+        # MMB_STREAM_PROJECT=0 / 1 forces the two kernels / the fused one
         if stream_project is None:
-            stream_project = os.environ.get("MMB_STREAM_PROJECT", "1") != "0"
+            env = os.environ.get("MMB_STREAM_PROJECT")
+            stream_project = fused_pays(self.a, self.vd) if env is None else env != "0"
         self.stream_project = (bool(stream_project) and (chunks or 1) == 1 and self.s_half
                                and stream_project_supported(self.t, self.d, self.a, self.vd))
         self.s = None if self.stream_project else s_buffer(self.n, kp, self.s_half, dev)

@@ -106,7 +106,7 @@ def test_compensated_arithmetic_vs_reference_fp32(gpu, golden, case):
               "wtab": torch.tensor(weights, device=gpu, dtype=torch.float32),
               "ids": torch.as_tensor(ids, dtype=torch.int32, device=gpu),
               "audio": torch.tensor(audio, device=gpu), "visual": torch.tensor(visual, device=gpu)}
-    step = P.FusedStep(inputs, gen.to(gpu).networks())
+    step = P.FusedStep(inputs, gen.to(gpu).networks(), stream_project=True)
     assert step.stream_project
     fused = step.run()[1].cpu().numpy()
     A, Vd = audio.shape[-1], visual.shape[-1]
@@ -641,3 +641,29 @@ def test_stream_project_repeatable_and_unit_rows(gpu):
     assert torch.equal(s1, s2) and torch.equal(m1, m2)
     norms = torch.linalg.norm(m1.double(), dim=1)
     assert (norms - 1).abs().max().item() < 1e-5
+
+
+def test_default_step_at_mosi_widths_is_two_kernel(gpu):
+    """configs[1] frame widths (COVAREP 76, FACET 48): FusedStep's default is
+    the two-kernel step (pipeline.fused_pays), its rows within the bar of the
+    CPU oracle (SIF) and of the reference's gpu2 restatement (MMB2)."""
+    from oracle import sif_oracle as O
+
+    N, T, A, Vd, V = 3000, 20, 76, 48, 3016
+    inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=63, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
+    step = P.FusedStep(inp, gen.networks())
+    assert not step.stream_project and step.s is not None
+    trace = {}
+    s1, m1 = step.run(trace=trace, check=True)
+    assert "mm2_stream" in trace and "mm2_stream_project" not in trace
+    E = inp["table"].cpu().numpy()
+    wt = inp["wtab"].cpu().numpy().astype(np.float64)
+    ids = inp["ids"].cpu().numpy().astype(np.int64)
+    assert M.row_rel_err(s1.cpu().numpy(), O.get_sentence_embeddings(E, wt, ids)) < TOL
+    audio, visual = inp["audio"].cpu().numpy(), inp["visual"].cpu().numpy()
+    sw = np.where(ids >= 0, wt.astype(np.float32)[ids], 0).astype(np.float32)
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(E[ids], audio, visual),
+                                            M.params_from_module(gen.cpu()), sw, E[ids])
+    assert M.row_rel_err(m1.cpu().numpy(), ref) < TOL
