@@ -1524,9 +1524,19 @@ constexpr int kPmPw = 15;  // waves holding G (wave 15 runs the Cholesky meanwhi
 constexpr int kPmKs = 6;   // k-steps of G per wave: ceil(kP16MaxD / 4 / kPmPw)
 constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
 
+#ifdef MMB_DIAG
+// tools build: a test shortens the bounded waits to drive the timeout path
+// (mmb_diag_pc_wait_iters)
+__device__ int g_pm_wait_iters = 1 << 20;
+#endif
 __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned* abort_w,
                                         int32_t* flag) {
-  for (int it = 0; it < (1 << 20); ++it) {
+#ifdef MMB_DIAG
+  const int iters = g_pm_wait_iters;
+#else
+  constexpr int iters = 1 << 20;
+#endif
+  for (int it = 0; it < iters; ++it) {
     if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
     if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     __builtin_amdgcn_s_sleep(4);
@@ -2342,3 +2352,13 @@ extern "C" int mmb_pc_remove_f64(const double* x, int64_t n, int d, const double
   if (per <= 8) return launch_remove<1, 8, double>(x, nullptr, n, d, pc, npc, nullptr, out64, stream);
   return MMB_EINVAL;
 }
+
+#ifdef MMB_DIAG
+// tools build: the multi-workgroup solve's bounded-wait budget (1 << 20 in
+// the product)
+extern "C" int mmb_diag_pc_wait_iters(int iters) {
+  MMB_REQUIRE(iters >= 1);
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_pm_wait_iters), &iters, sizeof(int));
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+#endif

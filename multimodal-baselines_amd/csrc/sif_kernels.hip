@@ -861,9 +861,23 @@ struct FusedArgs {
   int balanced;            // rows past the last full round split evenly over the workgroups
 };
 
+#ifdef MMB_DIAG
+// tools build: a test shortens the bounded waits to drive the timeout path
+// (mmb_diag_fused_wait_iters)
+__device__ int g_fused_wait_iters = 1 << 23;
+#endif
+__device__ __forceinline__ int fused_wait_iters() {
+#ifdef MMB_DIAG
+  return g_fused_wait_iters;
+#else
+  return 1 << 23;
+#endif
+}
+
 // bounded wait for *p >= target (workgroup scope); false once anything timed out
 __device__ __forceinline__ bool fused_wait(int* p, int target, int* abort_flag, int32_t* gflag) {
-  for (int it = 0; it < (1 << 23); ++it) {
+  const int iters = fused_wait_iters();
+  for (int it = 0; it < iters; ++it) {
     if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       return true;
@@ -2189,6 +2203,13 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
 }
 
 #ifdef MMB_DIAG
+// tools build: the bounded waits' iteration budget (1 << 23 in the product)
+extern "C" int mmb_diag_fused_wait_iters(int iters) {
+  MMB_REQUIRE(iters >= 1);
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_fused_wait_iters), &iters, sizeof(int));
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+
 // tools build: copy the fused kernel's per-workgroup wall-clock marks
 // [1024][9] (start, streamer waves 0-3 end, projector waves 4-7 end) and the
 // wall-clock rate (kHz) to the host

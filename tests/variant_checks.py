@@ -193,8 +193,58 @@ def check_gram_schedules(dev):
     print("gram: int8 schedule within 2e-9 of f64")
 
 
+def check_timeouts(dev):
+    """The bounded hand-over waits' timeout path, driven by cutting the tools
+    build's wait budget to one poll (mmb_diag_fused_wait_iters /
+    mmb_diag_pc_wait_iters): the fused stream + projection kernel and the
+    multi-workgroup PC solve end (no hang), report MMB_FLAG_SYNC_TIMEOUT, and
+    FusedStep.check raises RuntimeError; with the product budget restored
+    the same step and solve reproduce their results bit for bit."""
+    lib = L.load()
+    inp = synth.device_workload(20_000, 40, 20_000, seed=81, device=dev)
+    step = P.FusedStep(inp, _gen(dev).networks(), stream_project=True)
+    assert step.stream_project
+    s0, m0 = [t.clone() for t in step.run(check=True)]
+    try:
+        assert lib.mmb_diag_fused_wait_iters(1) == 0
+        step.run()
+        torch.cuda.synchronize()
+        assert int(step.flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT
+        try:
+            step.check()
+        except RuntimeError as e:
+            assert "timed out" in str(e)
+        else:
+            raise AssertionError("FusedStep.check did not raise on the hand-over timeout")
+    finally:
+        assert lib.mmb_diag_fused_wait_iters(1 << 23) == 0
+    step.reset()
+    s1, m1 = step.run(check=True)
+    assert torch.equal(s0, s1) and torch.equal(m0, m1)
+
+    G = step.G.clone()
+    z0 = torch.randn((300, 11), dtype=torch.float64, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    pc0 = P.pc_solve(G, z0, 1, False, flag=flag).clone()
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 0
+    try:
+        assert lib.mmb_diag_pc_wait_iters(1) == 0
+        P.pc_solve(G, z0, 1, False, flag=flag)
+        torch.cuda.synchronize()
+        assert int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT
+    finally:
+        assert lib.mmb_diag_pc_wait_iters(1 << 20) == 0
+    flag.zero_()
+    pc1 = P.pc_solve(G, z0, 1, False, flag=flag)
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 0 and torch.equal(pc0, pc1)
+    print("timeouts: fused kernel and PC solve end, flag the timeout, recover bit for bit")
+
+
 GROUPS = {"projection": check_projection, "fused_streamer": check_fused_streamer,
-          "remove_rows": check_remove_rows, "gram": check_gram_schedules}
+          "remove_rows": check_remove_rows, "gram": check_gram_schedules,
+          "timeouts": check_timeouts}
 
 
 def main(argv):
