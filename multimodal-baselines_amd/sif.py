@@ -18,68 +18,74 @@ from sif_functions import seq2weight
 
 
 def get_word_weights(word_freq_file, a=1e-3):
-    """sif.py:14-32 — weight(word) = a / (a + count/N) from a 'word count' file."""
-    word_weights = {}
-    N = 0
-    with open(word_freq_file, "r") as f:
-        for line in f:
-            line = line.strip()
-            if len(line) > 0:
-                line = line.split()
-                if len(line) == 2:
-                    word_weights[line[0]] = float(line[1])
-                    N += float(line[1])
-                else:
-                    print(line)
-    for key, value in word_weights.items():
-        word_weights[key] = a / (a + value / N)
-    return word_weights
+    """sif.py:14-32 -- SIF weight a / (a + p(w)) with p(w) = count / total count,
+    read from a "word count" file.  Blank lines are skipped; a line that is not
+    exactly two fields is echoed (as the list of its fields) and ignored; a word
+    listed twice keeps its last count but both counts enter the total."""
+    counts = {}
+    total = 0.0
+    with open(word_freq_file, "r") as fh:
+        for fields in (ln.split() for ln in fh):
+            if not fields:
+                continue
+            if len(fields) != 2:
+                print(fields)
+                continue
+            word, c = fields[0], float(fields[1])
+            counts[word] = c
+            total += c
+    return {word: a / (a + c / total) for word, c in counts.items()}
+
+
+# dataset -> the .npy weight table the reference loads (sif.py:34-50)
+_WEIGHT_FILES = {"pom": "pom/pom_word_weights.npy", "iemocap": "iemocap/iemocap_word_weights.npy"}
+
+
+def _load_table(path):
+    table = np.load(path).squeeze()
+    print(table.shape)
+    return table
 
 
 def load_weights(args):
-    """sif.py:34-42."""
-    if args["dataset"] == "mosi":
+    """sif.py:34-42: the dataset's word-weight table (NotImplementedError for
+    any other dataset name)."""
+    name = args["dataset"]
+    if name == "mosi":
         return load_mosi_weights()
-    elif args["dataset"] == "pom":
-        return load_pom_weights()
-    elif args["dataset"] == "iemocap":
-        return load_iemocap_weights()
+    if name in _WEIGHT_FILES:
+        return _load_table(_WEIGHT_FILES[name])
     raise NotImplementedError
 
 
 def load_pom_weights():
-    weights = np.load("pom/pom_word_weights.npy").squeeze()
-    print(weights.shape)
-    return weights
+    return _load_table(_WEIGHT_FILES["pom"])
 
 
 def load_iemocap_weights():
-    weights = np.load("iemocap/iemocap_word_weights.npy").squeeze()
-    print(weights.shape)
-    return weights
+    return _load_table(_WEIGHT_FILES["iemocap"])
 
 
 def load_mosi_weights(word2ix=None, word_freq_file="SIF/auxiliary_data/enwiki_vocab_min200.txt"):
     """sif.py:52-76.  The reference regenerates word_weights.npy from a word
     frequency file using a `word2ix` it never defines (sif.py:63, NameError);
     here the mapping is an explicit argument and the same rule is applied
-    (unknown words weigh 1.0)."""
-    if os.path.isfile("word_weights.npy"):
-        return np.load("word_weights.npy", allow_pickle=False).squeeze()
+    (lower-cased lookup; unknown words weigh 1.0)."""
+    cached = "word_weights.npy"
+    if os.path.isfile(cached):
+        return np.load(cached, allow_pickle=False).squeeze()
     if word2ix is None:
         raise NameError("word_weights.npy is absent and no word2ix mapping was given "
                         "(the reference fails here too: sif.py:63)")
-    word_weights = get_word_weights(word_freq_file)
-    weights = np.zeros((max(word2ix.values()) + 1))
-    unk = 0
-    for word, ix in word2ix.items():
-        if word.lower() not in word_weights:
-            weights[ix] = 1.0
-            unk += 1
-        else:
-            weights[ix] = word_weights[word.lower()]
-    print("# of words with unknown weight", unk)
-    np.save("word_weights.npy", weights, allow_pickle=False)
+    freq = get_word_weights(word_freq_file)
+    weights = np.zeros(max(word2ix.values()) + 1)  # indices no word maps to stay 0
+    n_unknown = 0
+    for word, ix in word2ix.items():  # later entries win on a shared index, as in the reference
+        w = freq.get(word.lower())
+        n_unknown += w is None
+        weights[ix] = 1.0 if w is None else w
+    print("# of words with unknown weight", n_unknown)
+    np.save(cached, weights, allow_pickle=False)
     return weights
 
 

@@ -157,3 +157,23 @@ def test_fused_step_dispatch_by_frame_width():
 
     assert P.fused_pays(300, 300) and P.fused_pays(256, 512)
     assert not P.fused_pays(76, 48) and not P.fused_pays(300, 48) and not P.fused_pays(255, 300)
+
+
+def test_word_weights_file_and_mosi_table(tmp_path, monkeypatch, capsys):
+    """sif.py:14-76: a / (a + count / total) per word; malformed lines echoed and
+    skipped; the MOSI table by lower-cased lookup, unknown words 1.0, unmapped
+    indices 0, cached to word_weights.npy."""
+    import sif
+
+    f = tmp_path / "freq.txt"
+    f.write_text("the 600\n\nof 300\nbad line here\ncat 100\n")
+    ww = sif.get_word_weights(str(f), a=1e-3)
+    assert capsys.readouterr().out.strip() == "['bad', 'line', 'here']"
+    assert ww == {w: 1e-3 / (1e-3 + c / 1000.0) for w, c in (("the", 600.0), ("of", 300.0), ("cat", 100.0))}
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(NameError):
+        sif.load_mosi_weights()
+    tab = sif.load_mosi_weights({"The": 1, "dog": 2, "CAT": 4}, word_freq_file=str(f))
+    np.testing.assert_array_equal(tab, [0.0, ww["the"], 1.0, 0.0, ww["cat"]])
+    assert "# of words with unknown weight 1" in capsys.readouterr().out
+    np.testing.assert_array_equal(sif.load_mosi_weights(), tab)  # the cached table
