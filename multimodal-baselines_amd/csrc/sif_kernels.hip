@@ -10,6 +10,7 @@
 // image per accumulator in a fixed order (deterministic), and only the
 // reductions leave the chip: the [N,L,300] gathered text tensor the reference
 // materialises (simplesif.py:319-340, :871) never exists.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -697,6 +698,269 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   }
 }
 
+// ------------------------------------------------------ narrow-frame stream
+// MMB2 stream kernel for narrow frame rows (MOSI: COVAREP A = 76, FACET
+// Vd = 48 -- 19 and 12 float4 units).  utt_wave_kernel gives every frame row
+// its own wave-instruction, so at these widths 19 / 12 of the 64 lanes load
+// (304 / 192 B per instruction) and a wave moves ~2 KB per HBM round trip:
+// latency-bound at ~2.9 TB/s.  Here a wave-instruction covers P = 64 / U
+// consecutive frame rows (lane -> frame slot f = lane / U, unit c = lane % U:
+// 3 rows = 912 contiguous bytes of audio, 5 rows = 960 B of visual; lanes past
+// P U load a duplicate), and ALL of an utterance's frame instructions (7 + 4
+// at T = 20) are issued together, before its text groups: one HBM round trip
+// per utterance for ~10 KB.  The
+// token ids of the next utterance are loaded one utterance ahead and its
+// weights gathered before the loop turns, so a text group waits for nothing
+// but the (L2-resident at MOSI's V = 3016) table rows.
+// Sums: the text sums (and so x, aux's count and weight sum, the column
+// bounds) are utt_wave_kernel's operations in its order: bit-identical.  The
+// frame sums (FR = 1, the product) are per-lane partials over the rows of one
+// slot (f, f + P, f + 2P, ...) added slot 0 + 1 + ... at the end -- another
+// f32 summation order than the wave kernel's t = 0, 1, ... (within f32
+// rounding of it; the reference's torch sum over T fixes no order either).
+// FR = 0 gathers every frame across the packed lanes (ds_bpermute) in t order
+// instead: bit-identical to the wave kernel, 0.5 ms slower at MOSI (r03z).
+// GA / GV: frame instructions per modality issued at once (7 + 4 = all of a
+// T = 20 MOSI utterance; longer utterances take further groups after the text)
+// ABL (tools build, timing-only ablations with wrong outputs): bit 0 skips the
+// text rows, bit 1 the frames, bit 2 the row stores (kept live behind a test
+// no value passes)
+// FR: 0 = frames gathered frame by frame (ds_bpermute, the wave kernel's
+// order), 1 = per-lane slot partials combined slot 0 + 1 + ... at the end.
+// ORD: 0 = utterances round robin over the waves, 1 = a contiguous range per
+// wave (neighbouring x / s / aux rows written by one wave: whole lines).
+template <int CT, int UNR, int GA_MAX, int GV_MAX, int OCC = 2, int ABL = 0, int FR = 0, int ORD = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void utt_narrow_kernel(StreamArgs a) {
+  const int lane = threadIdx.x & (kWave - 1);
+  // the wave index made visibly wave-uniform: utterance bases stay in SGPRs
+  const int64_t wid = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) +
+                      __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * (blockDim.x / kWave);
+  const int L = a.L, D = a.D;
+  const int UT = D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
+  const int PA = kWave / UA, PV = kWave / UV;  // frame rows per instruction (>= 2)
+  const int GA = (L + PA - 1) / PA, GV = (L + PV - 1) / PV;
+  // Loads go through buffer descriptors: a scalar offset per row / per packed
+  // instruction and a fixed per-lane column offset -- no 64-bit address
+  // arithmetic in VGPRs.  A row id < 0 (out of range, flagged) reads past the
+  // table's record count, which returns zeros (a zero row, as the wave
+  // kernel's select).  Text column offsets clamped into the row (lanes past
+  // unit 74 read a duplicate the L1 coalesces and never store it).
+  int vt[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) vt[c] = 16 * min(lane + kWave * c, UT - 1);
+  const int tbytes = static_cast<int>(a.V * D * 4);
+  const auto trsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.table), 0, tbytes, 0x00020000);
+  // lane f U + c of a packed frame instruction: frame row f, unit c
+  const int voa = ((lane / UA) * a.A + 4 * (lane % UA)) * 4;
+  const int vov = ((lane / UV) * a.Vd + 4 * (lane % UV)) * 4;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 cmx[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) cmx[c] = z4;
+
+  // token t of utterance i on lane t: the raw id (prefetched one utterance
+  // ahead), then stage_token's semantics
+  auto ld_id = [&](int64_t i) -> int { return (i < a.N && lane < L) ? a.ids[i * L + lane] : -1; };
+  // (the weight gather is issued here and first waited for by the text loop,
+  // behind the frame loads: the wave sums of the weights come after the text;
+  // an id outside [0, V) -- a negative one wraps for its ROW only -- reads
+  // past the weight table's record count: weight 0 with no select)
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wtab), 0,
+                                                       static_cast<int>(a.V * 4), 0x00020000);
+  auto resolve = [&](int raw, int& rid, float& w) {
+    rid = -1;
+    w = 0.f;
+    if (lane < L) {
+      int64_t id = raw;
+      const bool in = id >= 0 && id < a.V;
+      w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                        wrsrc, in ? static_cast<int>(id) * 4 : static_cast<int>(a.V * 4), 0, 0));
+      if (id < 0) id += a.V;
+      if (id < 0 || id >= a.V) {
+        if (a.flag) atomicOr(a.flag, MMB_FLAG_ID_RANGE);
+      } else {
+        rid = static_cast<int>(id);
+      }
+    }
+  };
+  const int64_t chunk = (a.N + nw - 1) / nw;
+  const int64_t i_beg = ORD ? wid * chunk : wid;
+  const int64_t i_end = ORD ? min(a.N, i_beg + chunk) : a.N;
+  const int64_t i_step = ORD ? 1 : nw;
+  int raw = i_beg < i_end ? ld_id(i_beg) : -1;
+  for (int64_t i = i_beg; i < i_end; i += i_step) {
+    int rid;
+    float w;
+    resolve(raw, rid, w);
+    raw = i + i_step < i_end ? ld_id(i + i_step) : -1;  // next utterance's ids: in flight through this one
+
+    // frames: the first GA_MAX / GV_MAX packed instructions per modality
+    // issued before the text loop (rows past L read zeros past the record count)
+    const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.audio + i * L * a.A), 0,
+                                                         L * a.A * 4, 0x00020000);
+    const auto vrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.visual + i * L * a.Vd), 0,
+                                                         L * a.Vd * 4, 0x00020000);
+    float4 sa = z4, saa = z4, sv = z4, svv = z4;
+    auto frames = [&](auto gmax, auto rsrc, int vo, int W, int U, int P, int g0, float4& s1, float4& s2) {
+      constexpr int GM = decltype(gmax)::value;
+      float4 v[GM > 0 ? GM : 1];
+#pragma unroll
+      for (int g = 0; g < GM; ++g)  // non-temporal: read-once streams
+        v[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, (g0 + g) * P * W * 4, 2));
+      // frame t = g P + q of unit c sits on lane q U + c: lane c < U adds the
+      // frames in order t = 0, 1, ... (ds_bpermute), the order of
+      // utt_wave_kernel / the fused kernel's frame_piece -- bit-identical sums
+      const int c = lane % U;
+      const bool mine = lane < P * U;
+      return [=, &s1, &s2]() {
+#pragma unroll
+        for (int g = 0; g < GM; ++g) {
+          if constexpr (FR == 1) {  // rows past L read zeros
+            if (mine) {
+              add4(s1, v[g]);
+              sq4(s2, v[g]);
+            }
+            continue;
+          }
+          for (int q = 0; q < P; ++q) {
+            if ((g0 + g) * P + q >= L) break;
+            const int src = min(q * U + c, kWave - 1);
+            float4 x;
+            x.x = __shfl(v[g].x, src, kWave);
+            x.y = __shfl(v[g].y, src, kWave);
+            x.z = __shfl(v[g].z, src, kWave);
+            x.w = __shfl(v[g].w, src, kWave);
+            add4(s1, x);
+            sq4(s2, x);
+          }
+        }
+      };
+    };
+    using GAc = std::integral_constant<int, GA_MAX>;
+    using GVc = std::integral_constant<int, GV_MAX>;
+    using G0 = std::integral_constant<int, 0>;
+    auto acc_a = frames(std::conditional_t<(ABL & 2) != 0, G0, GAc>{}, arsrc, voa, a.A, UA, PA, 0, sa, saa);
+    auto acc_v = frames(std::conditional_t<(ABL & 2) != 0, G0, GVc>{}, vrsrc, vov, a.Vd, UV, PV, 0, sv, svv);
+
+    // text: utt_sums' text half, the same operations in the same order
+    float4 num[CT], sx[CT], sxx[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) num[c] = sx[c] = sxx[c] = z4;
+    auto row = [&](int t, float4 (&v)[CT]) {
+      const int r = __builtin_amdgcn_readlane(rid, t);
+      const int so = r >= 0 ? r * D * 4 : tbytes;  // out of range: a zero row
+#pragma unroll
+      for (int c = 0; c < CT; ++c)
+        v[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
+    };
+    // (the weight is read at accumulation: its gather is waited for there)
+    auto accum = [&](int t, const float4 (&v)[CT]) {
+      const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        fma4(num[c], wt, v[c]);
+        add4(sx[c], v[c]);
+        sq4(sxx[c], v[c]);
+      }
+    };
+    int t = (ABL & 1) ? L : 0;
+    for (; t + UNR <= L; t += UNR) {
+      float4 v[UNR][CT];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) row(t + u, v[u]);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) accum(t + u, v[u]);
+    }
+    for (; t < L; ++t) {
+      float4 v[CT];
+      row(t, v);
+      accum(t, v);
+    }
+    acc_a();
+    acc_v();
+    const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+    const float sw = wave_sum(w);
+    if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+    if constexpr ((ABL & 2) == 0)
+    for (int g0 = GA_MAX; g0 < GA; g0 += GA_MAX) frames(GAc{}, arsrc, voa, a.A, UA, PA, g0, sa, saa)();
+    if constexpr ((ABL & 2) == 0)
+    for (int g0 = GV_MAX; g0 < GV; g0 += GV_MAX) frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, g0, sv, svv)();
+    if constexpr (FR == 1) {  // slot partials -> unit totals on lanes < U, slot 0 + 1 + ...
+      auto slots = [&](float4& acc, int U, int P) {
+        float4 r = acc;
+        for (int f = 1; f < P; ++f) {
+          const int src = min(lane + f * U, kWave - 1);
+          float4 o;
+          o.x = __shfl(acc.x, src, kWave);
+          o.y = __shfl(acc.y, src, kWave);
+          o.z = __shfl(acc.z, src, kWave);
+          o.w = __shfl(acc.w, src, kWave);
+          add4(r, o);
+        }
+        acc = r;
+      };
+      slots(sa, UA, PA);
+      slots(saa, UA, PA);
+      slots(sv, UV, PV);
+      slots(svv, UV, PV);
+    }
+    // lanes past a modality's units summed duplicates: keep them out of the row max
+    if (lane >= UA) sa = saa = z4;
+    if (lane >= UV) sv = svv = z4;
+
+    float m = fmaxf(fmaxf(amax4(sa), amax4(saa)), fmaxf(amax4(sv), amax4(svv)));
+#pragma unroll
+    for (int c = 0; c < CT; ++c) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
+    const float rs = row_scale(wave_max(m));
+    if ((ABL & 4) != 0 && rs != 3.f) continue;  // (never 3: a power of two)
+    _Float16* hrow = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * a.Kp;
+    auto put = [&](int f, float4 v) { split_store4<false>(hrow + f, hrow + a.Kp + f, v, rs); };
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int u = lane + kWave * c;
+      if (u < UT) {
+        const float4 xr = div4(num[c], cnt);
+        st4(a.num_out + i * D + 4 * u, xr);  // x = the a2 row
+        cmx[c] = bmax4(cmx[c], xr);
+        put(4 * u, sx[c]);
+        put(D + 4 * u, sxx[c]);
+      }
+    }
+    if (lane < UA) {
+      put(2 * D + 4 * lane, sa);
+      put(2 * D + a.A + 4 * lane, saa);
+    }
+    if (lane < UV) {
+      put(2 * (D + a.A) + 4 * lane, sv);
+      put(2 * (D + a.A) + a.Vd + 4 * lane, svv);
+    }
+    for (int f = 2 * (D + a.A + a.Vd) + lane; f < a.Kp; f += kWave)
+      hrow[f] = hrow[a.Kp + f] = static_cast<_Float16>(0.f);
+    if (lane == 0) {
+      a.aux_out[i] = cnt;  // planar [3][N]: count | sum w | fp16 row scale
+      a.aux_out[a.N + i] = sw;
+      a.aux_out[2 * a.N + i] = rs;
+    }
+  }
+  if (a.cmax_part) {  // this wave's column bounds (mmb_gram_i8)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int u = lane + kWave * c;
+      if (u < UT) st4(a.cmax_part + wid * D + 4 * u, cmx[c]);
+    }
+  }
+}
+
+// the narrow kernel's shapes: gathered ids with the weight table, fp16 s,
+// text rows of 65-128 float4 units (CT = 2; the MOSI / bench D = 300), frame
+// rows of at most 32 units (two or more rows per instruction), T <= 64
+static bool narrow_ok(const StreamArgs& a) {
+  return a.ids && a.wtab && !a.w_dense && a.s_half && a.D > 256 && a.D <= 512 &&
+         a.A <= 128 && a.Vd <= 128 && a.L <= kWave && a.V * a.D * 4 < (int64_t{1} << 31) &&
+         a.L * std::max(a.A, a.Vd) * 4 < (int64_t{1} << 31);
+}
+
 // colmax[f] = max over the P partial rows (float bits; non-negative floats
 // order like their bits), fixed order.  16 row groups per column, LDS reduce.
 __global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __restrict__ part, int P,
@@ -771,8 +1035,58 @@ static int stream_grid_mult() {
 // rows of the column-bound partials (one per wave / workgroup of a launch)
 constexpr int kCmaxRows = 8192;
 
+// Narrow-frame kernel variant (MMB_STREAM_NARROW, tools build; the product
+// runs 10).  Measured (r03z, MOSI 1M x 20, A = 76, Vd = 48, V = 3016, same
+// process, stream kernel ms): utt_wave_kernel (0) 5.04; frames gathered frame
+// by frame, 4 / 5 text rows per load group (2 / 3) 4.41 / 4.34; 10 rows at
+// occupancy 2 (4) 4.74; 5 rows forced to 4 waves per SIMD (5, spills) 5.15;
+// slot-partial frame sums (10) 3.81; contiguous utterance ranges per wave (11
+// = 3, 12 = 10 with it) no change; 8-row groups (13, occupancy 2) 4.41.
+// Timing-only ablations of 3 (wrong rows): no text 3.14 (6), no frames 2.32
+// (7), no row stores 3.61 (8), neither text nor frames 1.41 (9).
+static int narrow_variant() {
+#ifdef MMB_DIAG
+  const char* e = getenv("MMB_STREAM_NARROW");  // re-read per launch (in-process A/B)
+  return e ? atoi(e) : 10;
+#else
+  return 10;
+#endif
+}
+
+static int launch_narrow(const StreamArgs& a, hipStream_t stream, int* parts) {
+  const int var = narrow_variant();
+  // resident workgroups of 4 waves per CU at each variant's occupancy
+  const int per_cu = (var == 4 || var == 13) ? 2 : var == 5 ? 4 : 3;
+  const int64_t blocks = ceil_div(a.N, 4);
+  int grid_cap = per_cu * stream_cu_count(stream);
+  if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;
+  const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
+  if (parts) *parts = grid * 4;
+#ifdef MMB_DIAG
+  switch (var) {
+    case 2: utt_narrow_kernel<2, 4, 7, 4, 2><<<grid, 256, 0, stream>>>(a); break;
+    case 3: utt_narrow_kernel<2, 5, 7, 4, 2><<<grid, 256, 0, stream>>>(a); break;
+    case 4: utt_narrow_kernel<2, 10, 7, 4, 2><<<grid, 256, 0, stream>>>(a); break;
+    case 5: utt_narrow_kernel<2, 5, 7, 4, 4><<<grid, 256, 0, stream>>>(a); break;
+    case 6: utt_narrow_kernel<2, 5, 7, 4, 2, 1><<<grid, 256, 0, stream>>>(a); break;
+    case 7: utt_narrow_kernel<2, 5, 7, 4, 2, 2><<<grid, 256, 0, stream>>>(a); break;
+    case 8: utt_narrow_kernel<2, 5, 7, 4, 2, 4><<<grid, 256, 0, stream>>>(a); break;
+    case 9: utt_narrow_kernel<2, 5, 7, 4, 2, 3><<<grid, 256, 0, stream>>>(a); break;
+    case 11: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 0, 1><<<grid, 256, 0, stream>>>(a); break;
+    case 12: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
+    case 13: utt_narrow_kernel<2, 8, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
+    default: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a); break;
+  }
+#else
+  utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a);
+#endif
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
 template <bool MM2, int CT, int CA, int CV>
 static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nullptr) {
+  if (MM2 && narrow_ok(a) && narrow_variant() > 0) return launch_narrow(a, stream, parts);
   const int64_t blocks = ceil_div(a.N, 4);
   int grid_cap = stream_grid_mult() * stream_cu_count(stream);
   if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 import torch
 
+import mmb_lib as L
 import models
 import pipeline as P
 import sif2
@@ -76,7 +77,10 @@ def test_fused_id_path_equals_dense_path(gpu, golden, case):
     proj = P.MMB2Projection(gen.to(gpu).networks(), 300, A, Vd, t, gpu)
     num, s, aux = P.mm2_stream(n, t, 300, A, Vd, au, vi, ids32=ids32, table=table, wtab32=wtab)
     fused = P.mm2_project(s, num, aux, proj)
-    assert torch.equal(fused, dense)
+    if max(A, Vd) <= 128:  # the narrow-frame kernel: frame sums in another f32 order
+        assert M.row_rel_err(fused.cpu().numpy(), dense.cpu().numpy()) < 1e-6
+    else:
+        assert torch.equal(fused, dense)
 
 
 FP32_RATIO = 5.0  # measured 2.3-4.2x (r03d, tools/precision_probe.py)
@@ -667,3 +671,66 @@ def test_default_step_at_mosi_widths_is_two_kernel(gpu):
     ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(E[ids], audio, visual),
                                             M.params_from_module(gen.cpu()), sw, E[ids])
     assert M.row_rel_err(m1.cpu().numpy(), ref) < TOL
+
+
+@pytest.mark.parametrize("N,T,A,Vd,V", [(3000, 20, 76, 48, 3016), (1001, 40, 76, 48, 3016),
+                                        (517, 64, 128, 100, 5000), (64, 7, 20, 8, 300),
+                                        (259, 33, 44, 124, 400_000), (5, 1, 76, 48, 3016)])
+def test_narrow_frame_stream_kernel(gpu, N, T, A, Vd, V):
+    """The narrow-frame stream kernel (utt_narrow_kernel: frame rows of <= 32
+    float4 units packed 2-32 rows per wave-instruction, every frame load of an
+    utterance issued at once; fp16 s) against utt_wave_kernel (the fp32-s
+    stream of the same inputs): the text sums are the same operations in the
+    same order, so x, count, weight sum and the column bounds are
+    bit-identical; the frame sums (per-slot partials added slot by slot) and
+    the dequantised fp16 hi + lo text sums equal the fp32 sums to f32
+    rounding.
+    Ragged ids with negative (wrapping) and out-of-range ids (flagged) mixed
+    in; T past one issue group (40, 64 frames: later groups after the text)."""
+    rng = np.random.default_rng(N)
+    inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=70 + T, device=gpu)
+    ids = inp["ids"].clone()
+    if N > 10:
+        r = torch.as_tensor(rng.integers(0, N, 5), device=gpu)
+        ids[r, 0] = -3  # wraps to V - 3, like numpy fancy indexing
+    table, wtab = inp["table"], inp["wtab"]
+    proj = P.MMB2Projection(models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu).networks(),
+                            300, A, Vd, T, gpu)
+    f1 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    f2 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    cm1 = torch.zeros(300, dtype=torch.int32, device=gpu)
+    cm2 = torch.zeros(300, dtype=torch.int32, device=gpu)
+    nb = L.query("mmb_mm2_colmax_ws_bytes", 300)
+    ws1 = torch.empty((nb + 15) // 16 * 16, dtype=torch.uint8, device=gpu)
+    ws2 = torch.empty_like(ws1)
+    num, s, aux = P.mm2_stream(N, T, 300, A, Vd, inp["audio"], inp["visual"], ids32=ids, table=table,
+                               wtab32=wtab, flag=f1, colmax=cm1, colmax_ws=ws1)
+    num32, s32, aux32 = P.mm2_stream(N, T, 300, A, Vd, inp["audio"], inp["visual"], ids32=ids,
+                                     table=table, wtab32=wtab, s_half=False, flag=f2, colmax=cm2,
+                                     colmax_ws=ws2)
+    torch.cuda.synchronize()
+    assert s.dtype == torch.float16 and s.shape == (N, 2 * proj.kp)
+    assert torch.equal(num, num32) and torch.equal(aux[:2], aux32[:2])
+    assert torch.equal(cm1, cm2) and int(f1.item()) == int(f2.item()) == 0
+    k = 2 * (300 + A + Vd)
+    deq = (s[:, :k].double() + s[:, proj.kp:proj.kp + k].double()) / aux[2][:, None].double()
+    ref = s32[:, :k].double()
+    err = (deq - ref).abs().amax(1) / ref.abs().amax(1).clamp_min(1e-30)
+    assert err.max().item() < 2e-6
+    assert (s[:, k:proj.kp] == 0).all() and (s[:, proj.kp + k:] == 0).all()
+    # the row scale is the power of 2 of the row max: equal but where the max
+    # sits within rounding of a power of two
+    assert (aux[2] == aux32[2]).float().mean().item() > 0.99
+    # an out-of-range id: flagged, the row contributes nothing (as in the wave kernel)
+    bad = ids.clone()
+    bad[N // 2, 0] = V + 7
+    f3 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    n3, _, a3 = P.mm2_stream(N, T, 300, A, Vd, inp["audio"], inp["visual"], ids32=bad, table=table,
+                             wtab32=wtab, flag=f3)
+    f4 = torch.zeros(1, dtype=torch.int32, device=gpu)
+    n4, _, a4 = P.mm2_stream(N, T, 300, A, Vd, inp["audio"], inp["visual"], ids32=bad, table=table,
+                             wtab32=wtab, s_half=False, flag=f4)
+    torch.cuda.synchronize()
+    assert int(f3.item()) == int(f4.item()) and int(f3.item()) & L.MMB_FLAG_ID_RANGE
+    # (an utterance left with no valid token is 0 / 0 = NaN in both, as in numpy)
+    assert torch.allclose(n3, n4, rtol=0, atol=0, equal_nan=True) and torch.equal(a3[:2], a4[:2])
