@@ -335,8 +335,13 @@ def dominant_kernel(step, T, D, text_rows=None):
                 "utt_fused_kernel (mmb_mm2_stream_project: 4 streaming waves, one per "
                 "utterance, two 8-frame load groups in flight, + 4 projecting waves per CU, "
                 "sums in an LDS ring)")
-    kname = ("utt_wave_kernel (mmb_mm2_stream, one wave per utterance)" if T <= 64
-             else "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)")
+    if T > 64:
+        kname = "utt_stream_kernel (mmb_mm2_stream, one workgroup per utterance)"
+    elif max(step.a, step.vd) <= 128 and step.d > 256:
+        kname = ("utt_narrow_kernel (mmb_mm2_stream for narrow frame rows: 2-32 frame rows per "
+                 "wave-instruction, one wave per utterance)")
+    else:
+        kname = "utt_wave_kernel (mmb_mm2_stream, one wave per utterance)"
     return stream_kernel_bytes(T, D, step.a, step.vd, text_rows=text_rows), kname
 
 
@@ -643,10 +648,19 @@ def mosi_mmb2_config(P, models, synth, dev, steps, warmup, U=1_000_000):
     kb, kname = dominant_kernel(step, T, D)
     roof = stream_roofline(ph, traces, steps, kb, U, kname + f", T = {T}, A = {A}, Vd = {Vd}",
                            "mosi", T)
+    # The 3.6 MB table is L2 / Infinity-Cache resident (its rows are 24 KB of
+    # the 38.7 KB per utterance): on all algorithmic bytes the kernel runs
+    # above the HBM peak, so the HBM roofline is stated on the bytes HBM must
+    # deliver (text rows excluded); the all-bytes rate is kept beside it.
     hbm_b = kb - 4 * D * T
-    roof["hbm_bytes_per_utt_excl_table"] = hbm_b
-    roof["hbm_frac_excl_table"] = round(hbm_b * U / (roof["avg_launch_ms"] / 1e3) / 1e9
-                                        / HBM_PEAK_GBS, 4)
+    hbm_ach = hbm_b * U / (roof["avg_launch_ms"] / 1e3) / 1e9
+    roof.update({"achieved_incl_table": roof["achieved"], "frac_incl_table": roof["frac"],
+                 "algorithmic_bytes_per_utt_incl_table": roof["algorithmic_bytes_per_utt"],
+                 "achieved": round(hbm_ach, 1), "frac": round(hbm_ach / HBM_PEAK_GBS, 4),
+                 "algorithmic_bytes_per_utt": hbm_b,
+                 "bytes_note": "achieved / frac on the HBM bytes (ids, weights, frames read; a2 "
+                               "row, frame sums, aux written); the word-table rows come from "
+                               "L2 / Infinity Cache (*_incl_table counts them)"})
     out = {"workload": f"configs[1] MOSI-shaped: T = {T}, A = {A} (COVAREP 74 + 2 pos), Vd = {Vd} "
                        f"(FACET 46 + 2 pos), V = {V}, Zipf(1.1) ids, U(-1, 1) frames, SIF(+PC "
                        "removal) + closed-form MMB2",

@@ -729,7 +729,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 // order), 1 = per-lane slot partials combined slot 0 + 1 + ... at the end.
 // ORD: 0 = utterances round robin over the waves, 1 = a contiguous range per
 // wave (neighbouring x / s / aux rows written by one wave: whole lines).
-template <int CT, int UNR, int GA_MAX, int GV_MAX, int OCC = 2, int ABL = 0, int FR = 0, int ORD = 0>
+// TX = 1: the text rows' last column load (units 64..) issued on its live
+// lanes only (exec-masked; the other lanes' sums are kept out of the row max)
+template <int CT, int UNR, int GA_MAX, int GV_MAX, int OCC = 2, int ABL = 0, int FR = 0, int ORD = 0,
+          int TX = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void utt_narrow_kernel(StreamArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   // the wave index made visibly wave-uniform: utterance bases stay in SGPRs
@@ -788,12 +791,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
   const int64_t i_beg = ORD ? wid * chunk : wid;
   const int64_t i_end = ORD ? min(a.N, i_beg + chunk) : a.N;
   const int64_t i_step = ORD ? 1 : nw;
-  int raw = i_beg < i_end ? ld_id(i_beg) : -1;
+  // The next utterance's ids are loaded at the top of an iteration and
+  // resolved (row ids, weight gather issued) at its end BEFORE its row stores:
+  // with loads and stores both pending, gfx9's one vmcnt counter makes any
+  // wait a wait for everything (s_waitcnt vmcnt(0)), so an iteration that
+  // began by waiting for its ids waited for the previous row's stores too.
+  int rid_n, raw = -1;
+  float w_n;
+  resolve(i_beg < i_end ? ld_id(i_beg) : -1, rid_n, w_n);
   for (int64_t i = i_beg; i < i_end; i += i_step) {
-    int rid;
-    float w;
-    resolve(raw, rid, w);
-    raw = i + i_step < i_end ? ld_id(i + i_step) : -1;  // next utterance's ids: in flight through this one
+    const int rid = rid_n;
+    float w = w_n;
+    if (i + i_step < i_end) raw = ld_id(i + i_step);  // in flight through this utterance
 
     // frames: the first GA_MAX / GV_MAX packed instructions per modality
     // issued before the text loop (rows past L read zeros past the record count)
@@ -851,8 +860,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const int r = __builtin_amdgcn_readlane(rid, t);
       const int so = r >= 0 ? r * D * 4 : tbytes;  // out of range: a zero row
 #pragma unroll
-      for (int c = 0; c < CT; ++c)
+      for (int c = 0; c < CT; ++c) {
+        if (TX && c == CT - 1 && lane + kWave * c >= UT) continue;
         v[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
+      }
     };
     // (the weight is read at accumulation: its gather is waited for there)
     auto accum = [&](int t, const float4 (&v)[CT]) {
@@ -911,8 +922,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 
     float m = fmaxf(fmaxf(amax4(sa), amax4(saa)), fmaxf(amax4(sv), amax4(svv)));
 #pragma unroll
-    for (int c = 0; c < CT; ++c) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
+    for (int c = 0; c < CT; ++c)
+      if (!TX || lane + kWave * c < UT) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
     const float rs = row_scale(wave_max(m));
+    resolve(raw, rid_n, w_n);  // the next utterance's (see above)
     if ((ABL & 4) != 0 && rs != 3.f) continue;  // (never 3: a power of two)
     _Float16* hrow = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * a.Kp;
     auto put = [&](int f, float4 v) { split_store4<false>(hrow + f, hrow + a.Kp + f, v, rs); };
@@ -1041,7 +1054,10 @@ constexpr int kCmaxRows = 8192;
 // by frame, 4 / 5 text rows per load group (2 / 3) 4.41 / 4.34; 10 rows at
 // occupancy 2 (4) 4.74; 5 rows forced to 4 waves per SIMD (5, spills) 5.15;
 // slot-partial frame sums (10) 3.81; contiguous utterance ranges per wave (11
-// = 3, 12 = 10 with it) no change; 8-row groups (13, occupancy 2) 4.41.
+// = 3, 12 = 10 with it) no change; 8-row groups (13, occupancy 2) 4.41;
+// the text rows' last column load on its 11 live lanes only (14) 3.87 vs
+// 3.87; the next utterance's ids resolved before the row stores (so no
+// iteration starts by waiting for the previous row's stores) 3.87 vs 3.81.
 // Timing-only ablations of 3 (wrong rows): no text 3.14 (6), no frames 2.32
 // (7), no row stores 3.61 (8), neither text nor frames 1.41 (9).
 static int narrow_variant() {
@@ -1075,6 +1091,7 @@ static int launch_narrow(const StreamArgs& a, hipStream_t stream, int* parts) {
     case 11: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 0, 1><<<grid, 256, 0, stream>>>(a); break;
     case 12: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
     case 13: utt_narrow_kernel<2, 8, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
+    case 14: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0, 1><<<grid, 256, 0, stream>>>(a); break;
     default: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a); break;
   }
 #else
