@@ -729,10 +729,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 // order), 1 = per-lane slot partials combined slot 0 + 1 + ... at the end.
 // ORD: 0 = utterances round robin over the waves, 1 = a contiguous range per
 // wave (neighbouring x / s / aux rows written by one wave: whole lines).
-// TX = 1: the text rows' last column load (units 64..) issued on its live
-// lanes only (exec-masked; the other lanes' sums are kept out of the row max)
-template <int CT, int UNR, int GA_MAX, int GV_MAX, int OCC = 2, int ABL = 0, int FR = 0, int ORD = 0,
-          int TX = 0>
+template <int CT, int UNR, int GA_MAX, int GV_MAX, int OCC = 2, int ABL = 0, int FR = 0, int ORD = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void utt_narrow_kernel(StreamArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   // the wave index made visibly wave-uniform: utterance bases stay in SGPRs
@@ -860,10 +857,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
       const int r = __builtin_amdgcn_readlane(rid, t);
       const int so = r >= 0 ? r * D * 4 : tbytes;  // out of range: a zero row
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        if (TX && c == CT - 1 && lane + kWave * c >= UT) continue;
+      for (int c = 0; c < CT; ++c)
         v[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
-      }
     };
     // (the weight is read at accumulation: its gather is waited for there)
     auto accum = [&](int t, const float4 (&v)[CT]) {
@@ -922,8 +917,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 
     float m = fmaxf(fmaxf(amax4(sa), amax4(saa)), fmaxf(amax4(sv), amax4(svv)));
 #pragma unroll
-    for (int c = 0; c < CT; ++c)
-      if (!TX || lane + kWave * c < UT) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
+    for (int c = 0; c < CT; ++c) m = fmaxf(m, fmaxf(amax4(sx[c]), amax4(sxx[c])));
     const float rs = row_scale(wave_max(m));
     resolve(raw, rid_n, w_n);  // the next utterance's (see above)
     if ((ABL & 4) != 0 && rs != 3.f) continue;  // (never 3: a power of two)
@@ -1055,9 +1049,12 @@ constexpr int kCmaxRows = 8192;
 // occupancy 2 (4) 4.74; 5 rows forced to 4 waves per SIMD (5, spills) 5.15;
 // slot-partial frame sums (10) 3.81; contiguous utterance ranges per wave (11
 // = 3, 12 = 10 with it) no change; 8-row groups (13, occupancy 2) 4.41;
-// the text rows' last column load on its 11 live lanes only (14) 3.87 vs
-// 3.87; the next utterance's ids resolved before the row stores (so no
-// iteration starts by waiting for the previous row's stores) 3.87 vs 3.81.
+// not kept (removed after measuring): the text rows' last column load on
+// its 11 live lanes only 3.87 vs 3.87; the last 11 units of 5 text rows in
+// ONE packed instruction (16 instead of 40 text loads per utterance) 3.89 vs
+// 3.85 with 5-row groups, 4.44 with 10; the next utterance's ids resolved
+// before the row stores (kept: no iteration starts by waiting for the
+// previous row's stores) 3.87 vs 3.81.
 // Timing-only ablations of 3 (wrong rows): no text 3.14 (6), no frames 2.32
 // (7), no row stores 3.61 (8), neither text nor frames 1.41 (9).
 static int narrow_variant() {
@@ -1091,7 +1088,6 @@ static int launch_narrow(const StreamArgs& a, hipStream_t stream, int* parts) {
     case 11: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 0, 1><<<grid, 256, 0, stream>>>(a); break;
     case 12: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
     case 13: utt_narrow_kernel<2, 8, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
-    case 14: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0, 1><<<grid, 256, 0, stream>>>(a); break;
     default: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a); break;
   }
 #else
