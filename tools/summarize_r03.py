@@ -110,7 +110,8 @@ def main(src, tag):
             lines.append(f"| `{k}` | {len(fetch[k])} | {fv:.0f} | {wv:.0f} | {b:.4g} |")
         fused = [v for k, v in traffic.items() if "utt_fused_kernel" in k]
         stream = fused or [v for k, v in traffic.items()
-                           if "utt_stream_kernel" in k or "utt_wave_kernel" in k]
+                           if "utt_stream_kernel" in k or "utt_wave_kernel" in k
+                           or "utt_narrow_kernel" in k]
         cfg = wb["config"]
         alg = wb["roofline"]["algorithmic_bytes_per_utt"] * cfg["utts_rank0"]
         if stream:
