@@ -381,6 +381,20 @@ int mmb_gauss_backward(const double* const* stats, const int* fm, const int64_t*
                        int nkeys, const int* mods, const float* const* mu,
                        const float* const* sigma, const float* dlp, float* const* dmu,
                        float* const* dsigma, hipStream_t stream);
+/* The same two with row strides (elements; HOST arrays, one per key): mu_k /
+ * dmu_k rows ld_mu[k] apart, sigma_k / dsigma_k rows ld_sigma[k] apart -- the
+ * per-key column blocks of the generator's fused output [B, 2 F] (mu) and of
+ * exp() of its log-sigma half [B, F] (sigma) without copies.  ld >= F_k;
+ * null arrays mean F_k (contiguous rows), as in the unstrided entry points. */
+int mmb_gauss_loglik_strided(const double* const* stats, const int* fm, const int64_t* idx,
+                             int64_t b, int nkeys, const int* mods, const float* const* mu,
+                             const int64_t* ld_mu, const float* const* sigma,
+                             const int64_t* ld_sigma, float* lp, hipStream_t stream);
+int mmb_gauss_backward_strided(const double* const* stats, const int* fm, const int64_t* idx,
+                               int64_t b, int nkeys, const int* mods, const float* const* mu,
+                               const int64_t* ld_mu, const float* const* sigma,
+                               const int64_t* ld_sigma, const float* dlp, float* const* dmu,
+                               float* const* dsigma, hipStream_t stream);
 
 #ifdef __cplusplus
 }

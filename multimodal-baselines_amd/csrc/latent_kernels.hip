@@ -340,11 +340,13 @@ struct GaussArgs {
   int64_t B;
   int nkeys;
   int mods[kMaxKeys];      // bit 0 text, 1 audio, 2 visual (cat order text, audio, visual)
-  const float* mu[kMaxKeys];     // [B][F_k]
-  const float* sigma[kMaxKeys];  // [B][F_k]
+  const float* mu[kMaxKeys];     // [B][F_k], rows ldm[k] apart
+  const float* sigma[kMaxKeys];  // [B][F_k], rows lds[k] apart
   const float* dlp;              // [nkeys][B] (backward)
-  float* dmu[kMaxKeys];
-  float* dsigma[kMaxKeys];
+  float* dmu[kMaxKeys];          // rows ldm[k] apart
+  float* dsigma[kMaxKeys];       // rows lds[k] apart
+  int64_t ldm[kMaxKeys];
+  int64_t lds[kMaxKeys];
 };
 
 __device__ __forceinline__ int key_width(const GaussArgs& g, int k) {
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(256) void gauss_loglik_kernel(GaussArgs g, float* _
     key_feature(g, k, f, mod, ff);
     const double* st = g.stats[mod] + row * 3 * g.Fm[mod];
     const double m0 = st[ff], m1 = st[g.Fm[mod] + ff], m2 = st[2 * g.Fm[mod] + ff];
-    const double mu = g.mu[k][b * Fk + f], s = g.sigma[k][b * Fk + f];
+    const double mu = g.mu[k][b * g.ldm[k] + f], s = g.sigma[k][b * g.lds[k] + f];
     const double q = m2 - 2.0 * mu * m1 + mu * mu * m0;
     acc += m0 * (-log(s) - hl2pi) - q / (2.0 * s * s);
   }
@@ -404,10 +406,10 @@ __global__ __launch_bounds__(256) void gauss_backward_kernel(GaussArgs g) {
     key_feature(g, k, f, mod, ff);
     const double* st = g.stats[mod] + row * 3 * g.Fm[mod];
     const double m0 = st[ff], m1 = st[g.Fm[mod] + ff], m2 = st[2 * g.Fm[mod] + ff];
-    const double mu = g.mu[k][b * Fk + f], s = g.sigma[k][b * Fk + f];
+    const double mu = g.mu[k][b * g.ldm[k] + f], s = g.sigma[k][b * g.lds[k] + f];
     const double q = m2 - 2.0 * mu * m1 + mu * mu * m0;
-    if (g.dmu[k]) g.dmu[k][b * Fk + f] = static_cast<float>(d * (m1 - mu * m0) / (s * s));
-    if (g.dsigma[k]) g.dsigma[k][b * Fk + f] = static_cast<float>(d * (-m0 / s + q / (s * s * s)));
+    if (g.dmu[k]) g.dmu[k][b * g.ldm[k] + f] = static_cast<float>(d * (m1 - mu * m0) / (s * s));
+    if (g.dsigma[k]) g.dsigma[k][b * g.lds[k] + f] = static_cast<float>(d * (-m0 / s + q / (s * s * s)));
   }
 }
 
@@ -515,12 +517,28 @@ static int gauss_args(GaussArgs& g, const double* const* stats, const int* fm, c
   return MMB_OK;
 }
 
-extern "C" int mmb_gauss_loglik(const double* const* stats, const int* fm, const int64_t* idx,
-                                int64_t b, int nkeys, const int* mods, const float* const* mu,
-                                const float* const* sigma, float* lp, hipStream_t stream) {
+// row strides per key: given (the strided entry points), or the key widths
+static int gauss_strides(GaussArgs& g, const int64_t* ld_mu, const int64_t* ld_sigma) {
+  for (int k = 0; k < g.nkeys; ++k) {
+    int w = 0;
+    for (int m = 0; m < 3; ++m)
+      if (g.mods[k] >> m & 1) w += g.Fm[m];
+    g.ldm[k] = ld_mu ? ld_mu[k] : w;
+    g.lds[k] = ld_sigma ? ld_sigma[k] : w;
+    MMB_REQUIRE(g.ldm[k] >= w && g.lds[k] >= w);
+  }
+  return MMB_OK;
+}
+
+extern "C" int mmb_gauss_loglik_strided(const double* const* stats, const int* fm,
+                                        const int64_t* idx, int64_t b, int nkeys, const int* mods,
+                                        const float* const* mu, const int64_t* ld_mu,
+                                        const float* const* sigma, const int64_t* ld_sigma,
+                                        float* lp, hipStream_t stream) {
   GaussArgs g{};
-  const int rc = gauss_args(g, stats, fm, idx, b, nkeys, mods);
+  int rc = gauss_args(g, stats, fm, idx, b, nkeys, mods);
   if (rc != MMB_OK) return rc;
+  if ((rc = gauss_strides(g, ld_mu, ld_sigma)) != MMB_OK) return rc;
   MMB_REQUIRE(mu && sigma && lp);
   for (int k = 0; k < nkeys; ++k) {
     MMB_REQUIRE(mu[k] && sigma[k]);
@@ -533,13 +551,24 @@ extern "C" int mmb_gauss_loglik(const double* const* stats, const int* fm, const
   return MMB_OK;
 }
 
-extern "C" int mmb_gauss_backward(const double* const* stats, const int* fm, const int64_t* idx,
-                                  int64_t b, int nkeys, const int* mods, const float* const* mu,
-                                  const float* const* sigma, const float* dlp, float* const* dmu,
-                                  float* const* dsigma, hipStream_t stream) {
+extern "C" int mmb_gauss_loglik(const double* const* stats, const int* fm, const int64_t* idx,
+                                int64_t b, int nkeys, const int* mods, const float* const* mu,
+                                const float* const* sigma, float* lp, hipStream_t stream) {
+  return mmb_gauss_loglik_strided(stats, fm, idx, b, nkeys, mods, mu, nullptr, sigma, nullptr, lp,
+                                  stream);
+}
+
+extern "C" int mmb_gauss_backward_strided(const double* const* stats, const int* fm,
+                                          const int64_t* idx, int64_t b, int nkeys,
+                                          const int* mods, const float* const* mu,
+                                          const int64_t* ld_mu, const float* const* sigma,
+                                          const int64_t* ld_sigma, const float* dlp,
+                                          float* const* dmu, float* const* dsigma,
+                                          hipStream_t stream) {
   GaussArgs g{};
-  const int rc = gauss_args(g, stats, fm, idx, b, nkeys, mods);
+  int rc = gauss_args(g, stats, fm, idx, b, nkeys, mods);
   if (rc != MMB_OK) return rc;
+  if ((rc = gauss_strides(g, ld_mu, ld_sigma)) != MMB_OK) return rc;
   MMB_REQUIRE(mu && sigma && dlp && dmu && dsigma);
   for (int k = 0; k < nkeys; ++k) {
     MMB_REQUIRE(mu[k] && sigma[k]);
@@ -553,4 +582,12 @@ extern "C" int mmb_gauss_backward(const double* const* stats, const int* fm, con
   gauss_backward_kernel<<<dim3(static_cast<unsigned>(b), nkeys), 256, 0, stream>>>(g);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
+}
+
+extern "C" int mmb_gauss_backward(const double* const* stats, const int* fm, const int64_t* idx,
+                                  int64_t b, int nkeys, const int* mods, const float* const* mu,
+                                  const float* const* sigma, const float* dlp, float* const* dmu,
+                                  float* const* dsigma, hipStream_t stream) {
+  return mmb_gauss_backward_strided(stats, fm, idx, b, nkeys, mods, mu, nullptr, sigma, nullptr,
+                                    dlp, dmu, dsigma, stream);
 }

@@ -354,12 +354,14 @@ __global__ __launch_bounds__(256) void mlp_eval_kernel(const float* __restrict__
     __syncthreads();
     for (int h = tid; h < H; h += 256) {
       float p = b1[h];
+#pragma unroll 10
       for (int d = 0; d < D; ++d) p = fmaf(w1[static_cast<int64_t>(h) * D + d], sx[d], p);
       shid[h] = p > 0.f ? p : 0.f;
     }
     __syncthreads();
     for (int o = tid; o < O; o += 256) {
       float out = b2[o];
+#pragma unroll 20
       for (int h = 0; h < H; ++h) out = fmaf(w2[o * H + h], shid[h], out);
       if (pred) pred[(b0 + bb) * O + o] = out;
       if (lab) lsum += fabsf(out - lab[row * O + o]);
@@ -384,6 +386,22 @@ constexpr int kMlpRows = 8;  // rows per block of the row kernels
 // Block = kMlpRows rows staged in LDS; thread = hidden unit h, walking its own
 // w1 row (each 64-byte line reused over 16 k-steps from L1) with the block's
 // rows' x broadcast from LDS: one w1 load serves kMlpRows FMAs.
+// V4 (D % 4 == 0, 16-byte aligned w1): the block first copies W1 into LDS
+// (rows kMlpWPad floats apart) with all of its 16-byte loads in flight at
+// once, then every thread walks its own row from LDS as float4.  Reading the
+// thread-private rows from L2 instead (one cache line per lane per load, ~75
+// dependent round trips per thread) took 38 us for a 64-row batch.  Same FMAs
+// in the same order either way.
+// LDS row stride of the staged W1 (floats): >= D, a multiple of 4 (16-byte
+// rows) and 20 mod 32, so the float4 reads of consecutive threads' rows start
+// in 8 different 4-bank groups (D + 4 = 304 = 16 mod 32 put every other
+// thread in the same banks)
+__host__ __device__ constexpr int mlp_wld(int d) {
+  const int r = (d + 3) / 4 * 4;
+  return r + ((20 - r % 32) % 32 + 32) % 32;
+}
+
+template <bool V4>
 __global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restrict__ x, int64_t B,
                                                            int D, int H, int O,
                                                            const float* __restrict__ w1,
@@ -395,23 +413,68 @@ __global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restri
   extern __shared__ float sm[];
   float* sx = sm;                      // [kMlpRows][D]
   float* sh = sx + kMlpRows * D;       // [kMlpRows][H]
+  float* sw = sh + kMlpRows * H;       // V4: [H][wld]
+  const int wld = mlp_wld(D);
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kMlpRows;
   const int nr = static_cast<int>(min<int64_t>(kMlpRows, B - r0));
-  for (int e = threadIdx.x; e < kMlpRows * D; e += blockDim.x) {
-    const int r = e / D;
-    sx[e] = r < nr ? x[(r0 + r) * D + e % D] : 0.f;
+  {  // the block's x rows: every thread's loads issued before its LDS stores
+    constexpr int kBatch = 12;
+    for (int e0 = threadIdx.x; e0 < kMlpRows * D; e0 += kBatch * blockDim.x) {
+      float v[kBatch];
+#pragma unroll
+      for (int q = 0; q < kBatch; ++q) {
+        const int e = e0 + q * static_cast<int>(blockDim.x);
+        const int r = e / D;
+        v[q] = (e < kMlpRows * D && r < nr) ? x[(r0 + r) * D + e % D] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < kBatch; ++q) {
+        const int e = e0 + q * static_cast<int>(blockDim.x);
+        if (e < kMlpRows * D) sx[e] = v[q];
+      }
+    }
+  }
+  if constexpr (V4) {
+    const int U = D / 4, n4 = H * U;
+    constexpr int kBatch = 16;  // 16-byte loads per thread in flight
+    for (int e0 = threadIdx.x; e0 < n4; e0 += kBatch * blockDim.x) {
+      float4 v[kBatch];
+#pragma unroll
+      for (int q = 0; q < kBatch; ++q) {
+        const int e = min(e0 + q * static_cast<int>(blockDim.x), n4 - 1);
+        v[q] = reinterpret_cast<const float4*>(w1)[e];
+      }
+#pragma unroll
+      for (int q = 0; q < kBatch; ++q) {
+        const int e = e0 + q * static_cast<int>(blockDim.x);
+        if (e < n4)
+          *reinterpret_cast<float4*>(sw + (e / U) * wld + 4 * (e % U)) = v[q];
+      }
+    }
   }
   __syncthreads();
   for (int h = threadIdx.x; h < H; h += blockDim.x) {
-    const float* wr = w1 + static_cast<int64_t>(h) * D;
+    const float* wr = V4 ? sw + h * wld : w1 + static_cast<int64_t>(h) * D;
     float p[kMlpRows];
 #pragma unroll
     for (int r = 0; r < kMlpRows; ++r) p[r] = b1[h];
-#pragma unroll 4
-    for (int d = 0; d < D; ++d) {
-      const float w = wr[d];
+    if constexpr (V4) {
+#pragma unroll 5
+      for (int d = 0; d < D; d += 4) {
+        const float4 w4 = *reinterpret_cast<const float4*>(wr + d);
+        const float w[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-      for (int r = 0; r < kMlpRows; ++r) p[r] = fmaf(w, sx[r * D + d], p[r]);
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int r = 0; r < kMlpRows; ++r) p[r] = fmaf(w[k], sx[r * D + d + k], p[r]);
+      }
+    } else {
+#pragma unroll 4
+      for (int d = 0; d < D; ++d) {
+        const float w = wr[d];
+#pragma unroll
+        for (int r = 0; r < kMlpRows; ++r) p[r] = fmaf(w, sx[r * D + d], p[r]);
+      }
     }
 #pragma unroll
     for (int r = 0; r < kMlpRows; ++r) {
@@ -424,6 +487,9 @@ __global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restri
   for (int e = threadIdx.x; e < nr * O; e += blockDim.x) {
     const int o = e % O, r = e / O;
     float out = b2[o];
+    // (unrolled: the w2 loads are issued ahead of the in-order FMA chain -- one
+    // dependent L2 round trip per h was most of this kernel's 38 us)
+#pragma unroll 20
     for (int h = 0; h < H; ++h) out = fmaf(w2[o * H + h], sh[r * H + h], out);
     y[(r0 + r) * O + o] = out;
   }
@@ -431,6 +497,9 @@ __global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restri
 
 // dh[b][h] = [hid > 0] * sum_o dy[b][o] w2[o][h];  dx[b][d] = sum_h dh[b][h] w1[h][d]
 // (thread = column d: w1[h][d] coalesced over the block, dh broadcast from LDS)
+// R rows per block (2: 32 blocks for a 64-row batch instead of 8 -- the d
+// loop's w1 loads are latency-bound; more blocks keep more of them in flight)
+template <int R>
 __global__ __launch_bounds__(256) void mlp_bwd_rows_kernel(const float* __restrict__ hid, int64_t B,
                                                            int D, int H, int O,
                                                            const float* __restrict__ w1,
@@ -439,10 +508,10 @@ __global__ __launch_bounds__(256) void mlp_bwd_rows_kernel(const float* __restri
                                                            float* __restrict__ dh,
                                                            float* __restrict__ dx) {
   extern __shared__ float sm[];
-  float* sdh = sm;  // [kMlpRows][H]
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kMlpRows;
-  const int nr = static_cast<int>(min<int64_t>(kMlpRows, B - r0));
-  for (int e = threadIdx.x; e < kMlpRows * H; e += blockDim.x) {
+  float* sdh = sm;  // [R][H]
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int nr = static_cast<int>(min<int64_t>(R, B - r0));
+  for (int e = threadIdx.x; e < R * H; e += blockDim.x) {
     const int h = e % H, r = e / H;
     float g = 0.f;
     if (r < nr && hid[(r0 + r) * H + h] > 0.f)
@@ -453,17 +522,17 @@ __global__ __launch_bounds__(256) void mlp_bwd_rows_kernel(const float* __restri
   __syncthreads();
   if (dx == nullptr) return;
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float g[kMlpRows];
+    float g[R];
 #pragma unroll
-    for (int r = 0; r < kMlpRows; ++r) g[r] = 0.f;
-#pragma unroll 4
+    for (int r = 0; r < R; ++r) g[r] = 0.f;
+#pragma unroll 10
     for (int h = 0; h < H; ++h) {
       const float w = w1[static_cast<int64_t>(h) * D + d];
 #pragma unroll
-      for (int r = 0; r < kMlpRows; ++r) g[r] = fmaf(sdh[r * H + h], w, g[r]);
+      for (int r = 0; r < R; ++r) g[r] = fmaf(sdh[r * H + h], w, g[r]);
     }
 #pragma unroll
-    for (int r = 0; r < kMlpRows; ++r)
+    for (int r = 0; r < R; ++r)
       if (r < nr) dx[(r0 + r) * D + d] = g[r];
   }
 }
@@ -483,6 +552,7 @@ __global__ __launch_bounds__(256) void mlp_bwd_params_kernel(const float* __rest
   if (h == H) {
     for (int o = threadIdx.x; o < O; o += blockDim.x) {
       float g = 0.f;
+#pragma unroll 16
       for (int64_t b = 0; b < B; ++b) g += dy[b * O + o];
       if (db2) db2[o] = g;
     }
@@ -490,16 +560,19 @@ __global__ __launch_bounds__(256) void mlp_bwd_params_kernel(const float* __rest
   }
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float g = 0.f;
+#pragma unroll 16
     for (int64_t b = 0; b < B; ++b) g = fmaf(dh[b * H + h], x[b * D + d], g);
     if (dw1) dw1[static_cast<int64_t>(h) * D + d] = g;
   }
   if (threadIdx.x == 0 && db1) {
     float g = 0.f;
+#pragma unroll 16
     for (int64_t b = 0; b < B; ++b) g += dh[b * H + h];
     db1[h] = g;
   }
   for (int o = threadIdx.x; o < O; o += blockDim.x) {
     float g = 0.f;
+#pragma unroll 16
     for (int64_t b = 0; b < B; ++b) g = fmaf(dy[b * O + o], hid[b * H + h], g);
     if (dw2) dw2[o * H + h] = g;
   }
@@ -605,8 +678,21 @@ extern "C" int mmb_mlp_forward_train(const float* x, int64_t b, int d, int h, in
   if (b == 0) return MMB_OK;
   const size_t lds = sizeof(float) * kMlpRows * (d + h);
   MMB_REQUIRE(lds <= 64 * 1024);
-  mlp_fwd_rows_kernel<<<static_cast<int>(ceil_div(b, kMlpRows)), 256, lds, stream>>>(
-      x, b, d, h, o, w1, b1, w2, b2, y_out, hid_out);
+  const int grid = static_cast<int>(ceil_div(b, kMlpRows));
+  const size_t lds_w = lds + sizeof(float) * static_cast<size_t>(h) * mlp_wld(d);
+  if (d % 4 == 0 && (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && lds_w <= 160 * 1024) {
+    static bool attr_set = false;  // > 64 KB of dynamic LDS (the regressor: 134 KB)
+    if (!attr_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_fwd_rows_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_set = true;
+    }
+    mlp_fwd_rows_kernel<true><<<grid, 256, lds_w, stream>>>(x, b, d, h, o, w1, b1, w2, b2, y_out,
+                                                           hid_out);
+  } else {
+    mlp_fwd_rows_kernel<false><<<grid, 256, lds, stream>>>(x, b, d, h, o, w1, b1, w2, b2, y_out,
+                                                          hid_out);
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -627,9 +713,10 @@ extern "C" int mmb_mlp_backward(const float* x, const float* hid, int64_t b, int
     }
     return MMB_OK;
   }
-  const size_t lds = sizeof(float) * kMlpRows * h;
+  constexpr int kBwdRows = 2;
+  const size_t lds = sizeof(float) * kBwdRows * h;
   MMB_REQUIRE(lds <= 64 * 1024);
-  mlp_bwd_rows_kernel<<<static_cast<int>(ceil_div(b, kMlpRows)), 256, lds, stream>>>(
+  mlp_bwd_rows_kernel<kBwdRows><<<static_cast<int>(ceil_div(b, kBwdRows)), 256, lds, stream>>>(
       hid, b, d, h, o, w1, w2, dy, dh_ws, dx);
   MMB_LAUNCH_CHECK();
   if (dw1 || db1 || dw2 || db2) {

@@ -150,20 +150,31 @@ class GaussStats:
         self.fm = [0 if s is None else s.shape[2] for s in self.stats]
 
 
+def _rows(t: torch.Tensor):
+    """(tensor, row stride) for the strided Gaussian entry points: a [B, F]
+    view with unit column stride passes as is (e.g. a key's column block of
+    the generator's fused output), anything else as a contiguous copy."""
+    t = t.detach()
+    if t.dtype != torch.float32 or t.dim() != 2 or t.stride(1) != 1:
+        t = t.float().contiguous()
+    return t, t.stride(0)
+
+
 class _GaussLogProb(torch.autograd.Function):
     @staticmethod
     def forward(ctx, gs: GaussStats, idx, mods, *musig):
         K = len(mods)
-        mus = [m.detach().float().contiguous() for m in musig[:K]]
-        sigs = [s.detach().float().contiguous() for s in musig[K:]]
+        mus, ldm = zip(*[_rows(m) for m in musig[:K]])
+        sigs, lds = zip(*[_rows(s) for s in musig[K:]])
         B = mus[0].shape[0]
         lp = torch.empty((K, B), dtype=torch.float32, device=mus[0].device)
         st = _ptr_array(gs.stats)
         fm = (ctypes.c_int * 3)(*gs.fm)
         md = (ctypes.c_int * K)(*mods)
-        L.call("mmb_gauss_loglik", st, fm, L.ptr(idx), B, K, md, _ptr_array(mus), _ptr_array(sigs),
-               L.ptr(lp), L.stream_ptr())
-        ctx.gs, ctx.mods = gs, mods
+        L.call("mmb_gauss_loglik_strided", st, fm, L.ptr(idx), B, K, md, _ptr_array(mus),
+               (ctypes.c_int64 * K)(*ldm), _ptr_array(sigs), (ctypes.c_int64 * K)(*lds), L.ptr(lp),
+               L.stream_ptr())
+        ctx.gs, ctx.mods, ctx.ldm, ctx.lds = gs, mods, ldm, lds
         ctx.save_for_backward(idx, *mus, *sigs)
         return lp
 
@@ -176,11 +187,35 @@ class _GaussLogProb(torch.autograd.Function):
         B = mus[0].shape[0]
         need_mu = ctx.needs_input_grad[3:3 + K]
         need_s = ctx.needs_input_grad[3 + K:]
-        dmu = [torch.empty_like(m) if n else None for m, n in zip(mus, need_mu)]
-        dsg = [torch.empty_like(s) if n else None for s, n in zip(sigs, need_s)]
+
+        def grads(ts, lds, need):
+            # one buffer for all keys, each key's block at its input's offset
+            # and row stride (the layout of the generator's fused output), so
+            # the gradients reach the split / linear backward without copies
+            if not any(need):
+                return [None] * K
+            base = ts[0]
+            same = all(t.stride(0) == lds[0] and t.untyped_storage().data_ptr() ==
+                       base.untyped_storage().data_ptr() for t in ts)
+            if not same:
+                return [torch.empty_like(t) if n else None for t, n in zip(ts, need)]
+            lo = min(t.storage_offset() for t in ts)
+            width = max(t.storage_offset() - lo + t.shape[1] for t in ts)
+            buf = torch.empty((B, lds[0]), dtype=torch.float32, device=base.device)
+            return [buf[:, t.storage_offset() - lo:t.storage_offset() - lo + t.shape[1]] if n
+                    else None for t, n in zip(ts, need)] if width <= lds[0] else \
+                [torch.empty_like(t) if n else None for t, n in zip(ts, need)]
+
+        dmu = grads(mus, ctx.ldm, need_mu)
+        dsg = grads(sigs, ctx.lds, need_s)
+        ldm = [d.stride(0) if d is not None else l for d, l in zip(dmu, ctx.ldm)]
+        lds = [d.stride(0) if d is not None else l for d, l in zip(dsg, ctx.lds)]
+        # (a key's gradient must share its input's row stride: the kernel walks both with one)
+        assert all(a == b for a, b in zip(ldm, ctx.ldm)) and all(a == b for a, b in zip(lds, ctx.lds))
         gs = ctx.gs
-        L.call("mmb_gauss_backward", _ptr_array(gs.stats), (ctypes.c_int * 3)(*gs.fm), L.ptr(idx),
-               B, K, (ctypes.c_int * K)(*ctx.mods), _ptr_array(mus), _ptr_array(sigs),
+        L.call("mmb_gauss_backward_strided", _ptr_array(gs.stats), (ctypes.c_int * 3)(*gs.fm),
+               L.ptr(idx), B, K, (ctypes.c_int * K)(*ctx.mods), _ptr_array(mus),
+               (ctypes.c_int64 * K)(*ctx.ldm), _ptr_array(sigs), (ctypes.c_int64 * K)(*ctx.lds),
                L.ptr(dlp.float().contiguous()), _ptr_array(dmu), _ptr_array(dsg), L.stream_ptr())
         return (None, None, None, *dmu, *dsg)
 

@@ -86,6 +86,8 @@ SIGNATURES = {
     "mmb_gauss_stats": (_I, [_P, _P, _L, _I, _I, _P, _P]),
     "mmb_gauss_loglik": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P]),
     "mmb_gauss_backward": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_gauss_loglik_strided": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_gauss_backward_strided": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None

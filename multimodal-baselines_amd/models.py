@@ -7,14 +7,20 @@ closed-form estimate (`sif2.py:164-208`) reads only ``.weight [F_k, D]`` and
 ``.bias [F_k]`` of those layers.  Construction order matches the reference so
 ``torch.manual_seed(s)`` reproduces the reference's initial weights bit for bit.
 
-The generator *forward* (latent-optimisation objective) is a next row
-(SURVEY.md §8f row 1); it is provided here only as plain torch for the CLI's
-bookkeeping and is not on the accelerated path.
+The generator *forward* (latent-optimisation objective)
+runs all twelve linears as ONE GEMM over their concatenated weights (the
+reference's per-key `nn.Linear` calls, `/root/reference/models.py:187-202`,
+are the same dot products; only the GEMM grouping differs): one forward GEMM
+and two backward GEMMs instead of 36 small ones, one `exp` for all the
+sigmas, and the per-key mu / sigma outputs are column views of the result
+(the Gaussian kernels take row strides, `mmb_gauss_loglik_strided`).  The
+parameters, their layout and their initialisation stay per key.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 # fixed key order of sif2.py:167-174 (also the ModuleDict order, models.py:134-159)
 MMB2_KEYS = ("audio", "visual", "audiovisual", "textaudio", "textvisual", "textaudiovisual")
@@ -74,9 +80,19 @@ class AudioVisualGeneratorMultimodal(nn.Module):
         self.embedding_dim = self.embedding.size()[-1]
 
     def forward(self, embeddings):
+        """{key: {'mu': x W_mu^T + b_mu, 'sigma': exp(x W_ls^T + b_ls)}} with x
+        the (normalised) embeddings (models.py:187-202): y = x [W_mu; W_ls]^T
+        + [b_mu; b_ls] in one GEMM, every key's block a column view of y."""
         x = self.norm(embeddings) if self.norm is not None else embeddings
-        return {k: {"mu": m["mu"](x), "sigma": m["log_sigma"](x).exp()}
-                for k, m in self.embed2out.items()}
+        mods = list(self.embed2out.values())
+        w = torch.cat([m["mu"].weight for m in mods] + [m["log_sigma"].weight for m in mods])
+        b = torch.cat([m["mu"].bias for m in mods] + [m["log_sigma"].bias for m in mods])
+        widths = [m["mu"].out_features for m in mods]
+        f = sum(widths)
+        mu, ls = F.linear(x, w, b).split([f, f], dim=-1)
+        mus = mu.split(widths, dim=-1)
+        sigmas = ls.exp().split(widths, dim=-1)
+        return {k: {"mu": mus[i], "sigma": sigmas[i]} for i, k in enumerate(self.embed2out)}
 
     def networks(self):
         """``{key: (mu_linear, log_sigma_linear)}`` as built at simplesif.py:853-856."""

@@ -210,7 +210,17 @@ class StepGraphs:
     parameters' .grad are pointed at that graph's buffers.  Capture needs
     warm-up passes; module buffers (BatchNorm running statistics) are
     restored after them, so the first real step sees the same state as the
-    reference's."""
+    reference's.
+
+    Host / device overlap (r03): the batch's indices go up from a pinned
+    buffer without blocking, and the checked values come back into a pinned
+    buffer behind an event, so a caller can launch the optimiser step BEFORE
+    it waits for them (`step()`): the optimiser's kernels run while the host
+    reads the values and runs the checks.  Only the order of the host-side
+    effects moves -- a check that exits does so with the step's optimiser
+    update already applied to parameters the process then discards; the
+    printed `out` tensors are the step's own (the next replay has not been
+    launched)."""
 
     def __init__(self, body, modules, params, device):
         self.body, self.modules, self.params, self.dev = body, modules, list(params), device
@@ -237,18 +247,43 @@ class StepGraphs:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             outs = self.body(j)
-        self.graphs[b] = (g, j, outs, [p.grad for p in self.params])
+        j_pin = torch.empty(b, dtype=torch.int64).pin_memory()
+        vals_pin = torch.empty(outs[1].shape, dtype=outs[1].dtype).pin_memory()
+        self.graphs[b] = (g, j, outs, [p.grad for p in self.params], j_pin, vals_pin,
+                          torch.cuda.Event())
 
-    def __call__(self, j_host):
+    def launch(self, j_host):
+        """Replay the step for index batch `j_host`; returns (out, vals) with
+        vals a pinned host tensor that is valid after `wait()`."""
         b = len(j_host)
         if b not in self.graphs:
             self._capture(b)
-        g, j, outs, grads = self.graphs[b]
-        j.copy_(j_host)
+        g, j, outs, grads, j_pin, vals_pin, ev = self.graphs[b]
+        j_pin.copy_(j_host)  # (the previous step's wait() has retired its upload)
+        j.copy_(j_pin, non_blocking=True)
         g.replay()
+        vals_pin.copy_(outs[1], non_blocking=True)
+        ev.record()
         for p, gr in zip(self.params, grads):
             p.grad = gr
-        return outs
+        self._ev = ev
+        return outs[0], vals_pin
+
+    def wait(self):
+        self._ev.synchronize()
+
+    def step(self, j_host, optimizer):
+        """launch + optimizer.step() + wait: the optimiser's kernels are queued
+        before the host blocks on the values."""
+        out, vals = self.launch(j_host)
+        optimizer.step()
+        self.wait()
+        return out, vals
+
+    def __call__(self, j_host):
+        out, vals = self.launch(j_host)
+        self.wait()
+        return out, vals
 
 
 def _sigma_check(out):
@@ -292,9 +327,8 @@ def optimize_latents(args, train: bool, gen_model, embed_arr, dataloader, n_epoc
         for j in _index_batches(dataloader):
             iters += 1
             if graphs is not None:
-                out, vals = graphs(j)
+                out, vals = graphs.step(j, optimizer)
                 epoch_loss += check_step(out, vals, embeddings[:len(j)].size())
-                optimizer.step()
                 continue
             optimizer.zero_grad()
             out = gen_model(embeddings[j])
@@ -543,9 +577,8 @@ def main(argv=None):
             for j in _index_batches(dataloader):
                 if graphs is not None:
                     iters += 1
-                    out, vals = graphs(j)
+                    out, vals = graphs.step(j, optimizer)
                     epoch_loss += check_step(out, vals, train_embed[:len(j)].size())
-                    optimizer.step()
                     continue
                 _, s_data = senti_train_data[j]
                 iters += 1

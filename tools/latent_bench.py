@@ -125,10 +125,8 @@ def run(cfg, objective, gen, senti, lat0, label, dev, steps, batch, warm=2, grap
 
         def gstep():
             j = torch.randperm(n, generator=g)[:batch]
-            out, vals = graphs(j)
-            loss = simplesif.check_step(out, vals, lat[:batch].size())
-            opt.step()
-            return loss
+            out, vals = graphs.step(j, opt)
+            return simplesif.check_step(out, vals, lat[:batch].size())
 
         for _ in range(warm):
             gstep()
@@ -185,10 +183,18 @@ def main():
     ap.add_argument("--a", type=int, default=75)
     ap.add_argument("--vd", type=int, default=46)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--only-graph", action="store_true",
+                    help="time the graph step alone (for a kernel trace of just that path)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg, obj, gen, senti, lat0, label, data = build(args, dev)
     import copy
+
+    if args.only_graph:
+        ms_graph = run(cfg, None, copy.deepcopy(gen), copy.deepcopy(senti), lat0, label, dev,
+                       args.steps, args.batch, graph_obj=obj)
+        print(json.dumps({"ms_per_step": {"libmmb_graph": round(ms_graph, 4)}, "steps": args.steps}))
+        return
 
     ms_hip = run(cfg, obj.log_prob, copy.deepcopy(gen), copy.deepcopy(senti), lat0, label, dev,
                  args.steps, args.batch)
