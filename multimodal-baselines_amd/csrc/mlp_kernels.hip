@@ -420,17 +420,19 @@ __global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restri
   {  // the block's x rows: every thread's loads issued before its LDS stores
     constexpr int kBatch = 12;
     for (int e0 = threadIdx.x; e0 < kMlpRows * D; e0 += kBatch * blockDim.x) {
+      // (unconditional loads of clamped addresses: a load under a per-lane
+      // condition was waited for inside its branch, one round trip each)
       float v[kBatch];
 #pragma unroll
       for (int q = 0; q < kBatch; ++q) {
-        const int e = e0 + q * static_cast<int>(blockDim.x);
-        const int r = e / D;
-        v[q] = (e < kMlpRows * D && r < nr) ? x[(r0 + r) * D + e % D] : 0.f;
+        const int e = min(e0 + q * static_cast<int>(blockDim.x), kMlpRows * D - 1);
+        const int r = min(e / D, nr - 1);
+        v[q] = x[(r0 + r) * D + e % D];
       }
 #pragma unroll
       for (int q = 0; q < kBatch; ++q) {
         const int e = e0 + q * static_cast<int>(blockDim.x);
-        if (e < kMlpRows * D) sx[e] = v[q];
+        if (e < kMlpRows * D) sx[e] = e / D < nr ? v[q] : 0.f;
       }
     }
   }
@@ -453,42 +455,65 @@ __global__ __launch_bounds__(256) void mlp_fwd_rows_kernel(const float* __restri
     }
   }
   __syncthreads();
-  for (int h = threadIdx.x; h < H; h += blockDim.x) {
-    const float* wr = V4 ? sw + h * wld : w1 + static_cast<int64_t>(h) * D;
-    float p[kMlpRows];
+  if constexpr (V4) {
+    // two thread groups of 128, each a half of the block's rows (4 each):
+    // half the FMA chain per thread of one group per row block
+    constexpr int RH = kMlpRows / 2;
+    const int half = threadIdx.x >> 7;
+    for (int h = threadIdx.x & 127; h < H; h += 128) {
+      const float* wr = sw + h * wld;
+      const float* xs = sx + half * RH * D;
+      float p[RH];
 #pragma unroll
-    for (int r = 0; r < kMlpRows; ++r) p[r] = b1[h];
-    if constexpr (V4) {
+      for (int r = 0; r < RH; ++r) p[r] = b1[h];
 #pragma unroll 5
       for (int d = 0; d < D; d += 4) {
         const float4 w4 = *reinterpret_cast<const float4*>(wr + d);
-        const float w[4] = {w4.x, w4.y, w4.z, w4.w};
+        float4 x4[RH];  // the rows' 4 values as one broadcast 16-byte read each
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int r = 0; r < RH; ++r) x4[r] = *reinterpret_cast<const float4*>(xs + r * D + d);
 #pragma unroll
-          for (int r = 0; r < kMlpRows; ++r) p[r] = fmaf(w[k], sx[r * D + d + k], p[r]);
+        for (int r = 0; r < RH; ++r) p[r] = fmaf(w4.x, x4[r].x, p[r]);
+#pragma unroll
+        for (int r = 0; r < RH; ++r) p[r] = fmaf(w4.y, x4[r].y, p[r]);
+#pragma unroll
+        for (int r = 0; r < RH; ++r) p[r] = fmaf(w4.z, x4[r].z, p[r]);
+#pragma unroll
+        for (int r = 0; r < RH; ++r) p[r] = fmaf(w4.w, x4[r].w, p[r]);
       }
-    } else {
+#pragma unroll
+      for (int r = 0; r < RH; ++r) {
+        const int row = half * RH + r;
+        const float v = p[r] > 0.f ? p[r] : 0.f;
+        sh[row * H + h] = v;
+        if (row < nr) hid[(r0 + row) * H + h] = v;
+      }
+    }
+  } else {
+    for (int h = threadIdx.x; h < H; h += blockDim.x) {
+      const float* wr = w1 + static_cast<int64_t>(h) * D;
+      float p[kMlpRows];
+#pragma unroll
+      for (int r = 0; r < kMlpRows; ++r) p[r] = b1[h];
 #pragma unroll 4
       for (int d = 0; d < D; ++d) {
         const float w = wr[d];
 #pragma unroll
         for (int r = 0; r < kMlpRows; ++r) p[r] = fmaf(w, sx[r * D + d], p[r]);
       }
-    }
 #pragma unroll
-    for (int r = 0; r < kMlpRows; ++r) {
-      const float v = p[r] > 0.f ? p[r] : 0.f;
-      sh[r * H + h] = v;
-      if (r < nr) hid[(r0 + r) * H + h] = v;
+      for (int r = 0; r < kMlpRows; ++r) {
+        const float v = p[r] > 0.f ? p[r] : 0.f;
+        sh[r * H + h] = v;
+        if (r < nr) hid[(r0 + r) * H + h] = v;
+      }
     }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < nr * O; e += blockDim.x) {
     const int o = e % O, r = e / O;
     float out = b2[o];
-    // (unrolled: the w2 loads are issued ahead of the in-order FMA chain -- one
-    // dependent L2 round trip per h was most of this kernel's 38 us)
+    // (unrolled: the w2 loads are issued ahead of the in-order FMA chain)
 #pragma unroll 20
     for (int h = 0; h < H; ++h) out = fmaf(w2[o * H + h], sh[r * H + h], out);
     y[(r0 + r) * O + o] = out;
