@@ -263,3 +263,56 @@ def test_cli_time_test(gpu, tmp_path, monkeypatch, capsys):
         simplesif.main(["configs/t/config_0.json", "mosi", "--time_test"])
     assert "time taken:" in capsys.readouterr().out
     assert os.path.exists("model_saves/t/config_0_run_0/pre/embed.bin")
+
+
+def test_fused_generator_and_strided_gaussians(gpu):
+    """The generator's twelve linears as one GEMM (per-key mu / sigma column
+    views) against the per-key nn.Linear calls of the reference's layout, and
+    the strided Gaussian kernels (views passed with their row strides, the
+    gradients written into one buffer in the forward's layout) against the
+    same kernels on contiguous copies: lp and every gradient equal."""
+    import latent as LT
+    import models
+
+    torch.manual_seed(5)
+    B, A, Vd, T, N = 48, 77, 48, 20, 200
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm="layer_norm",
+                                                frozen_weights=False).to(gpu)
+    lat = torch.randn(B, 300, device=gpu)
+    out = gen(lat)
+    x = gen.norm(lat)
+    for k, m in gen.embed2out.items():
+        close(out[k]["mu"].detach().cpu().numpy(), m["mu"](x).detach().cpu().numpy(), 1e-5, 1e-5)
+        close(out[k]["sigma"].detach().cpu().numpy(), m["log_sigma"](x).exp().detach().cpu().numpy(),
+              1e-5, 1e-5)
+        assert out[k]["mu"].stride(1) == 1 and not out[k]["mu"].is_contiguous()
+    g = torch.Generator().manual_seed(3)
+    stats = LT.GaussStats(
+        text=LT.gauss_stats(torch.randn(N, T, 300, generator=g).to(gpu)),
+        audio=LT.gauss_stats(torch.randn(N, T, A, generator=g).to(gpu)),
+        visual=LT.gauss_stats(torch.randn(N, T, Vd, generator=g).to(gpu)))
+    keys = list(out)
+    idx = torch.randint(0, N, (B,), generator=g).to(gpu)
+    up = torch.randn(len(keys), B, device=gpu)
+
+    # contiguous copies (the unstrided layout)
+    mus_c = [out[k]["mu"].detach().clone().requires_grad_(True) for k in keys]
+    sgs_c = [out[k]["sigma"].detach().clone().requires_grad_(True) for k in keys]
+    lp_c = LT.gauss_log_prob(stats, keys, mus_c, sgs_c, idx=idx)
+    (lp_c * up).sum().backward()
+    g_c = [t.grad for t in mus_c + sgs_c]
+    # the same values as column blocks of one [B, 2F] (mu) and one [B, F]
+    # (sigma) buffer, like the generator's output
+    widths = [out[k]["mu"].shape[1] for k in keys]
+    f = sum(widths)
+    y = torch.zeros(B, 2 * f, device=gpu)
+    y[:, :f] = torch.cat([t.detach() for t in mus_c], 1)
+    sg_blk = torch.cat([t.detach() for t in sgs_c], 1)
+    mus = [t.detach().requires_grad_(True) for t in y[:, :f].split(widths, 1)]
+    sgs = [t.detach().requires_grad_(True) for t in sg_blk.split(widths, 1)]
+    assert mus[1].stride(0) == 2 * f and sgs[1].stride(0) == f
+    lp_s = LT.gauss_log_prob(stats, keys, mus, sgs, idx=idx)
+    (lp_s * up).sum().backward()
+    assert torch.equal(lp_s.detach(), lp_c.detach())
+    for a, b in zip([t.grad for t in mus + sgs], g_c):
+        assert torch.equal(a, b)
