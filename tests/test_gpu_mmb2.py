@@ -506,9 +506,13 @@ def test_gpu2_rejects_combinations_that_are_not_concatenations(gpu, golden):
     assert M.row_rel_err(ok.cpu().numpy(), z["cs_f64"]) < TOL
 
 
-def test_full_size_step_sampled_rows_vs_oracle(gpu):
+@pytest.mark.parametrize("T,V,A,Vd", [(40, 400_000, 300, 300), (20, 3016, 76, 48)],
+                         ids=["configs3", "configs1_mosi"])
+def test_full_size_step_sampled_rows_vs_oracle(gpu, T, V, A, Vd):
     """BASELINE configs[3] at full size (1M utterances x 40 x 3 x 300-d, V =
-    400k, Zipf ids): the bench step itself, checked against the oracle where
+    400k, Zipf ids) and configs[1] at 1M utterances of MOSI shape (T = 20,
+    COVAREP 76, FACET 48, V = 3016: the two-kernel step with the narrow-frame
+    stream kernel): the bench step itself, checked against the oracle where
     the check is size-independent.  MMB2 rows are per-utterance: 512 sampled
     rows against the oracle's sif2.estimate_embedding_overall_gpu2 on those
     rows (1e-5).  The SIF a2 rows of the sample against the oracle's
@@ -518,12 +522,12 @@ def test_full_size_step_sampled_rows_vs_oracle(gpu):
     oracle's removal with that PC (1e-5)."""
     from oracle import sif_oracle as O
 
-    N, T, V = 1_000_000, 40, 400_000
-    inp = synth.device_workload(N, T, V, seed=1, device=gpu)
+    N = 1_000_000
+    inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=1, device=gpu)
     torch.manual_seed(0)
-    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
     step = P.FusedStep(inp, gen.networks())
-    assert step.gram_i8
+    assert step.gram_i8 and step.stream_project == (A == 300)
     sif_out, mm2_out = step.run()
     step.check()
     torch.cuda.synchronize()
