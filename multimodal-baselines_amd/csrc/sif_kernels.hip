@@ -1054,7 +1054,9 @@ constexpr int kCmaxRows = 8192;
 // ONE packed instruction (16 instead of 40 text loads per utterance) 3.89 vs
 // 3.85 with 5-row groups, 4.44 with 10; the next utterance's ids resolved
 // before the row stores (kept: no iteration starts by waiting for the
-// previous row's stores) 3.87 vs 3.81.
+// previous row's stores) 3.87 vs 3.81; slot partials with 7 / 10 text rows
+// per group (occupancy 2) 4.31 / 3.90, 7 rows forced to occupancy 3 (7 VGPRs
+// spilled) 4.09 vs 3.84.
 // Timing-only ablations of 3 (wrong rows): no text 3.14 (6), no frames 2.32
 // (7), no row stores 3.61 (8), neither text nor frames 1.41 (9).
 static int narrow_variant() {
