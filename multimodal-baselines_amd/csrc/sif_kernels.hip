@@ -708,10 +708,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 // 3 rows = 912 contiguous bytes of audio, 5 rows = 960 B of visual; lanes past
 // P U load a duplicate), and ALL of an utterance's frame instructions (7 + 4
 // at T = 20) are issued together, before its text groups: one HBM round trip
-// per utterance for ~10 KB.  The
-// token ids of the next utterance are loaded one utterance ahead and its
-// weights gathered before the loop turns, so a text group waits for nothing
-// but the (L2-resident at MOSI's V = 3016) table rows.
+// per utterance for ~10 KB.  The token ids of the next utterance are loaded
+// one utterance ahead and its weights gathered before the loop turns, so a
+// text group waits for nothing but the (L2-resident at MOSI's V = 3016) table
+// rows.  (The last iteration resolves its own ids a second time: an
+// out-of-range id sets the same flag bit again.)
 // Sums: the text sums (and so x, aux's count and weight sum, the column
 // bounds) are utt_wave_kernel's operations in its order: bit-identical.  The
 // frame sums (FR = 1, the product) are per-lane partials over the rows of one
