@@ -313,9 +313,10 @@ def optimize_latents(args, train: bool, gen_model, embed_arr, dataloader, n_epoc
     graphs = None
     if USE_GRAPHS:
         def body(j):
-            out = gen_model(embeddings[j])
+            e = embeddings[j]  # one gather for both uses (see the e2e body below)
+            out = gen_model(e)
             sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
-            lp, mins = objective.log_prob_nocheck(embeddings[j], out, j)
+            lp, mins = objective.log_prob_nocheck(e, out, j)
             avg_log_prob = (-lp).mean()
             avg_log_prob.backward()
             return out, torch.cat([avg_log_prob.detach().view(1), sig, mins])
@@ -558,10 +559,17 @@ def main(argv=None):
             lw = args["likelihood_weight"]
 
             def body(j):
-                out = gen_model(train_embed[j])
+                # ONE gather of the batch's latents for the generator, the
+                # objective and the regressor (the reference indexes three
+                # times: three sort-based index backwards and two dense adds
+                # of the [N, 300] gradient per step; here the three gradient
+                # contributions are summed on the [B, 300] rows and scattered
+                # once -- the same three terms per row)
+                e = train_embed[j]
+                out = gen_model(e)
                 sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
-                lp, mins = train_obj.log_prob_nocheck(train_embed[j], out, j)
-                senti_loss = loss_function(senti_model(train_embed[j]), senti_labels[j])
+                lp, mins = train_obj.log_prob_nocheck(e, out, j)
+                senti_loss = loss_function(senti_model(e), senti_labels[j])
                 if sentiment_train_idxes is not None:
                     senti_loss = senti_loss * senti_mask[j]
                 senti_loss = senti_loss.mean(dim=-1)

@@ -113,10 +113,11 @@ def run(cfg, objective, gen, senti, lat0, label, dev, steps, batch, warm=2, grap
         lw = cfg["likelihood_weight"]
 
         def body(j):
-            out = gen(lat[j])
+            e = lat[j]  # one gather (simplesif's graph body)
+            out = gen(e)
             sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
-            lp, mins = graph_obj.log_prob_nocheck(lat[j], out, j)
-            sl = l1(senti(lat[j]), lab[j]).mean(dim=-1)
+            lp, mins = graph_obj.log_prob_nocheck(e, out, j)
+            sl = l1(senti(e), lab[j]).mean(dim=-1)
             lm = (lw * (-lp) + (1 - lw) * sl).mean()
             lm.backward()
             return out, torch.cat([lm.detach().view(1), sig, mins])
