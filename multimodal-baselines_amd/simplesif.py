@@ -168,23 +168,46 @@ class Objective:
         return combine_weighted(self.args, {k: lp[i] for i, k in enumerate(keys)}, word), mins
 
 
-def check_step(out, mins_all, latents_size):
+def sigma_mins(out):
+    """|min sigma| for the per-step 'boo!' check, as device values: one min
+    over the generator's whole sigma block when the keys' sigmas are column
+    views of one tensor (models.py's fused head), else one per key.  check_step
+    reads which form it got from its length."""
+    sigs = [d["sigma"] for d in out.values()]
+    base = sigs[0]._base
+    if base is not None and all(t._base is base for t in sigs) and base.dim() == 2 and \
+            sum(t.shape[1] for t in sigs) == base.shape[1]:
+        return base.detach().amin().abs().view(1)
+    return torch.stack([t.detach().min() for t in sigs]).abs()
+
+
+def check_step(out, mins_all, latents_size, n_sig=None):
     """The reference's per-step host checks, in its order, from one device
     read: sigma < 1e-7 prints (simplesif.py:82-84 / 724-726), a word
     log-prob of inf exits (simplesif.py:517-523), a Gaussian one of inf
-    exits (losses.py:258-264).  mins_all = [loss, sigma mins (K), word min,
-    Gaussian mins (K)]; returns the loss."""
+    exits (losses.py:258-264).  mins_all = [loss, sigma mins (n_sig: K, or 1
+    from sigma_mins' whole-block form), word min, Gaussian mins (K)]; returns
+    the loss.  With one block minimum the per-key minima are read from `out`
+    only when it is below the threshold (the step's tensors are still intact:
+    the next replay has not been launched)."""
     v = mins_all.cpu().numpy()
     K = len(out)
-    for (modality, d), m in zip(out.items(), v[1:1 + K]):
+    ns = K if n_sig is None else n_sig
+    if ns == K:
+        per_key = v[1:1 + K]
+    elif float(v[1]) < 1e-7:
+        per_key = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs().cpu().numpy()
+    else:
+        per_key = [1.0] * K
+    for (modality, d), m in zip(out.items(), per_key):
         if float(m) < 1e-7:
             print(d, "boo!")
-    if float(v[1 + K]) == np.inf:
+    if float(v[1 + ns]) == np.inf:
         print("word inf")
         print(latents_size)
         sys.exit()
     bad = False
-    for k, m in zip(out.keys(), v[2 + K:]):
+    for k, m in zip(out.keys(), v[2 + ns:]):
         if float(m) == np.inf:
             print(k, "inf")
             bad = True
@@ -315,7 +338,7 @@ def optimize_latents(args, train: bool, gen_model, embed_arr, dataloader, n_epoc
         def body(j):
             e = embeddings[j]  # one gather for both uses (see the e2e body below)
             out = gen_model(e)
-            sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
+            sig = sigma_mins(out)
             lp, mins = objective.log_prob_nocheck(e, out, j)
             avg_log_prob = (-lp).mean()
             avg_log_prob.backward()
@@ -329,7 +352,8 @@ def optimize_latents(args, train: bool, gen_model, embed_arr, dataloader, n_epoc
             iters += 1
             if graphs is not None:
                 out, vals = graphs.step(j, optimizer)
-                epoch_loss += check_step(out, vals, embeddings[:len(j)].size())
+                epoch_loss += check_step(out, vals, embeddings[:len(j)].size(),
+                                         len(vals) - 2 - len(out))
                 continue
             optimizer.zero_grad()
             out = gen_model(embeddings[j])
@@ -567,7 +591,7 @@ def main(argv=None):
                 # once -- the same three terms per row)
                 e = train_embed[j]
                 out = gen_model(e)
-                sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
+                sig = sigma_mins(out)
                 lp, mins = train_obj.log_prob_nocheck(e, out, j)
                 senti_loss = loss_function(senti_model(e), senti_labels[j])
                 if sentiment_train_idxes is not None:
@@ -586,7 +610,8 @@ def main(argv=None):
                 if graphs is not None:
                     iters += 1
                     out, vals = graphs.step(j, optimizer)
-                    epoch_loss += check_step(out, vals, train_embed[:len(j)].size())
+                    epoch_loss += check_step(out, vals, train_embed[:len(j)].size(),
+                                             len(vals) - 2 - len(out))
                     continue
                 _, s_data = senti_train_data[j]
                 iters += 1

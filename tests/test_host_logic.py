@@ -177,3 +177,30 @@ def test_word_weights_file_and_mosi_table(tmp_path, monkeypatch, capsys):
     np.testing.assert_array_equal(tab, [0.0, ww["the"], 1.0, 0.0, ww["cat"]])
     assert "# of words with unknown weight 1" in capsys.readouterr().out
     np.testing.assert_array_equal(sif.load_mosi_weights(), tab)  # the cached table
+
+
+def test_check_step_sigma_block_form(capsys):
+    """simplesif.check_step with the whole-block sigma minimum (sigma_mins on
+    the fused generator head's column views): 'boo!' printed for exactly the
+    keys whose own sigma minimum is below 1e-7 (read from `out` only then),
+    nothing otherwise; the per-key form gives the same prints."""
+    import simplesif
+
+    blk = torch.full((4, 6), 0.5)
+    views = blk.split([2, 1, 3], dim=1)
+    out = {k: {"mu": torch.zeros_like(v), "sigma": v} for k, v in zip(("audio", "visual", "audiovisual"), views)}
+    rest = torch.tensor([0.0, 1.0, 2.0, 3.0])  # word min, three Gaussian mins (finite)
+    loss = torch.tensor([7.0])
+    sig = simplesif.sigma_mins(out)
+    assert sig.shape == (1,)
+    vals = torch.cat([loss, sig, rest])
+    assert simplesif.check_step(out, vals, (4, 300), len(vals) - 2 - len(out)) == 7.0
+    assert "boo!" not in capsys.readouterr().out
+    blk[2, 3] = 1e-9  # column 3: the third key
+    sig = simplesif.sigma_mins(out)
+    simplesif.check_step(out, torch.cat([loss, sig, rest]), (4, 300), 1)
+    text = capsys.readouterr().out
+    assert text.count("boo!") == 1 and "1.0000e-09" in text  # the third key's dict
+    per_key = torch.stack([d["sigma"].min() for d in out.values()]).abs()
+    simplesif.check_step(out, torch.cat([loss, per_key, rest]), (4, 300))
+    assert capsys.readouterr().out == text

@@ -115,7 +115,7 @@ def run(cfg, objective, gen, senti, lat0, label, dev, steps, batch, warm=2, grap
         def body(j):
             e = lat[j]  # one gather (simplesif's graph body)
             out = gen(e)
-            sig = torch.stack([d["sigma"].detach().min() for d in out.values()]).abs()
+            sig = simplesif.sigma_mins(out)
             lp, mins = graph_obj.log_prob_nocheck(e, out, j)
             sl = l1(senti(e), lab[j]).mean(dim=-1)
             lm = (lw * (-lp) + (1 - lw) * sl).mean()
@@ -127,7 +127,7 @@ def run(cfg, objective, gen, senti, lat0, label, dev, steps, batch, warm=2, grap
         def gstep():
             j = torch.randperm(n, generator=g)[:batch]
             out, vals = graphs.step(j, opt)
-            return simplesif.check_step(out, vals, lat[:batch].size())
+            return simplesif.check_step(out, vals, lat[:batch].size(), len(vals) - 2 - len(out))
 
         for _ in range(warm):
             gstep()
