@@ -25,7 +25,7 @@ the same way:
 * g8_matrix: every parameter gradient larger than 50 KB keeps every 16th row
   (larger than 20 KB: every 4th) plus the whole tensor's max |.| (the per-tensor scale of the gradient check)
   -- the test compares those rows against that scale.
-* g9_cli_*: the pre / post embeddings keep every 4th row (`rows`); the test
+* g9_cli_*: the pre / post embeddings keep every 8th row (`rows`); the test
   compares those rows with the same row-relative bars.
 * seeded inputs (g7, g8, g5_senti_step: numpy default_rng / torch CPU
   generator streams) and the a2 rows `emb` (g1*, g2, g3, g3b: the BLAS-free
@@ -152,7 +152,7 @@ def slim_g9(variant):
     z = load(name)
     if "rows" in z:
         return
-    rows = np.arange(0, z["pre"].shape[0], 4)
+    rows = np.arange(0, z["pre"].shape[0], 8)
     z["rows"] = rows
     z["pre"] = z["pre"][rows]
     z["post"] = z["post"][rows]

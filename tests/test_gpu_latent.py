@@ -218,7 +218,7 @@ def test_cli_matches_reference_run(gpu, tmp_path, monkeypatch, variant, graphs):
     assert files == ref["files"]
     pre = torch.load(run / "pre/embed.bin", weights_only=True).detach().cpu().numpy()
     post = torch.load(run / "post/embed.bin", weights_only=True).detach().cpu().numpy()
-    if "rows" in arr.files:  # the fixture keeps every 4th row (tests/golden/slim_goldens.py)
+    if "rows" in arr.files:  # the fixture keeps every 8th row (tests/golden/slim_goldens.py)
         pre, post = pre[arr["rows"]], post[arr["rows"]]
     e_pre, e_post = row_rel(pre, arr["pre"]), row_rel(post, arr["post"])
     print(f"{variant}: pre {e_pre:.2e} post {e_post:.2e}")
