@@ -396,6 +396,16 @@ int mmb_gauss_backward_strided(const double* const* stats, const int* fm, const 
                                const int64_t* ld_sigma, const float* dlp, float* const* dmu,
                                float* const* dsigma, hipStream_t stream);
 
+/* Backward of the generator's LayerNorm (reference models.py:163-164,
+ * nn.LayerNorm(embedding_dim); its backward is torch's).  dy, x, dx: [n, d]
+ * row-major f32; mean, rstd: [n], the forward's saved statistics
+ * (torch.native_layer_norm); gamma: [d].  Writes dx and, when non-null,
+ * dgamma = sum_rows dy xhat and dbeta = sum_rows dy (fixed reduction order:
+ * deterministic).  One launch. */
+int mmb_layer_norm_backward(const float* dy, const float* x, const float* mean, const float* rstd,
+                            const float* gamma, int64_t n, int d, float* dx, float* dgamma,
+                            float* dbeta, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

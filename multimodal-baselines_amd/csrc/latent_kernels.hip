@@ -591,3 +591,87 @@ extern "C" int mmb_gauss_backward(const double* const* stats, const int* fm, con
   return mmb_gauss_backward_strided(stats, fm, idx, b, nkeys, mods, mu, nullptr, sigma, nullptr,
                                     dlp, dmu, dsigma, stream);
 }
+
+// ------------------------------------------------------------ LayerNorm backward
+// The generator's optional LayerNorm (reference models.py:163-164:
+// nn.LayerNorm(embedding_dim) ahead of the mu / log-sigma heads) trains with the
+// latents (e2e).  torch's backward is two launches, one of them a column
+// reduction that runs ~21 us for a 64 x 300 batch; here ONE launch: blocks
+// [0, rb) take 4 rows each (one wave per row: dx), blocks [rb, rb + cb) take
+// 64 columns each (4 row groups, fixed-order LDS combine: dgamma, dbeta —
+// deterministic).  xhat = (x - mean) rstd from the forward's saved statistics;
+//   dx = rstd (g - (sum g + xhat sum g xhat) / D),  g = dy gamma.
+__global__ __launch_bounds__(256) void ln_backward_kernel(
+    const float* __restrict__ dy, const float* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ gamma, float* __restrict__ dx,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t n, int d, int rb) {
+  const int tid = threadIdx.x;
+  if (static_cast<int>(blockIdx.x) < rb) {
+    const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (tid >> 6);
+    if (r >= n) return;
+    const int lane = tid & 63;
+    const float mu = mean[r], rs = rstd[r];
+    const float* dyr = dy + r * d;
+    const float* xr = x + r * d;
+    float a = 0.f, b = 0.f;
+    for (int c = lane; c < d; c += 64) {
+      const float g = dyr[c] * gamma[c];
+      a += g;
+      b += g * ((xr[c] - mu) * rs);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o);
+      b += __shfl_xor(b, o);
+    }
+    const float inv_d = 1.f / static_cast<float>(d);
+    float* dxr = dx + r * d;
+    for (int c = lane; c < d; c += 64) {
+      const float xh = (xr[c] - mu) * rs;
+      dxr[c] = rs * (dyr[c] * gamma[c] - (a + xh * b) * inv_d);
+    }
+    return;
+  }
+  __shared__ float part[2][4][64];
+  const int cl = tid & 63, rg = tid >> 6;
+  const int c = (static_cast<int>(blockIdx.x) - rb) * 64 + cl;
+  float sg = 0.f, sb = 0.f;
+  if (c < d) {
+#pragma unroll 4
+    for (int64_t r = rg; r < n; r += 4) {
+      const float g = dy[r * d + c];
+      sg += g * ((x[r * d + c] - mean[r]) * rstd[r]);
+      sb += g;
+    }
+  }
+  part[0][rg][cl] = sg;
+  part[1][rg][cl] = sb;
+  __syncthreads();
+  if (rg == 0 && c < d) {
+    if (dgamma) dgamma[c] = (part[0][0][cl] + part[0][1][cl]) + (part[0][2][cl] + part[0][3][cl]);
+    if (dbeta) dbeta[c] = (part[1][0][cl] + part[1][1][cl]) + (part[1][2][cl] + part[1][3][cl]);
+  }
+}
+
+extern "C" int mmb_layer_norm_backward(const float* dy, const float* x, const float* mean,
+                                       const float* rstd, const float* gamma, int64_t n, int d,
+                                       float* dx, float* dgamma, float* dbeta,
+                                       hipStream_t stream) {
+  MMB_REQUIRE(gamma && n >= 0 && d > 0);
+  if (n == 0) {  // (empty tensors may hand over null row pointers)
+    for (float* p : {dgamma, dbeta}) {
+      if (!p) continue;
+      const hipError_t e = hipMemsetAsync(p, 0, sizeof(float) * d, stream);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return MMB_OK;
+  }
+  MMB_REQUIRE(dy && x && mean && rstd && dx && n <= (int64_t{1} << 33));
+  const int64_t rb = ceil_div(n, int64_t{4});
+  const int cb = (dgamma || dbeta) ? static_cast<int>(ceil_div(int64_t{d}, int64_t{64})) : 0;
+  MMB_REQUIRE(rb + cb < (int64_t{1} << 31));
+  ln_backward_kernel<<<static_cast<unsigned>(rb + cb), 256, 0, stream>>>(
+      dy, x, mean, rstd, gamma, dx, dgamma, dbeta, n, d, static_cast<int>(rb));
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}

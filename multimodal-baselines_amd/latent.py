@@ -11,6 +11,8 @@ torch autograd Functions with hand-written backward passes:
   _GaussLogProb  the Gaussian log-likelihood of every combination from
                  per-utterance masked frame sums (streamed once per split);
                  backward: closed-form d lp / d mu, d lp / d sigma
+  layer_norm     the generator's LayerNorm: torch's forward, backward in ONE
+                 libmmb launch (dx + deterministic dgamma / dbeta)
 
 Gradients flow to the latents and, through torch's own autograd, to the
 generator (norm + linears) and the regressor, exactly as in the reference
@@ -227,3 +229,39 @@ def gauss_log_prob(gs: GaussStats, keys, mus, sigmas, idx=None):
     if idx is not None:
         idx = idx.to(device=mus[0].device, dtype=torch.int64).contiguous()
     return _GaussLogProb.apply(gs, idx, mods, *mus, *sigmas)
+
+
+class _LayerNorm(torch.autograd.Function):
+    """nn.LayerNorm over the last dim (reference models.py:163-164); the forward
+    is torch's (native_layer_norm, which also returns the row mean / rstd), the
+    backward is `mmb_layer_norm_backward` — one launch where torch's takes two,
+    its column reduction ~21 us for a 64 x 300 batch (profiles/r03_latent)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D).contiguous()
+        y, mean, rstd = torch.native_layer_norm(x2, [D], weight, bias, eps)
+        ctx.save_for_backward(x2, mean, rstd, weight)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, mean, rstd, w = ctx.saved_tensors
+        N, D = x2.shape
+        dy2 = dy.reshape(N, D).contiguous()
+        dx = torch.empty_like(x2)
+        dw = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        db = torch.empty_like(w) if ctx.needs_input_grad[2] else None
+        L.call("mmb_layer_norm_backward", L.ptr(dy2), L.ptr(x2), L.ptr(mean), L.ptr(rstd),
+               L.ptr(w), N, D, L.ptr(dx), L.ptr(dw), L.ptr(db), L.stream_ptr())
+        return dx.view(ctx.shape), dw, db, None
+
+
+def layer_norm(x, weight, bias, eps):
+    """LayerNorm with the libmmb backward (f32 device tensors, affine)."""
+    for t in (x, weight, bias):
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise L.MMBError("layer_norm takes f32 device tensors")
+    return _LayerNorm.apply(x, weight.contiguous(), bias.contiguous(), eps)

@@ -88,6 +88,7 @@ SIGNATURES = {
     "mmb_gauss_backward": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_gauss_loglik_strided": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_gauss_backward_strided": (_I, [_P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_layer_norm_backward": (_I, [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P]),
 }
 
 _lib = None

@@ -316,3 +316,36 @@ def test_fused_generator_and_strided_gaussians(gpu):
     assert torch.equal(lp_s.detach(), lp_c.detach())
     for a, b in zip([t.grad for t in mus + sgs], g_c):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,d", [(0, 300), (1, 300), (64, 300), (1000, 300), (37, 17), (130, 1000)])
+def test_layer_norm_backward_matches_torch(n, d):
+    """models.LayerNorm (backward: mmb_layer_norm_backward) against torch's
+    nn.LayerNorm, both f32 on the device, same parameters and upstream
+    gradient: dx per row and dgamma / dbeta within 1e-5 of the tensor's
+    largest entry (different reduction order), the forward bit-identical
+    (it is torch's)."""
+    import models
+    gpu = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(n * 7 + d)
+    x = (torch.randn(n, d, generator=g) * 3 + 1).to(gpu)
+    dy = torch.randn(n, d, generator=g).to(gpu)
+    ours, ref = models.LayerNorm(d).to(gpu), torch.nn.LayerNorm(d).to(gpu)
+    with torch.no_grad():
+        w, b = torch.randn(d, generator=g), torch.randn(d, generator=g)
+        for m in (ours, ref):
+            m.weight.copy_(w)
+            m.bias.copy_(b)
+    outs = []
+    for m in (ours, ref):
+        xi = x.clone().requires_grad_(True)
+        y = m(xi)
+        y.backward(dy)
+        outs.append((y.detach(), xi.grad, m.weight.grad, m.bias.grad))
+    (y, dx, dw, db), (y_r, dx_r, dw_r, db_r) = outs
+    assert torch.equal(y, y_r)
+    if n:
+        err = (dx - dx_r).abs().amax(1) / dx_r.abs().amax(1).clamp_min(1e-30)
+        assert err.max().item() <= 1e-5
+    for a, r in ((dw, dw_r), (db, db_r)):
+        assert (a - r).abs().max().item() <= 1e-5 * max(r.abs().max().item(), 1e-30)
