@@ -18,8 +18,10 @@ import os
 import torch  # noqa: F401  (must precede the dlopen below)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# MMB_LIB_PATH: another build of the library (same-box A/B of kernel builds)
-LIB_PATH = os.environ.get("MMB_LIB_PATH") or os.path.join(HERE, "libmmb.so")
+# The product library.  No environment variable redirects it: the tools build
+# (libmmb_diag.so, timing-only variants that write wrong rows by design) is
+# loaded only by an explicit load(path) from tools/ or tests/variant_checks.py.
+LIB_PATH = os.path.join(HERE, "libmmb.so")
 
 MMB_FLAG_ID_RANGE = 1
 MMB_FLAG_ZERO_WEIGHTS = 2
@@ -98,20 +100,38 @@ class MMBError(RuntimeError):
     pass
 
 
-def load():
-    """dlopen libmmb.so once (no GPU needed to load or query symbols)."""
-    global _lib
+_loaded_path = None
+
+
+def load(path=None):
+    """dlopen the library once (no GPU needed to load or query symbols).
+
+    `path` (tools only) names another build, e.g. the tools build
+    libmmb_diag.so; it must be given before anything else loads the library,
+    and a second, different path raises instead of silently mixing builds."""
+    global _lib, _loaded_path
+    want = os.path.abspath(path) if path is not None else None
+    if _lib is not None:
+        if want is not None and want != _loaded_path:
+            raise MMBError(f"libmmb already loaded from {_loaded_path}; cannot switch to {want}")
+        return _lib
+    lib_path = want or LIB_PATH
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"libmmb.so not built at {LIB_PATH}; run `make -C "
+        if not os.path.exists(lib_path):
+            raise ImportError(f"libmmb not built at {lib_path}; run `make -C "
                               f"{os.path.join(HERE, 'csrc')}` or __graft_entry__.build()")
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(lib_path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        _loaded_path = lib_path
     return _lib
+
+
+def loaded_path():
+    return _loaded_path
 
 
 def call(name, *args):

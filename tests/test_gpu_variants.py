@@ -2,9 +2,11 @@
 
 The product library carries only the default kernels and reads no
 environment variable (`strings libmmb.so` has no MMB_* knob); the variants
-and timing-only ablations live in libmmb_diag.so (`make diag`).  Each group
-of tests/variant_checks.py runs in ONE child process with MMB_LIB_PATH set to
-that build; the fused-streamer group also dumps the group-at-a-time
+and timing-only ablations live in tools/diag/libmmb_diag.so (`make diag`, on
+request: build() does not make it and .gpurunignore keeps it off the GPU box
+unless a tools session asks for it -- these tests skip without it).  Each group
+of tests/variant_checks.py runs in ONE child process that loads that build
+explicitly; the fused-streamer group also dumps the group-at-a-time
 streamer's outputs, which the product library (this process) must reproduce
 bit for bit with its default streamer.
 """
@@ -20,13 +22,14 @@ import mmb_lib as L
 import variant_checks as VC
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DIAG = os.path.join(ROOT, "multimodal-baselines_amd", "libmmb_diag.so")
-pytestmark = pytest.mark.gpu
+DIAG = VC.DIAG_LIB
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.path.exists(DIAG),
+                                 reason="tools build absent (make -C multimodal-baselines_amd/csrc diag)")]
 
 
 def _child(group, tmp_path):
-    assert os.path.exists(DIAG), "libmmb_diag.so missing: build() runs `make diag`"
-    env = {**os.environ, "MMB_LIB_PATH": DIAG, "VARIANT_DUMP": str(tmp_path)}
+    env = {**os.environ, "VARIANT_DUMP": str(tmp_path)}
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "variant_checks.py"),
                         group], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -85,3 +85,26 @@ def test_invalid_arguments_rejected_without_gpu():
         mmb_lib.call("mmb_pc_solve", None, 300, None, 11, 1, 7, 0, None, None)
     with pytest.raises(mmb_lib.MMBError):
         mmb_lib.call("mmb_host_randn", 0, -1, None)
+
+
+def test_environment_cannot_redirect_the_product_library(tmp_path):
+    """MMB_LIB_PATH (the round-3 A/B hook) no longer exists: a fresh process
+    with it set to the tools build still loads libmmb.so; the tools build is
+    reachable only through an explicit mmb_lib.load(path)."""
+    import sys
+    diag = os.path.join(ROOT, "tools", "diag", "libmmb_diag.so")
+    code = ("import sys; sys.path.insert(0, %r); import mmb_lib; mmb_lib.load(); "
+            "print(mmb_lib.loaded_path())" % os.path.join(ROOT, "multimodal-baselines_amd"))
+    env = {**os.environ, "MMB_LIB_PATH": diag, "MMB_TOOLS_LIB": diag}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         check=True).stdout.strip().splitlines()[-1]
+    assert out == os.path.join(ROOT, "multimodal-baselines_amd", "libmmb.so")
+    src = open(os.path.join(ROOT, "multimodal-baselines_amd", "mmb_lib.py")).read()
+    assert "os.environ" not in src and "getenv" not in src
+
+
+def test_second_library_path_is_refused():
+    lib = mmb_lib.load()
+    assert mmb_lib.load() is lib
+    with pytest.raises(mmb_lib.MMBError):
+        mmb_lib.load(os.path.join(ROOT, "tools", "diag", "libmmb_diag.so"))

@@ -7,12 +7,12 @@ register-B (6) kernels and its tile-layout epilogue, the stream kernel's
 load/store policies and grid sizes, the fused kernel's group-at-a-time and
 pipelined streamers and its unbalanced tail, the one-row PC removal -- live in
 the tools build, libmmb_diag.so (`make diag`, -DMMB_DIAG), where MMB_* knobs
-select them per launch.  This script runs in a child process with
-MMB_LIB_PATH pointing at that build (tests/test_gpu_variants.py) and asserts
+select them per launch.  This script runs in a child process that loads
+that build explicitly (mmb_lib.load(path), tests/test_gpu_variants.py) and asserts
 that each variant reproduces the default path: bit-identical where the
 variant sums in the same order, within the stated bar otherwise.
 
-    MMB_LIB_PATH=.../libmmb_diag.so python tests/variant_checks.py <group>
+    make -C multimodal-baselines_amd/csrc diag && python tests/variant_checks.py <group>
 """
 from __future__ import annotations
 
@@ -22,6 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multimodal-baselines_amd")]
+DIAG_LIB = os.path.join(ROOT, "tools", "diag", "libmmb_diag.so")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -249,11 +250,11 @@ GROUPS = {"projection": check_projection, "fused_streamer": check_fused_streamer
 
 def main(argv):
     want = argv[1:] or list(GROUPS)
-    lib = os.path.basename(L.LIB_PATH)
-    if lib != "libmmb_diag.so":
-        print(f"variant_checks: needs the tools build (MMB_LIB_PATH=.../libmmb_diag.so), "
-              f"got {L.LIB_PATH}", file=sys.stderr)
+    if not os.path.exists(DIAG_LIB):
+        print(f"variant_checks: needs the tools build at {DIAG_LIB} (`make -C "
+              f"multimodal-baselines_amd/csrc diag`)", file=sys.stderr)
         return 2
+    L.load(DIAG_LIB)
     L.require_gpu()
     dev = torch.device("cuda", 0)
     for g in want:

@@ -18,8 +18,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the MMB_* knobs these runs flip live in the tools build (make -C multimodal-baselines_amd/csrc diag)
-os.environ.setdefault("MMB_LIB_PATH", os.path.join(ROOT, "multimodal-baselines_amd", "libmmb_diag.so"))
+DIAG_LIB = os.environ.get("MMB_TOOLS_LIB", os.path.join(ROOT, "tools", "diag", "libmmb_diag.so"))
 sys.path.insert(0, os.path.join(ROOT, "multimodal-baselines_amd"))
+import mmb_lib  # noqa: E402
+
+mmb_lib.load(DIAG_LIB)  # the tools build: explicit, never through the product loader
 
 import torch  # noqa: E402
 
