@@ -761,8 +761,10 @@ def latent_step_config(dev, steps=50, cpu_steps=3):
                       steps, args.batch, graph_obj=obj)
     ms_eager = LB.run(cfg, obj.log_prob, copy.deepcopy(gen), copy.deepcopy(senti), lat0, label,
                       dev, steps, args.batch)
-    ms_torch = LB.run(cfg, LB.eager_objective(cfg, data, dev), copy.deepcopy(gen).float(),
-                      copy.deepcopy(senti), lat0, label, dev, steps, args.batch)
+    # the reference's arithmetic on the GPU: torch's LayerNorm and regressor
+    # (no libmmb kernel in this leg)
+    ms_torch = LB.run(cfg, LB.eager_objective(cfg, data, dev), LB.plain_torch(gen).float(),
+                      LB.CpuSenti(senti), lat0, label, dev, steps, args.batch)
     # the word objective's forward kernel alone: B = 64 latents x V = 3016 words
     lat = (torch.randn(args.batch, 300, device=dev) * 0.5)
     j = torch.arange(args.batch, device=dev)
@@ -782,7 +784,7 @@ def latent_step_config(dev, steps=50, cpu_steps=3):
     cores, aff = host_threads()
     with cpu_threads(cores):
         cpu = torch.device("cpu")
-        ms_cpu = LB.run(cfg, LB.eager_objective(cfg, data, cpu), copy.deepcopy(gen).cpu(),
+        ms_cpu = LB.run(cfg, LB.eager_objective(cfg, data, cpu), LB.plain_torch(gen).cpu(),
                         LB.CpuSenti(senti), lat0, label, cpu, cpu_steps, args.batch, warm=1)
     return {"workload": "e2e latent step at MOSI shape: batch 64, V = 3016, T = 20, audio 75+2, "
                         "visual 46+2 (simplesif.py:712-790)",

@@ -583,11 +583,15 @@ __global__ __launch_bounds__(256) void gram_tri_reduce_kernel(const double* __re
   }
 }
 
-static void launch_tri_reduce(const double* part, int d, int nt, int R, int accumulate, double* g,
-                              hipStream_t stream) {
+static int launch_tri_reduce(const double* part, int d, int nt, int R, int accumulate, double* g,
+                             hipStream_t stream) {
+  // the kernel sums ranges u + 8 j (j < R / 8, at most kRedMaxPer per thread)
+  // for R >= 8: a plan outside that would silently drop ranges
+  MMB_REQUIRE(R >= 1 && (R < 8 || (R % 8 == 0 && R <= 8 * kRedMaxPer)));
   const int64_t total = static_cast<int64_t>(nt) * (nt + 1) / 2 * 256;
   gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, kRedEl)), 256, 0, stream>>>(
       part, d, nt, R, accumulate, g);
+  return MMB_OK;
 }
 
 // Fixed-order sum over the S row chunks (deterministic), mirrored to both halves.
@@ -1765,16 +1769,29 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) {
+        // release: the tile stores above are visible at agent scope before
+        // the arrival that announces them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!(last && t != 0)) {
           if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) s_abort = 1;
+          // acquire: the gather below reads the other workgroups' tiles only
+          // after their arrivals were observed (the __syncthreads that follows
+          // releases the other waves of this workgroup)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
       }
     }
     if (last && t != 0) return;  // the tail runs on workgroup 0 only
     PC_MARK(2 + 3 * r);
     __syncthreads();
-    if (s_abort) return;
+    if (s_abort) {
+      // no caller may go on with a stale PC: an aborted solve leaves NaN in
+      // pc_out (every aborting workgroup writes the same NaNs; workgroup 0
+      // cannot complete the tail once any workgroup has left)
+      for (int e = tid; e < npc * D; e += kP16NT) pc_out[e] = __builtin_nan("");
+      return;
+    }
     PC_MARK(3 + 3 * r);
     // gather every tile into sY and the partial Grams: all of a thread's
     // loads (sc1, 8 B: the table's first row) issued before any is used
@@ -2134,7 +2151,10 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
     const size_t lds = gram2_lds();
     gram_tri_kernel<<<2 * q.R, kG2NT, lds, stream>>>(num, cnt, n, d, q.nt, q.R, q.chunk, q.xcd, 0, part);
     MMB_LAUNCH_CHECK();
-    launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
+    {
+      const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
+      if (rc != MMB_OK) return rc;
+    }
     MMB_LAUNCH_CHECK();
     return MMB_OK;
   }
@@ -2189,7 +2209,10 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
   launch_gram_i8<0>(x, colmax, n, d, q, part, stream);
 #endif
   MMB_LAUNCH_CHECK();
-  launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
+  {
+    const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
+    if (rc != MMB_OK) return rc;
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -2209,7 +2232,10 @@ extern "C" int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate,
                                hipStream_t stream) {
   MMB_REQUIRE(g && ws && n_plan >= 0 && d > 0 && d % 4 == 0 && d <= 320);
   const Gram2Plan q = gram2_plan(n_plan, d);
-  launch_tri_reduce(static_cast<const double*>(ws), d, q.nt, q.R, accumulate, g, stream);
+  {
+    const int rc = launch_tri_reduce(static_cast<const double*>(ws), d, q.nt, q.R, accumulate, g, stream);
+    if (rc != MMB_OK) return rc;
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

@@ -199,6 +199,13 @@ class _GaussLogProb(torch.autograd.Function):
             base = ts[0]
             same = all(t.stride(0) == lds[0] and t.untyped_storage().data_ptr() ==
                        base.untyped_storage().data_ptr() for t in ts)
+            if same:
+                # one slot per key only if the keys' column blocks are disjoint
+                # (one tensor or overlapping views passed for two keys would
+                # otherwise share a slot: the kernel keeps one key's gradient
+                # and autograd adds it once per key)
+                blocks = sorted((t.storage_offset(), t.shape[1]) for t, n in zip(ts, need) if n)
+                same = all(o0 + w0 <= o1 for (o0, w0), (o1, _) in zip(blocks, blocks[1:]))
             if not same:
                 return [torch.empty_like(t) if n else None for t, n in zip(ts, need)]
             lo = min(t.storage_offset() for t in ts)

@@ -47,11 +47,14 @@ def combo_dims(key: str, D: int, A: int, Vd: int) -> list[tuple[str, int]]:
 
 class LayerNorm(nn.LayerNorm):
     """nn.LayerNorm (same parameters, state-dict keys and forward) whose
-    backward on the device is one libmmb launch (`latent.layer_norm`); CPU
-    tensors (the host-side tests) take torch's."""
+    backward on the device is one libmmb launch (`latent.layer_norm`, f32
+    only); CPU tensors (the host-side tests) and other dtypes (a generator cast
+    to .double() / .half()) take torch's, as nn.LayerNorm would."""
 
     def forward(self, x):
-        if x.is_cuda and self.weight is not None and self.bias is not None:
+        if (x.is_cuda and self.weight is not None and self.bias is not None
+                and x.dtype == self.weight.dtype == self.bias.dtype == torch.float32
+                and self.weight.is_cuda):
             return LT.layer_norm(x, self.weight, self.bias, self.eps)
         return super().forward(x)
 

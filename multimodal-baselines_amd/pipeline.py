@@ -203,16 +203,25 @@ def pc_solve(G: torch.Tensor, z0: torch.Tensor, npc: int, transposed: bool,
              n_iter: int = N_ITER, out: torch.Tensor | None = None,
              flag: torch.Tensor | None = None, ws: torch.Tensor | None = None) -> torch.Tensor:
     """sklearn's randomized-SVD components from the Gram (a3's solve).  d <=
-    320: the multi-workgroup solver (mmb_pc_solve_mc; a hand-over timeout
-    sets MMB_FLAG_SYNC_TIMEOUT in `flag`); larger d: one workgroup."""
+    320: the multi-workgroup solver (mmb_pc_solve_mc); larger d: one
+    workgroup.  A hand-over timeout of the multi-workgroup solver leaves NaN
+    in the PC and sets MMB_FLAG_SYNC_TIMEOUT in `flag`: a caller that passes
+    its own flag (FusedStep, graph-capturable) checks it later; without one,
+    this call checks a flag of its own and raises here (one host sync)."""
     d = G.shape[0]
     k = z0.shape[1]
     pc = out if out is not None else torch.empty((npc, d), dtype=torch.float64, device=G.device)
     if d <= PC_SOLVE_MC_MAX_D and k <= 16:
         if ws is None:
             ws = solve_workspace(d, G.device)
+        own = flag is None
+        if own:
+            flag = torch.zeros(1, dtype=torch.int32, device=G.device)
         L.call("mmb_pc_solve_mc", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed),
                L.ptr(pc), L.ptr(ws), L.ptr(flag), L.stream_ptr())
+        if own and int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT:
+            raise RuntimeError("mmb_pc_solve_mc: a bounded hand-over between the solver's "
+                               "workgroups timed out; the PC is invalid (NaN)")
     else:
         L.call("mmb_pc_solve", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed), L.ptr(pc),
                L.stream_ptr())

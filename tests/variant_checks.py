@@ -231,9 +231,20 @@ def check_timeouts(dev):
     assert int(flag.item()) == 0
     try:
         assert lib.mmb_diag_pc_wait_iters(1) == 0
-        P.pc_solve(G, z0, 1, False, flag=flag)
+        pcx = P.pc_solve(G, z0, 1, False, flag=flag)
         torch.cuda.synchronize()
         assert int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT
+        assert bool(torch.isnan(pcx).all())  # never a stale PC
+        # callers that pass no flag raise too (pc_solve's own flag), and so
+        # does the composed a1-a5 path
+        for call in (lambda: P.pc_solve(G, z0, 1, False),
+                     lambda: P.sif_embeddings(inp["table"], inp["ids"][:2000], wtab32=inp["wtab"])):
+            try:
+                call()
+            except RuntimeError as e:
+                assert "timed out" in str(e)
+            else:
+                raise AssertionError("a no-flag PC solve did not raise on the hand-over timeout")
     finally:
         assert lib.mmb_diag_pc_wait_iters(1 << 20) == 0
     flag.zero_()

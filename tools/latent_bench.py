@@ -16,6 +16,7 @@ Gaussian combinations), the regressor, backward, SGD on latents + generator
 Prints one JSON line (ms per step, steps/s).
 """
 import argparse
+import copy
 import json
 import os
 import sys
@@ -161,6 +162,23 @@ def run(cfg, objective, gen, senti, lat0, label, dev, steps, batch, warm=2, grap
     return (time.perf_counter() - t0) / steps * 1e3
 
 
+def plain_torch(gen):
+    """A copy of the generator with every models.LayerNorm (libmmb backward on
+    the device) swapped for torch's nn.LayerNorm: the reference's arithmetic
+    for the torch legs."""
+    import models
+
+    g = copy.deepcopy(gen)
+    for name, mod in list(g.named_modules()):
+        for cname, child in list(mod.named_children()):
+            if isinstance(child, models.LayerNorm):
+                ln = torch.nn.LayerNorm(child.normalized_shape, eps=child.eps,
+                                        elementwise_affine=child.elementwise_affine)
+                ln.load_state_dict(child.state_dict())
+                setattr(mod, cname, ln.to(next(child.parameters()).device))
+    return g
+
+
 class CpuSenti(torch.nn.Module):  # the reference regressor in plain torch (no libmmb on CPU)
     def __init__(self, m):
         super().__init__()
@@ -202,12 +220,12 @@ def main():
     ms_graph = run(cfg, None, copy.deepcopy(gen), copy.deepcopy(senti), lat0, label, dev,
                    args.steps, args.batch, graph_obj=obj)
 
-    ms_eager = run(cfg, eager_objective(cfg, data, dev), copy.deepcopy(gen).float(),
-                   copy.deepcopy(senti), lat0, label, dev, args.steps, args.batch)
+    ms_eager = run(cfg, eager_objective(cfg, data, dev), plain_torch(gen).float(),
+                   CpuSenti(senti), lat0, label, dev, args.steps, args.batch)
     cpu = torch.device("cpu")
     from oracle import latent_oracle as LO  # noqa: F401  (cpu leg: the reference arithmetic)
 
-    ms_cpu = run(cfg, eager_objective(cfg, data, cpu), copy.deepcopy(gen).cpu(), CpuSenti(senti),
+    ms_cpu = run(cfg, eager_objective(cfg, data, cpu), plain_torch(gen).cpu(), CpuSenti(senti),
                  lat0, label, cpu, args.cpu_steps, args.batch, warm=1)
     print(json.dumps({"workload": f"e2e latent step, MOSI shape: batch {args.batch}, vocab "
                                   f"{args.vocab}, T {args.t}, audio {args.a}+2, visual {args.vd}+2",
