@@ -518,7 +518,9 @@ def test_full_size_step_sampled_rows_vs_oracle(gpu, T, V, A, Vd):
     rows (1e-5).  The SIF a2 rows of the sample against the oracle's
     get_weighted_average (2e-6), the step's PC (int8 Gram + device solve)
     against the oracle's randomized-SVD-from-Gram on the exact f64 Gram of
-    all 1M a2 rows (1e-9), and the sample's PC-removed rows against the
+    all 1M a2 rows AND against the sklearn-path restatement
+    (oracle.sif_oracle.compute_pc: LU-normalised power iteration on the 1M x
+    300 f64 X itself) (1e-9), and the sample's PC-removed rows against the
     oracle's removal with that PC (1e-5)."""
     from oracle import sif_oracle as O
 
@@ -549,10 +551,17 @@ def test_full_size_step_sampled_rows_vs_oracle(gpu, T, V, A, Vd):
     assert M.row_rel_err(x[rows], x_ref) < 2e-6
     X = x.astype(np.float64)
     G = X.T @ X
+    # the reference algorithm itself on all 1M rows: TruncatedSVD(1, n_iter=7,
+    # random_state=0)'s randomized SVD on X (sif_functions.py:58-67; the
+    # restatement is pinned bit for bit to sklearn 1.7.2 by
+    # test_oracle_golden.py), not only the device solver's CPU twin
+    pc_sk = O.compute_pc(X, 1)
     del X
     z0 = np.random.RandomState(0).normal(size=(300, 11))
     pc = O.pc_from_gram(G, z0, 1, False)
-    assert np.abs(step.pc.cpu().numpy() - pc).max() < 1e-9
+    got = step.pc.cpu().numpy()
+    assert np.abs(got - pc).max() < 1e-9
+    assert np.abs(got - pc_sk).max() < 1e-9
     sif_ref = x_ref - (x_ref @ pc.T) @ pc
     assert M.row_rel_err(sif_out[ridx].cpu().numpy(), sif_ref) < TOL
 
