@@ -805,6 +805,66 @@ def latent_step_config(dev, steps=50, cpu_steps=3):
             "speedup_vs_cpu": round(ms_cpu / ms_graph, 1)}
 
 
+def hbm_ceilings(dev, nbytes=4 << 30, reps=10):
+    """Same-process HBM ceilings (SURVEY §8d "a measured stream-copy
+    ceiling"): libmmb's float4 probes (non-temporal, 4 loads in flight per
+    lane) over `nbytes` -- far above the 256 MB Infinity Cache -- timed with
+    HIP events on the launch stream, best of a few grid sizes.  Copy counts
+    read + write bytes."""
+    import torch
+
+    import mmb_lib as L
+
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    cus = L.cu_count(dev)
+    sink = torch.empty(cus * 16, dtype=torch.int32, device=dev)
+    sp = L.stream_ptr()
+    out = {}
+    for name, launch, moved in (
+            ("copy", lambda b, nt: L.call("mmb_probe_copy", L.ptr(src), L.ptr(dst), nbytes, b, nt,
+                                          sp), 2 * nbytes),
+            ("read", lambda b, nt: L.call("mmb_probe_read", L.ptr(src), nbytes, b, nt,
+                                          L.ptr(sink), sp), nbytes)):
+        best, how = 0.0, None
+        for nt in (0, 1):
+            for per_cu in (1, 2, 4, 8):
+                b = cus * per_cu
+                launch(b, nt)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    launch(b, nt)
+                e1.record()
+                torch.cuda.synchronize()
+                r = moved * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+                out.setdefault("sweep", {})[f"{name}_nt{nt}_wg{per_cu}"] = round(r, 1)
+                if r > best:
+                    best, how = r, f"nt={nt}, {per_cu} workgroups per CU"
+        out[name] = round(best, 1)
+        out[name + "_config"] = how
+    del src, dst, sink
+    torch.cuda.empty_cache()
+    return out
+
+
+def annotate_ceilings(obj, ceil):
+    """Every GB/s roofline in the line gains the measured ceilings beside the
+    8 TB/s spec: copy_ceiling_gbs / read_ceiling_gbs and achieved over each."""
+    if isinstance(obj, dict):
+        if (str(obj.get("unit", "")).startswith("GB/s") and isinstance(obj.get("achieved"),
+                                                                      (int, float))):
+            obj["copy_ceiling_gbs"] = ceil["copy"]
+            obj["read_ceiling_gbs"] = ceil["read"]
+            obj["frac_of_ceiling"] = round(obj["achieved"] / ceil["copy"], 4)
+            obj["frac_of_read_ceiling"] = round(obj["achieved"] / ceil["read"], 4)
+        for v in obj.values():
+            annotate_ceilings(v, ceil)
+    elif isinstance(obj, list):
+        for v in obj:
+            annotate_ceilings(v, ceil)
+
+
 def dump_rows(path, rank, row0, step):
     """--dump-rows: this rank's PC and every 97th of its SIF / MMB2 rows (plus
     its last), for tests/test_gpu_bench_dist.py to compare with the unsharded
@@ -1078,6 +1138,17 @@ def main():
         except Exception as exc:  # keep the GPU line even if the host leg fails
             log(f"cpu baseline failed: {exc!r}")
     out["cpu_baseline"] = cpu
+    try:
+        ceil = hbm_ceilings(dev)
+        out["hbm_ceilings"] = {"copy_gbs": ceil["copy"], "read_gbs": ceil["read"],
+                               "copy_config": ceil["copy_config"],
+                               "read_config": ceil["read_config"], "sweep": ceil["sweep"],
+                               "note": "libmmb float4 probes (mmb_probe_copy / mmb_probe_read) "
+                                       "over 4 GiB in this process, best of the sweep; copy "
+                                       "counts read + write"}
+        annotate_ceilings(out, ceil)
+    except Exception as exc:  # keep the line
+        log(f"hbm ceilings failed: {exc!r}")
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -161,6 +161,18 @@ int mmb_pc_remove_f64(const double* x, int64_t n, int d, const double* pc, int n
  * mmb_cu_count writes the device's CU count.  No reference counterpart
  * (scheduling only).                                                         */
 int mmb_cu_count(int device, int* out);
+
+/* Bandwidth probes (measurement only, no reference counterpart): the
+ * same-process HBM ceilings the bench quotes beside the 8 TB/s spec (SURVEY.md
+ * §8d "a measured stream-copy ceiling").  16-byte words (nt != 0: non-temporal
+ * loads / stores), four loads in flight per lane, a grid of min(blocks,
+ * bytes / 4 KB) 256-thread workgroups.  mmb_probe_copy: dst = src (2 * bytes moved).  mmb_probe_read:
+ * reads src once and writes one word per workgroup into sink[blocks].
+ * bytes and both pointers must be 16-byte aligned.                           */
+int mmb_probe_copy(const void* src, void* dst, int64_t bytes, int blocks, int nt,
+                   hipStream_t stream);
+int mmb_probe_read(const void* src, int64_t bytes, int blocks, int nt, uint32_t* sink,
+                   hipStream_t stream);
 int mmb_stream_create_cu_mask(const uint32_t* cu_mask, int mask_words, hipStream_t* out);
 int mmb_stream_destroy(hipStream_t stream);
 

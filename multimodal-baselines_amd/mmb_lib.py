@@ -56,6 +56,8 @@ SIGNATURES = {
     "mmb_cu_count": (_I, [_I, _P]),
     "mmb_stream_create_cu_mask": (_I, [_P, _I, _P]),
     "mmb_stream_destroy": (_I, [_P]),
+    "mmb_probe_copy": (_I, [_P, _P, _L, _I, _I, _P]),
+    "mmb_probe_read": (_I, [_P, _L, _I, _I, _P, _P]),
     "mmb_calc_weights": (_I, [_P, _L, _I, _P, _P, _P, _P, _P]),
     "mmb_mm2_k": (_I, [_I, _I, _I]),
     "mmb_mm2_ldw": (_I, [_I]),
