@@ -646,6 +646,88 @@ def table_resident_roofline(roof, kb, U, D, T):
     return roof
 
 
+def _lat_ms(fn, dev, reps):
+    """Host wall per call (each call ends with a device sync): median, min."""
+    import statistics
+
+    import torch
+
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return round(statistics.median(ts), 4), round(min(ts), 4)
+
+
+def dataset_splits_config(P, models, synth, dev, reps=30):
+    """configs[0]/[1]/[2] at their real sizes and call pattern: SIF (+ its own
+    PC) and MMB2 once per split (simplesif.py:296-311; --time_test :862-880).
+    MOSI: train / valid / test = 1284 / 229 / 686 utterances, T = 20, A = 76,
+    Vd = 48 (synthetic: the MOSI h5 is absent).  POM: the reference's own
+    pom_valid_ids (100 x 1089) / pom_test_ids (203 x 1357) and
+    pom_word_weights.npy (tests/golden/g11_pom_splits.npz), V = 7763, aligned
+    300-d frames.  Per split: eager (FusedStep.run + its flag check), one HIP
+    graph replay per split (StepGraph), and all splits of a dataset in ONE
+    graph with concurrent branches (the splits' PC solves side by side).  Every
+    time is host wall around the call including the sync that reads the flag
+    (what a CLI user waits for), median of `reps`; phase_ms: HIP events of an
+    eager run.  SIF rows of the POM splits against the reference's recorded
+    rows (g11)."""
+    import numpy as np
+    import torch
+
+    from oracle import mmb2_oracle as M
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "g11_pom_splits.npz"), allow_pickle=False)
+    sets = {"mosi": (synth.mosi_splits(), ("train", "valid", "test"), 76, 48),
+            "pom": (synth.pom_splits(z["valid_ids"], z["test_ids"], z["weights"],
+                                     int(z["table_seed"])), ("valid", "test"), 300, 300)}
+    out = {}
+    for name, (splits, names, A, Vd) in sets.items():
+        torch.manual_seed(0)
+        gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(dev)
+        inps = [synth.to_device(sp, dev) for sp in splits]
+        steps = [P.FusedStep(inp, gen.networks()) for inp in inps]
+        res = {"splits": {}}
+        for nm, sp, st in zip(names, splits, steps):
+            st.run(check=True)
+            tr = {}
+            st.run(trace=tr)
+            torch.cuda.synchronize(dev)
+            ph = {k: round(sum(a.elapsed_time(b) for a, b in v), 4) for k, v in tr.items()}
+            eager = _lat_ms(lambda: st.run(check=True), dev, reps)
+            g = P.StepGraph(st)
+            graph = _lat_ms(lambda: g.run(check=True), dev, reps)
+            n, L = sp["ids"].shape
+            res["splits"][nm] = {"utts": n, "tokens": L, "eager_ms": eager[0],
+                                 "graph_ms": graph[0], "graph_ms_min": graph[1],
+                                 "phase_ms": ph, "kernel_ms": round(sum(ph.values()), 4)}
+            if name == "pom":
+                got = st.sif.double().cpu().numpy()[::int(z["row_step"])]
+                res["splits"][nm]["sif_row_rel_err_vs_reference"] = float(
+                    M.row_rel_err(got, z[f"{nm}_out_rows"]))
+            del g
+        gall = P.StepGraph(steps, concurrent=True)
+        allm = _lat_ms(lambda: gall.run(check=True), dev, reps)
+        gser = P.StepGraph(steps, concurrent=False)
+        serm = _lat_ms(lambda: gser.run(check=True), dev, reps)
+        res["all_splits_one_graph_concurrent_ms"] = allm[0]
+        res["all_splits_one_graph_serial_ms"] = serm[0]
+        res["per_split_ms_concurrent_graph"] = round(allm[0] / len(steps), 4)
+        res["utterances"] = int(sum(sp["ids"].shape[0] for sp in splits))
+        res["value_concurrent_graph"] = round(res["utterances"] / (allm[0] / 1e3), 1)
+        res["unit"] = "utterance-embeds/s (SIF + MMB2, every split with its own PC)"
+        out[name] = res
+        del gall, gser, steps, inps
+        torch.cuda.empty_cache()
+    out["note"] = ("host wall per call incl. the flag check's sync; graph-replay floor per "
+                   "the MI355X guide ~10-16 us per replay")
+    return out
+
+
 def mosi_mmb2_config(P, models, synth, dev, steps, warmup, U=1_000_000):
     """configs[1]: MMB2 at MOSI shape -- T = 20 aligned frames, COVAREP 74 + 2
     positional dims = 76, FACET 46 + 2 = 48 (make_configs.py:28),
@@ -918,6 +1000,8 @@ def main():
     ap.add_argument("--only-main", action="store_true",
                     help="skip per_rank_steps, configs_measured (the other BASELINE configs) and "
                          "the fp32 projection timing")
+    ap.add_argument("--only-leg", default=None,
+                    help="run only this configs_measured leg (e.g. dataset_splits) and print it")
     ap.add_argument("--launch-check", action="store_true",
                     help="only start the ranks and all-reduce a one (tests the launcher)")
     args = ap.parse_args()
@@ -963,6 +1047,14 @@ def main():
     import synth
 
     mmb_lib.require_gpu()
+    if args.only_leg:
+        legs = {"dataset_splits": lambda: dataset_splits_config(P, models, synth, dev),
+                "mosi_mmb2": lambda: mosi_mmb2_config(P, models, synth, dev, 5, 2),
+                "regressor": lambda: regressor_config(dev),
+                "latent_step": lambda: latent_step_config(dev),
+                "mmb1_sif_mosi": lambda: mmb1_sif_mosi_config(dev)}
+        print(json.dumps({args.only_leg: legs[args.only_leg]()}), flush=True)
+        return 0
     kind = args.workload
     dflt = {"synthetic": (1_000_000, 40, 400_000), "pom": (10_000, 1357, 7763),
             "ragged": (1_000_000, 64, 400_000), "mosi": (1_000_000, 20, 3016)}[kind]
@@ -1121,6 +1213,7 @@ def main():
         cm = {}
         for name, fn in (("mmb1_sif_mosi", lambda: mmb1_sif_mosi_config(dev)),
                          ("mosi_mmb2", lambda: mosi_mmb2_config(P, models, synth, dev, 5, 2)),
+                         ("dataset_splits", lambda: dataset_splits_config(P, models, synth, dev)),
                          ("ragged", lambda: ragged_config(P, models, synth, dev, 5, 2, U)),
                          ("pom", lambda: pom_config(P, models, synth, dev, 5, 2)),
                          ("regressor", lambda: regressor_config(dev)),

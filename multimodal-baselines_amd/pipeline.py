@@ -856,3 +856,57 @@ class FusedStep:
                 remove_pc(self.x[r0:r1], None, pc, out=self.sif[r0:r1])
         self.pc = pc
         return self.sif, self.mmb2
+
+
+class StepGraph:
+    """One or more FusedSteps' device work captured ONCE as a HIP graph and
+    replayed: the per-split call pattern of the reference (SIF once per split,
+    each split with its own PC: simplesif.py:296-311) pays the host launch
+    cost of ~10 kernels per split on every call; a replay is one launch.
+
+    `concurrent=True` captures every step on its own stream (fork / join
+    branches of the graph), so independent splits overlap on the chip -- the
+    PC solves of different splits (each ceil(d/16) workgroups) run side by
+    side instead of back to back.  Steps are warmed up eagerly first (weight
+    merge, Omega upload, workspaces); a later in-place update of a generator
+    parameter is re-merged eagerly before the replay (the merge writes the
+    buffers the graph reads).  No host sync unless `check`."""
+
+    def __init__(self, steps, concurrent: bool = False, warmup: int = 1):
+        self.steps = list(steps) if isinstance(steps, (list, tuple)) else [steps]
+        dev = self.steps[0].table.device
+        caller = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(caller)
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                for st in self.steps:
+                    st.run()
+        caller.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        for st in self.steps:
+            st.reset()
+        self._branches = ([torch.cuda.Stream(device=dev) for _ in self.steps]
+                          if concurrent and len(self.steps) > 1 else None)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            cap = torch.cuda.current_stream(dev)
+            if self._branches is None:
+                self.outs = [st._run(None) for st in self.steps]
+            else:
+                self.outs = []
+                for st, br in zip(self.steps, self._branches):
+                    br.wait_stream(cap)
+                    with torch.cuda.stream(br):
+                        self.outs.append(st._run(None))
+                for br in self._branches:
+                    cap.wait_stream(br)
+
+    def run(self, check: bool = False):
+        for st in self.steps:
+            st.proj.refresh_if_changed()
+        self.graph.replay()
+        if check:
+            for st in self.steps:
+                st.check()
+        return self.outs if len(self.steps) > 1 else self.outs[0]

@@ -217,3 +217,59 @@ def mm_splits(seed: int = 0, sizes=(96, 32, 32), T: int = 12, V: int = 300, A_ra
             d["text_id"] = tid
         splits.append(d)
     return word2ix, E, tuple(splits)
+
+
+# ---------------------------------------------------------------- per-split (real call pattern)
+MOSI_SPLITS = (1284, 229, 686)  # train / valid / test utterances (SURVEY.md §8 shapes)
+
+
+def split_arrays(ids: np.ndarray, E: np.ndarray, wt: np.ndarray, A: int, Vd: int,
+                 seed: int) -> dict:
+    """Host arrays of one split: ids [N, L] int64, the word table, the f64
+    weights, and aligned audio / visual frames [N, L, A|Vd] (U(-1, 1), -10 at
+    the time steps past each utterance's last non-zero id, utils.py:188-189)."""
+    n, L = ids.shape
+    rng = np.random.default_rng(seed)
+    nz = ids != 0
+    lens = np.where(nz.any(1), L - np.argmax(nz[:, ::-1], axis=1), 0)
+    pad = np.arange(L)[None, :] >= lens[:, None]
+    out = {"ids": ids, "table": E, "weights": wt}
+    for key, F in (("audio", A), ("visual", Vd)):
+        x = rng.uniform(-1.0, 1.0, size=(n, L, F)).astype(np.float32)
+        x[pad] = -10.0
+        out[key] = x
+    return out
+
+
+def mosi_splits(sizes=MOSI_SPLITS, L: int = 20, V: int = 3016, A: int = 76, Vd: int = 48,
+                seed: int = 21) -> list[dict]:
+    """configs[0]/[1] at their real call pattern: three MOSI-shaped splits
+    (1284 / 229 / 686 utterances, L = T = 20, V = 3016, COVAREP 74 + 2 and
+    FACET 46 + 2 positional dims) sharing one word table and weight table
+    (w0 = 0: MOSI pads carry no weight); ragged transcripts."""
+    E = word_table(V, 300, seed=seed)
+    wt = sif_weights(V, w0=0.0)
+    return [split_arrays(token_ids(n, L, V, seed=seed + 1 + i, ragged=True), E, wt, A, Vd,
+                         seed=seed + 11 + i) for i, n in enumerate(sizes)]
+
+
+def pom_splits(valid_ids, test_ids, weights, table_seed: int, A: int = 300,
+               Vd: int = 300) -> list[dict]:
+    """configs[2] at its real call pattern: the reference's own POM valid /
+    test id matrices (100 x 1089, 203 x 1357) and weights, the seeded V = 7763
+    word table (GloVe is absent), aligned frames of the transcripts' length."""
+    E = word_table(len(weights), 300, seed=table_seed)
+    return [split_arrays(np.asarray(ids, np.int64), E, np.asarray(weights, np.float64), A, Vd,
+                         seed=table_seed + 1 + i) for i, ids in enumerate((valid_ids, test_ids))]
+
+
+def to_device(split: dict, device) -> dict:
+    """A split's FusedStep inputs on the device (ids int32, wtab = the f32
+    rounding of the f64 weights, simplesif.py:315)."""
+    import torch
+
+    return {"table": torch.as_tensor(split["table"]).to(device),
+            "wtab": torch.as_tensor(split["weights"], dtype=torch.float32).to(device),
+            "ids": torch.as_tensor(split["ids"], dtype=torch.int32).to(device),
+            "audio": torch.as_tensor(split["audio"]).to(device),
+            "visual": torch.as_tensor(split["visual"]).to(device)}

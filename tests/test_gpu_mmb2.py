@@ -747,3 +747,86 @@ def test_narrow_frame_stream_kernel(gpu, N, T, A, Vd, V):
     assert int(f3.item()) == int(f4.item()) and int(f3.item()) & L.MMB_FLAG_ID_RANGE
     # (an utterance left with no valid token is 0 / 0 = NaN in both, as in numpy)
     assert torch.allclose(n3, n4, rtol=0, atol=0, equal_nan=True) and torch.equal(a3[:2], a4[:2])
+
+
+def _split_check(gen, sp, sif_out, mm2_out, pc, rows, ref_rows=None, ref_pc=None):
+    """One split against the oracle: SIF over the whole split (its own PC,
+    the reference's loops + sklearn-path randomized SVD), MMB2 on a row sample."""
+    E, wt, ids = sp["table"], sp["weights"], sp["ids"]
+    sif_ref = O.get_sentence_embeddings(E, wt, ids)
+    assert M.row_rel_err(sif_out.double().cpu().numpy(), sif_ref) < TOL
+    pc_ref = O.compute_pc(O.get_weighted_average(E, ids, O.seq2weight(ids, np.ones(ids.shape), wt)))
+    assert np.abs(pc.cpu().numpy() - pc_ref).max() < 1e-8
+    if ref_pc is not None:  # the reference's own run (g11)
+        assert np.abs(pc.cpu().numpy() - ref_pc).max() < 1e-8
+        assert M.row_rel_err(sif_out.double().cpu().numpy()[::8], ref_rows) < TOL
+    r = rows
+    sw = O.seq2weight(ids[r], np.ones(ids[r].shape), wt)
+    text = E[ids[r]]
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, sp["audio"][r], sp["visual"][r]),
+                                            M.params_from_module(gen), sw, text)
+    assert M.row_rel_err(mm2_out[torch.as_tensor(r, device=mm2_out.device)].cpu().numpy(),
+                         ref) < TOL
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+def test_real_pom_splits_vs_reference_and_oracle(gpu, golden, mode):
+    """configs[2] at its real call pattern: the reference's own pom_valid_ids
+    (100 x 1089) and pom_test_ids (203 x 1357) with pom_word_weights.npy, SIF
+    + MMB2 once per split, each split with its own PC (simplesif.py:296-311;
+    n < 300: sklearn's transposed branch).  SIF rows and PC against the
+    reference's recorded run (g11) and the oracle, MMB2 on 32 rows per split
+    against the oracle's sif2.estimate_embedding_overall_gpu2; the graph mode
+    (both splits in ONE HIP graph, concurrent branches) equals eager bit for bit."""
+    z = golden("g11_pom_splits")
+    splits = synth.pom_splits(z["valid_ids"], z["test_ids"], z["weights"], int(z["table_seed"]))
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    steps = [P.FusedStep(synth.to_device(sp, gpu), gen.networks()) for sp in splits]
+    eager = [[t.clone() for t in st.run(check=True)] for st in steps]
+    if mode == "graph":
+        g = P.StepGraph(steps, concurrent=True)
+        for _ in range(2):
+            outs = g.run(check=True)
+        for (s0, m0), (s1, m1) in zip(eager, outs):
+            assert torch.equal(s0, s1) and torch.equal(m0, m1)
+    gen_cpu = gen.cpu()
+    for nm, sp, st, (sif_out, mm2_out) in zip(("valid", "test"), splits, steps, eager):
+        rows = np.sort(np.random.default_rng(7).choice(sp["ids"].shape[0], 32, replace=False))
+        _split_check(gen_cpu, sp, sif_out, mm2_out, st.pc, rows, z[f"{nm}_out_rows"],
+                     z[f"{nm}_pc"])
+
+
+def test_mosi_splits_each_with_its_own_pc(gpu):
+    """configs[0]/[1] at their real call pattern: three MOSI-shaped splits
+    (1284 / 229 / 686 utterances, T = 20, A = 76, Vd = 48; 229 < 300 takes
+    the transposed branch) in one concurrent HIP graph: every split's SIF rows
+    and PC against the oracle, MMB2 on 64 rows per split."""
+    splits = synth.mosi_splits()
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 76, 48, norm=None).to(gpu)
+    steps = [P.FusedStep(synth.to_device(sp, gpu), gen.networks()) for sp in splits]
+    outs = P.StepGraph(steps, concurrent=True).run(check=True)
+    gen_cpu = gen.cpu()
+    for sp, st, (sif_out, mm2_out) in zip(splits, steps, outs):
+        rows = np.sort(np.random.default_rng(8).choice(sp["ids"].shape[0], 64, replace=False))
+        _split_check(gen_cpu, sp, sif_out, mm2_out, st.pc, rows)
+
+
+def test_step_graph_follows_weight_updates(gpu):
+    """A captured step re-merges the generator weights eagerly before the
+    replay when a parameter changed in place (what an optimiser step does):
+    the replayed rows equal a fresh eager step's."""
+    inp = synth.device_workload(1500, 20, 3016, A=76, Vd=48, seed=71, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 76, 48, norm=None).to(gpu)
+    st = P.FusedStep(inp, gen.networks())
+    g = P.StepGraph(st)
+    s0, m0 = [t.clone() for t in g.run(check=True)]
+    with torch.no_grad():
+        gen.embed2out["visual"]["mu"].weight.mul_(1.5)
+    s1, m1 = [t.clone() for t in g.run(check=True)]
+    fresh = P.FusedStep(inp, gen.networks())
+    s2, m2 = fresh.run(check=True)
+    assert torch.equal(s1, s2) and torch.equal(m1, m2) and not torch.equal(m0, m1)
+    assert torch.equal(s0, s1)

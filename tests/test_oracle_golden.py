@@ -165,3 +165,20 @@ def test_sliced_gram_restatement_meets_pc_bar(golden):
         z0 = np.random.RandomState(0).normal(size=(X.shape[1], npc + 10))
         pc = O.pc_from_gram(Gs, z0, npc, False)
         assert np.abs(pc - z["pc"]).max() < 1e-9, case
+
+
+@pytest.mark.parametrize("split", ["valid", "test"])
+def test_real_pom_split_end_to_end(golden, split):
+    """g11: the reference's get_sentence_embeddings on a WHOLE real POM split
+    (pom_valid_ids 100 x 1089 / pom_test_ids 203 x 1357, real weights, its
+    own PC: simplesif.py:296-311), reproduced by the oracle -- PC bit for bit
+    (the transposed randomized-SVD branch, n < 300) and the recorded rows."""
+    z = golden("g11_pom_splits")
+    E = synth.word_table(int(z["V"]), 300, seed=int(z["table_seed"]))
+    assert float(np.asarray(E, np.float64).sum()) == float(z["table_checksum"])
+    ids = z[f"{split}_ids"].astype(np.int64)
+    w = O.seq2weight(ids, np.ones(ids.shape), z["weights"])
+    x = O.get_weighted_average(E, ids, w)
+    assert np.array_equal(O.compute_pc(x, 1), z[f"{split}_pc"])
+    out = O.get_sentence_embeddings(E, z["weights"], ids)
+    assert np.array_equal(out[::int(z["row_step"])], z[f"{split}_out_rows"])
