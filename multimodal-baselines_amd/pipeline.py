@@ -570,6 +570,14 @@ def side_cu_set(n_cu: int, side: int, layout: str = "balanced") -> list[int]:
     return sorted(set(c for c in out if c < n_cu))
 
 
+# Splits below this many utterances take the exact f64 Gram (mmb_gram): at
+# dataset sizes (MOSI 229-1284, POM 100-203 rows) it costs microseconds, and
+# sklearn's transposed branch (n < d: a rank-n Gram) is where the int8 Gram's
+# ~1e-10 relative error reached the PC at 2e-8 (r04d, real POM valid split);
+# the int8 Gram pays from tens of thousands of rows up.
+GRAM_I8_MIN_ROWS = 1 << 15
+
+
 class FusedStep:
     """One pass of the north-star hot path over a batch of utterances resident
     in HBM (bench 'step'): both the SIF text embedding (a1-a5, PC-removed) and
@@ -666,7 +674,8 @@ class FusedStep:
         # the stream kernel) or "f64" (mmb_gram, exact f64 products).
         # MMB_GRAM overrides the default (A/B runs).
         if gram_kind is None:
-            gram_kind = os.environ.get("MMB_GRAM", "i8")
+            gram_kind = os.environ.get("MMB_GRAM", "i8" if self.n_total >= GRAM_I8_MIN_ROWS
+                                       else "f64")
         if gram_kind not in ("i8", "f64"):
             raise ValueError(f"gram_kind must be 'i8' or 'f64', not {gram_kind!r}")
         self.gram_i8 = (gram_kind == "i8" and len(self.bounds) == 1 and self.d % 4 == 0
