@@ -529,8 +529,8 @@ def regressor_config(dev, cpu_epochs=40):
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     L.call("mmb_mlp_train", L.ptr(x), L.ptr(y), L.ptr(perm), sizes[0], epochs, B, 300, H, 1,
-           float(lr), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(sl), L.ptr(ws),
-           L.stream_ptr())
+           float(lr), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(sl), None, None, None, 0,
+           1, 0, None, L.ptr(ws), None, L.stream_ptr())
     b.record()
     torch.cuda.synchronize()
     k_ms = a.elapsed_time(b)
@@ -553,15 +553,16 @@ def regressor_config(dev, cpu_epochs=40):
                         "686, batch 32, SGD lr 0.1, 400 epochs, validation every 10 epochs",
             "steps": steps, "train_s": round(t_prod, 4),
             "ms_per_step": round(t_prod * 1e3 / steps, 5),
-            "kernel": {"name": "mlp_train_kernel (mmb_mlp_train: every SGD step in one launch of "
-                               "one 16-wave workgroup)",
+            "kernel": {"name": "mlp_train_mc_kernel (mmb_mlp_train: every SGD step in one launch "
+                               "of ceil(H / 32) workgroups, one hidden tile each, one exchange of "
+                               "output shares per step)",
                        "ms_400_epochs": round(k_ms, 3), "us_per_step": round(k_ms * 1e3 / steps, 3),
                        "mfma": {"achieved": round(tf, 3), "peak": F32_MFMA_PEAK_TFS,
                                 "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TFS, 5),
                                 "flop_per_step": flop_step,
-                                "bound": "latency: 16,400 dependent SGD steps in sequence on "
-                                         "one workgroup (a 32 x 300 x 100 step is ~0.6 us of "
-                                         "one CU's MFMA time)"}},
+                                "bound": "latency: 16,400 dependent SGD steps in sequence, "
+                                         "each a forward, an exchange between the workgroups "
+                                         "and a backward (~1 us of MFMA per workgroup)"}},
             "cpu_baseline": {"ms_per_step": round(t_cpu * 1e3 / cpu_steps, 4),
                              "train_s_400_epochs_extrapolated": round(t_cpu * epochs / cpu_epochs, 2),
                              "cores": cores, "kind": "port",

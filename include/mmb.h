@@ -328,19 +328,30 @@ int mmb_mlp_eval(const float* latents, const float* labels, const int64_t* perm,
                  const float* w2, const float* b2, float* batch_loss, float* pred_out,
                  hipStream_t stream);
 
-/* SGD training of the regressor over `n_steps` consecutive mini-batches drawn
- * from `perm` (the DataLoader order, batches of `batch` rows, last one
- * ragged, epochs concatenated: steps_per_epoch batches each), with
- * loss = L1(reduction='none').mean() and p -= lr * grad, all in one launch of
- * one workgroup.  Parameters are updated in place; per-step losses go to
- * step_loss; ws is scratch of mmb_mlp_workspace_bytes(d, h) bytes (16-B aligned).
- * replaces: sentiment_model.train_sentiment inner loop
- *   /root/reference/sentiment_model.py:98-110                               */
+/* SGD training of the regressor over n_epochs epochs of mini-batches drawn
+ * from `perm` (the DataLoader order: epochs concatenated, batches of `batch`
+ * rows, the last one ragged), with loss = L1(reduction='none').mean() and
+ * p -= lr * grad, all in ONE launch of ceil(h / 32) workgroups (one 32-wide
+ * hidden tile each, exchanging their output shares once per mini-batch).
+ * Parameters are updated in place; per-step losses go to step_loss
+ * [n_epochs * ceil(n_per_epoch / batch)].  With v_latents non-null the
+ * launch also runs the validation passes: after every epoch e with
+ * (epoch0 + e) % valid_every == 0 the per-batch mean L1 of the validation rows
+ * v_perm[k * n_valid ...] (k = the k-th such epoch of this launch) with the
+ * weights of that moment go to valid_loss[k * ceil(n_valid / batch) + j].
+ * ws: scratch of mmb_mlp_workspace_bytes(d, h) bytes (16-B aligned); flag
+ * (nullable) gets MMB_FLAG_SYNC_TIMEOUT if the workgroups' exchange stalls
+ * (~1 s; the parameters are then invalid).  d % 4 == 0, d <= 512, h <= 512,
+ * n_out <= 16.
+ * replaces: sentiment_model.train_sentiment loop incl. its validation passes
+ *   /root/reference/sentiment_model.py:76-127                               */
 size_t mmb_mlp_workspace_bytes(int d, int h);
 int mmb_mlp_train(const float* latents, const float* labels, const int64_t* perm,
                   int64_t n_per_epoch, int n_epochs, int batch, int d, int h, int o, float lr,
-                  float* w1, float* b1, float* w2, float* b2, float* step_loss, void* ws,
-                  hipStream_t stream);
+                  float* w1, float* b1, float* w2, float* b2, float* step_loss,
+                  const float* v_latents, const float* v_labels, const int64_t* v_perm,
+                  int64_t n_valid, int valid_every, int epoch0, float* valid_loss, void* ws,
+                  int32_t* flag, hipStream_t stream);
 
 /* ---------------------------------------------------------------- §8f row 1
  * Latent-optimisation likelihoods (the objective simplesif.py:49-162,708-806

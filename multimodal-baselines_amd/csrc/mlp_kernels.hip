@@ -2,18 +2,33 @@
 // backward and SGD, for MI355X.
 //
 // The reference trains with one PyTorch step per 32-row mini-batch
-// (sentiment_model.py:98-110): ~16 k tiny launches-worth of work per run.
-// Here a whole run of mini-batches is ONE launch of ONE workgroup (16 waves):
-// the parameters never leave the CU's L1/L2 and no host round trip sits
-// between steps.  W1 is kept as fp32-MFMA accumulator tiles of W1^T
-// (lane&31 = hidden unit, the 16 accumulator registers = 16 input features)
-// in an L2-resident tiled copy.  That layout is at once
-//   * the B operand of the forward  pre = X W1^T   (32x32x2, K = features, taken
-//     in the accumulator's register order — any K order is a valid sum), and
-//   * the C layout of the gradient  dW1^T = X^T dH (32x32x2, K = batch rows),
-// so the SGD update W1 -= lr dW1 is a lane-local FMA on the fragment with no
-// shuffles.  Each tile is owned by one wave for the whole run (its own
-// stores are re-read only by itself).  Bias, output layer and loss are VALU on LDS.
+// (sentiment_model.py:98-110): ~16 k tiny launches-worth of work per run, and
+// a validation pass every 10 epochs (:114-127).  Here a whole run -- every
+// SGD step AND the validation passes -- is ONE launch (mmb_mlp_train).
+//
+// r04: the run is split over P = ceil(h / 32) workgroups, one 32-wide tile of
+// hidden units each (one XCD's worth of CUs at most: P <= 16).  A workgroup
+// keeps its tile of W1^T in registers for the whole run as fp32-MFMA
+// (32x32x2) accumulator tiles -- lane & 31 = hidden unit, the 16 registers =
+// 16 input features of a 32-feature tile, tile t on wave t % 8 -- which is at
+// once the B operand of the forward pre = X W1^T (K = features, taken in the
+// registers' order: any K order is a valid sum) and the C layout of its
+// gradient dW1^T = X^T dH (K = batch rows): the SGD update is a lane-local FMA.
+// Per mini-batch (all workgroups in lockstep):
+//   forward partial products per wave -> fixed-order sum + b1 -> ReLU (LDS);
+//   this tile's share of the output, yp[b][o] = sum_{h in tile} W2[o][h] hid[b][h],
+//   published with write-through stores, then ONE exchange: an arrival
+//   counter (relaxed agent-scope atomics, release / acquire fences around it,
+//   bounded poll), and every workgroup sums the P shares in tile order --
+//   identical outputs, loss and gradient sign everywhere;
+//   g = sign(y - label) / (rows * o); dH = relu' g W2 (own tile); dW1^T for
+//   the own tiles (MFMA) and the SGD steps of W1 / b1 / W2 (own tile) and b2
+//   (every workgroup, identical).
+// The next mini-batch's rows are loaded into registers while this one is
+// computed (their indices two batches ahead) and land in the other LDS
+// buffer at the end of the step.  The single-workgroup kernel this replaces
+// spent ~8.5 us of its 19.3 us step in the MFMAs of all hidden tiles on one
+// CU.
 #include <algorithm>
 #include <cstdlib>
 
@@ -27,306 +42,356 @@ constexpr int kMlpNT = 1024;
 constexpr int kMaxWaves = kMlpNT / kWave;
 constexpr int kBatchMax = 32;  // one MFMA M-tile of batch rows
 
-struct MlpArgs {
+__device__ __forceinline__ int c_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+constexpr int kTrWaves = 8;
+constexpr int kTrNT = kTrWaves * kWave;  // 512
+constexpr int kTrMaxFT = 2;              // 32-feature tiles per wave (d <= 512)
+constexpr int kTrMaxP = 16;              // hidden tiles = workgroups (h <= 512)
+constexpr int kTrMaxO = 16;              // outputs (n_out <= 16)
+
+struct TrainArgs {
   const float* lat;
   const float* lab;
   const int64_t* perm;
-  int64_t n_per_epoch;
-  int n_epochs, B, D, H, O;
+  int64_t n;
+  int n_epochs;
+  const float* vlat;  // nullable: no validation
+  const float* vlab;
+  const int64_t* vperm;
+  int64_t nv;
+  int valid_every, epoch0;
+  float* valid_loss;
+  int B, D, H, O, nTd, P, spe, nbv;
   float lr;
   float* w1;
   float* b1;
   float* w2;
   float* b2;
   float* step_loss;
-  float* w1t;  // workspace: [nTh*nTd][64 lanes][16] tiled W1^T
-  // tiling
-  int nTh, nTd, G, DP, HP;
+  float* xbuf;    // [2][P][32 * O] output shares
+  unsigned* ctl;  // arrival counter, abort word (zeroed by the launcher)
+  int32_t* flag;
 };
 
-__device__ __forceinline__ int c_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+// Position in the run's item sequence: epoch e, item pos (< spe: training
+// mini-batch, else validation batch pos - spe), vk = validations before e.
+struct TrItem {
+  int e, pos, vk;
+};
 
-__device__ __forceinline__ f32x16 load_frag(const float* p) {
-  f32x16 v;
-  const float4* q = reinterpret_cast<const float4*>(p);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float4 x = q[i];
-    v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+__device__ __forceinline__ bool tr_valid_epoch(const TrainArgs& a, int e) {
+  return a.vlat != nullptr && (a.epoch0 + e) % a.valid_every == 0;
+}
+__device__ __forceinline__ void tr_advance(const TrainArgs& a, TrItem& it) {
+  const bool v = tr_valid_epoch(a, it.e);
+  if (++it.pos >= a.spe + (v ? a.nbv : 0)) {
+    it.pos = 0;
+    it.vk += v ? 1 : 0;
+    ++it.e;
   }
-  return v;
+}
+// rows of an item: index base into perm / vperm, row count
+__device__ __forceinline__ void tr_rows(const TrainArgs& a, const TrItem& it, bool& train,
+                                        int64_t& base, int& bc) {
+  train = it.pos < a.spe;
+  if (train) {
+    base = static_cast<int64_t>(it.e) * a.n + static_cast<int64_t>(it.pos) * a.B;
+    bc = static_cast<int>(min<int64_t>(a.B, a.n - static_cast<int64_t>(it.pos) * a.B));
+  } else {
+    const int j = it.pos - a.spe;
+    base = static_cast<int64_t>(it.vk) * a.nv + static_cast<int64_t>(j) * a.B;
+    bc = static_cast<int>(min<int64_t>(a.B, a.nv - static_cast<int64_t>(j) * a.B));
+  }
 }
 
-__device__ __forceinline__ void store_frag(float* p, const f32x16& v) {
-  float4* q = reinterpret_cast<float4*>(p);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) q[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-}
-
-// NT threads; REGT > 0: each wave's W1^T tiles (<= REGT) held in registers for
-// the whole run (8 waves x 256 VGPRs), so neither the forward nor the SGD
-// update touches L2 for W1; REGT = 0: tiles re-read from the L2-resident
-// tiled copy every step (16 waves x 128 VGPRs, where the tiles spilled).
-template <int NT, int REGT>
-__global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
-  constexpr int kNW = NT / kWave;
+// NTD: 32-feature tiles (d <= 32 NTD), a compile-time count so the row
+// prefetch and the tile loops carry no runtime bounds
+template <int NTD>
+__global__ __launch_bounds__(kTrNT) void mlp_train_mc_kernel(TrainArgs a) {
+  constexpr int DP = 32 * NTD, SX = DP + 1;
+  constexpr int U = DP / 4;                                    // float4 units of a padded row
+  constexpr int kPf = (kBatchMax * U + kTrNT - 1) / kTrNT;     // prefetched float4 per thread
+  constexpr int kFT = (NTD + kTrWaves - 1) / kTrWaves;         // feature tiles per wave
+  constexpr int nwu = NTD < kTrWaves ? NTD : kTrWaves;         // waves holding feature tiles
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int DP = a.DP, HP = a.HP, O = a.O;
-  int64_t* s_perm = reinterpret_cast<int64_t*>(smem);  // [2][32] row indices (prefetch)
-  float* sx = smem + 4 * kBatchMax;                   // [32][DP+1]
-  float* spart = sx + kBatchMax * (DP + 1);           // [G][32][HP]  (aliased by sdh)
-  float* shid = spart + a.G * kBatchMax * HP;         // [32][HP]
-  float* sW2 = shid + kBatchMax * HP;                 // [O][HP]
-  float* sb1 = sW2 + O * HP;                          // [HP]
-  float* sb2 = sb1 + HP;                              // [O]
-  float* sg = sb2 + O;                                // [32][O]
-  float* sy = sg + kBatchMax * O;                     // [32][O]
-  float* s_red = sy + kBatchMax * O;                  // [kNW]
-  float* sdh = spart;                                 // [32][HP]
-  const int SX = DP + 1;
+  const int O = a.O;
+  int64_t* s_perm = reinterpret_cast<int64_t*>(smem);  // [3][32] row indices
+  float* sx = smem + 6 * kBatchMax;                     // [2][32][SX]
+  float* sy = sx + 2 * kBatchMax * SX;                  // [2][32][O]
+  float* spart = sy + 2 * kBatchMax * O;                // [8][32][32] (aliased by sdh)
+  float* shid = spart + kTrWaves * kBatchMax * 32;      // [32][32]
+  float* sg = shid + kBatchMax * 32;                    // [32][O]
+  float* sW2 = sg + kBatchMax * O;                      // [O][32]
+  float* sb1 = sW2 + O * 32;                            // [32]
+  float* sb2 = sb1 + 32;                                // [O]
+  float* s_red = sb2 + O;                               // [8]
+  float* sdh = spart;                                   // [32][32]
+  __shared__ int s_abort;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool mw = wave < a.nTh * a.G;
-  const int Th = mw ? wave % a.nTh : 0, grp = mw ? wave / a.nTh : 0;
-  const int tpg = (a.nTd + a.G - 1) / a.G;
-  const int td0 = grp * tpg;
-  const int ntiles = mw ? max(0, min(tpg, a.nTd - td0)) : 0;
-  const int hcol = 32 * Th + (lane & 31);
-  float* wt = a.w1t + (static_cast<int64_t>(Th) * a.nTd * kWave + lane) * 16;  // + td*64*16
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.x;       // hidden tile
+  const int h0 = 32 * g;
+  const int hl = lane & 31;       // this lane's hidden unit in MFMA layouts
 
-  // W1 -> tiled W1^T workspace (zero outside [H) x [D))
-  for (int64_t e = tid; e < static_cast<int64_t>(a.nTh) * a.nTd * kWave * 16; e += NT) {
-    const int r = static_cast<int>(e & 15), l = static_cast<int>((e >> 4) & 63);
-    const int64_t tile = e >> 10;
-    const int th = static_cast<int>(tile / a.nTd), td = static_cast<int>(tile % a.nTd);
-    const int h = 32 * th + (l & 31), d = 32 * td + c_row(r, l);
-    a.w1t[e] = (h < a.H && d < a.D) ? a.w1[static_cast<int64_t>(h) * a.D + d] : 0.f;
+  // parameters: this tile's W1^T (registers), W2 columns, b1, b2
+  f32x16 wreg[kFT];
+#pragma unroll
+  for (int j = 0; j < kFT; ++j) {
+    const int td = wave + kTrWaves * j;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int h = h0 + hl, d = 32 * td + c_row(r, lane);
+      wreg[j][r] = (td < NTD && h < a.H && d < a.D) ? a.w1[static_cast<int64_t>(h) * a.D + d] : 0.f;
+    }
   }
-  for (int e = tid; e < O * HP; e += NT) {
-    const int o = e / HP, h = e % HP;
+  for (int e = tid; e < O * 32; e += kTrNT) {
+    const int o = e >> 5, h = h0 + (e & 31);
     sW2[e] = h < a.H ? a.w2[o * a.H + h] : 0.f;
   }
-  for (int h = tid; h < HP; h += NT) sb1[h] = h < a.H ? a.b1[h] : 0.f;
-  for (int o = tid; o < O; o += NT) sb2[o] = a.b2[o];
-  __threadfence_block();
-  __syncthreads();
-  f32x16 wreg[REGT > 0 ? REGT : 1];
-  if constexpr (REGT > 0) {
-#pragma unroll
-    for (int t = 0; t < REGT; ++t)
-      if (t < ntiles) wreg[t] = load_frag(wt + static_cast<int64_t>(td0 + t) * kWave * 16);
-  }
+  if (tid < 32) sb1[tid] = h0 + tid < a.H ? a.b1[h0 + tid] : 0.f;
+  if (tid < O) sb2[tid] = a.b2[tid];
+  if (tid == 0) s_abort = 0;
 
-  const int64_t spe = (a.n_per_epoch + a.B - 1) / a.B;
-  const int64_t nsteps = spe * a.n_epochs;
-  auto batch_of = [&](int64_t st, int64_t& base, int& bc) {
-    const int64_t ep = st / spe, bi = st % spe;
-    base = ep * a.n_per_epoch + bi * a.B;
-    bc = static_cast<int>(min<int64_t>(a.B, a.n_per_epoch - bi * a.B));
+  // rows of an item -> registers (one float4 unit per (row, unit) item)
+  float4 pf[kPf];
+  float pfy = 0.f;
+  auto fetch_rows = [&](const TrItem& it, const int64_t* pidx) {
+    bool train;
+    int64_t base;
+    int bc;
+    tr_rows(a, it, train, base, bc);
+    const float* src = train ? a.lat : a.vlat;
+    const float* lsrc = train ? a.lab : a.vlab;
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) {
+      const int e = tid + kTrNT * k;
+      const int b = e / U, u = e - b * U;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (it.e < a.n_epochs && b < bc && 4 * u < a.D)
+        v = *reinterpret_cast<const float4*>(src + pidx[b] * a.D + 4 * u);
+      pf[k] = v;
+    }
+    pfy = 0.f;
+    if (it.e < a.n_epochs && tid < kBatchMax * O) {
+      const int b = tid / O, o = tid - (tid / O) * O;
+      if (b < bc) pfy = lsrc[pidx[b] * O + o];
+    }
   };
-  // The batch gather was two dependent round trips (permutation index, then
-  // the row) per step.  Now wave 0 reads step s+1's indices into LDS during
-  // step s, so a step issues its row loads at once (16-byte loads when
-  // D % 4 == 0).
-  auto fetch_perm = [&](int64_t st) {
-    if (wave == 0 && lane < kBatchMax && st < nsteps) {
+  auto store_rows = [&](int buf) {
+    float* dst = sx + buf * kBatchMax * SX;
+#pragma unroll
+    for (int k = 0; k < kPf; ++k) {
+      const int e = tid + kTrNT * k;
+      const int b = e / U, u = e - b * U;
+      if (b < kBatchMax) {
+        float* q = dst + b * SX + 4 * u;
+        q[0] = pf[k].x; q[1] = pf[k].y; q[2] = pf[k].z; q[3] = pf[k].w;
+      }
+    }
+    if (tid < kBatchMax * O) sy[buf * kBatchMax * O + tid] = pfy;
+  };
+  auto fetch_perm = [&](const TrItem& it, int slot) {
+    if (wave == 0 && lane < kBatchMax && it.e < a.n_epochs) {
+      bool train;
       int64_t base;
       int bc;
-      batch_of(st, base, bc);
-      s_perm[(st & 1) * kBatchMax + lane] = lane < bc ? a.perm[base + lane] : 0;
+      tr_rows(a, it, train, base, bc);
+      s_perm[slot * kBatchMax + lane] = lane < bc ? (train ? a.perm : a.vperm)[base + lane] : 0;
     }
   };
-  const bool v4 = (a.D & 3) == 0 && (reinterpret_cast<uintptr_t>(a.lat) & 15) == 0;
-  fetch_perm(0);
+
+  // pipeline: item k's rows in sx[k & 1]; item k + 1's rows in registers
+  // during k; item k + 2's indices land in s_perm during k
+  TrItem cur{0, 0, 0}, nx1 = cur, nx2;
+  tr_advance(a, nx1);
+  nx2 = nx1;
+  tr_advance(a, nx2);
+  fetch_perm(cur, 0);
+  fetch_perm(nx1, 1);
   __syncthreads();
-  for (int64_t step = 0; step < nsteps; ++step) {
+  fetch_rows(cur, s_perm);
+  store_rows(0);
+  __syncthreads();
+  unsigned xc = 0;  // exchanges so far
+  for (int k = 0; cur.e < a.n_epochs; ++k) {
+    bool train;
     int64_t base;
     int Bc;
-    batch_of(step, base, Bc);
-    const int64_t* pp = s_perm + (step & 1) * kBatchMax;
-    // 1. gather the batch rows (DataLoader order) into LDS
-    if (v4) {
-      const int U = DP >> 2;  // float4 units of a padded row
-      for (int e = tid; e < kBatchMax * U; e += NT) {
-        const int b = e / U, u = e - b * U;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (b < Bc && 4 * u < a.D) v = *reinterpret_cast<const float4*>(a.lat + pp[b] * a.D + 4 * u);
-        float* dst = sx + b * SX + 4 * u;
-        dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-      }
-    } else {
-      for (int e = tid; e < kBatchMax * DP; e += NT) {
-        const int b = e / DP, d = e % DP;
-        float v = 0.f;
-        if (b < Bc && d < a.D) v = a.lat[pp[b] * a.D + d];
-        sx[b * SX + d] = v;
-      }
-    }
-    for (int e = tid; e < kBatchMax * O; e += NT) {
-      const int b = e / O, o = e % O;
-      sy[e] = (b < Bc) ? a.lab[pp[b] * O + o] : 0.f;
-    }
-    fetch_perm(step + 1);  // lands during this step
-    __syncthreads();
-    // 2. forward partials: pre[b][h] over this wave's feature tiles (MFMA)
-    if (mw) {
+    tr_rows(a, cur, train, base, Bc);
+    const float* xs = sx + (k & 1) * kBatchMax * SX;
+    const float* ys = sy + (k & 1) * kBatchMax * O;
+    fetch_rows(nx1, s_perm + ((k + 1) % 3) * kBatchMax);  // in flight through this item
+    fetch_perm(nx2, (k + 2) % 3);
+
+    // 1. forward partial products of this wave's feature tiles
+    if (wave < nwu) {
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const float* xb = sx + (lane & 31) * SX + 4 * (lane >> 5);
-      auto fwd_tile = [&](int t, const f32x16& w) {
-        const int td = td0 + t;
+      const float* xb = xs + (lane & 31) * SX + 4 * (lane >> 5);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float xa = xb[32 * td + (r & 3) + 8 * (r >> 2)];
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, w[r], acc, 0, 0, 0);
+      for (int j = 0; j < kFT; ++j) {
+        const int td = wave + kTrWaves * j;
+        if (td < NTD) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xb[32 * td + (r & 3) + 8 * (r >> 2)], wreg[j][r],
+                                                       acc, 0, 0, 0);
         }
-      };
-      if constexpr (REGT > 0) {
-#pragma unroll
-        for (int t = 0; t < REGT; ++t)
-          if (t < ntiles) fwd_tile(t, wreg[t]);
-      } else {
-        for (int t = 0; t < ntiles; ++t)
-          fwd_tile(t, load_frag(wt + static_cast<int64_t>(td0 + t) * kWave * 16));
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) spart[(grp * kBatchMax + c_row(r, lane)) * HP + hcol] = acc[r];
+      for (int r = 0; r < 16; ++r) spart[(wave * kBatchMax + c_row(r, lane)) * 32 + hl] = acc[r];
     }
     __syncthreads();
-    // 3. hidden = relu(sum_g partial + b1)  (fixed group order)
-    for (int e = tid; e < kBatchMax * HP; e += NT) {
-      const int b = e / HP, h = e % HP;
+    // 2. hid = relu(b1 + sum of the partials in wave order)
+    for (int e = tid; e < kBatchMax * 32; e += kTrNT) {
+      const int h = e & 31;
       float p = sb1[h];
-      for (int g = 0; g < a.G; ++g) p += spart[(g * kBatchMax + b) * HP + h];
-      shid[e] = (h < a.H && p > 0.f) ? p : 0.f;
+      for (int w = 0; w < nwu; ++w) p += spart[w * kBatchMax * 32 + e];
+      shid[e] = (h0 + h < a.H && p > 0.f) ? p : 0.f;
     }
     __syncthreads();
-    // 4. output layer, L1 loss and its gradient (mean over Bc*O elements);
-    //    O = 1: a half-wave per batch row (16 waves x 2 = 32 rows), lane
-    //    h-stride partial dots and a 32-lane shuffle sum, instead of a
-    //    100-long serial chain per row
-    float lsum = 0.f;
-    if (O == 1) {
-#pragma unroll
-      for (int k = 0; k < kBatchMax / (2 * kNW); ++k) {
-        const int b = 2 * (wave + kNW * k) + (lane >> 5), l32 = lane & 31;
-        float part = 0.f;
-        for (int h = l32; h < a.H; h += 32) part = fmaf(sW2[h], shid[b * HP + h], part);
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) part += __shfl_xor(part, o, kWave);
-        const float diff = (sb2[0] + part) - sy[b];
-        const bool valid = b < Bc;
-        if (l32 == 0) {
-          sg[b] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc) : 0.f;
-          if (valid) lsum += fabsf(diff);
+    // 3. this tile's share of the outputs -> exchange slot (write-through),
+    //    drained by every storing wave before the arrival
+    float* slot = a.xbuf + static_cast<int64_t>(xc & 1) * a.P * kBatchMax * O;
+    if (tid < kBatchMax * O) {
+      const int b = tid / O, o = tid - b * O;
+      float yp = 0.f;
+#pragma unroll 8
+      for (int h = 0; h < 32; ++h) yp = fmaf(sW2[o * 32 + h], shid[b * 32 + h], yp);
+      __hip_atomic_store(reinterpret_cast<unsigned*>(slot + g * kBatchMax * O + tid),
+                         __float_as_uint(yp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = static_cast<unsigned>(a.P) * (xc + 1);
+      bool ok = false;
+      for (int it = 0; it < (1 << 21); ++it) {
+        if (__hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+          ok = true;
+          break;
         }
+        if (__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        __builtin_amdgcn_s_sleep(1);
       }
-    } else {
-      for (int e = tid; e < kBatchMax * O; e += NT) {
-        const int b = e / O, o = e % O;
-        float out = sb2[o];
-        for (int h = 0; h < a.H; ++h) out = fmaf(sW2[o * HP + h], shid[b * HP + h], out);
-        const float diff = out - sy[e];
-        const bool valid = b < Bc;
-        sg[e] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc * O) : 0.f;
-        if (valid) lsum += fabsf(diff);
+      if (!ok) {  // ~1 s without the other workgroups (or one of them gave up)
+        __hip_atomic_store(a.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.flag) atomicOr(a.flag, MMB_FLAG_SYNC_TIMEOUT);
+        s_abort = 1;
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (s_abort) return;
+    ++xc;
+    // 4. outputs = b2 + the P shares in tile order (identical everywhere),
+    //    the L1 loss and its gradient sign(y - label) / (rows * o)
+    float lsum = 0.f;
+    if (tid < kBatchMax * O) {
+      const int b = tid / O, o = tid - b * O;
+      float sh[kTrMaxP];
+#pragma unroll
+      for (int q = 0; q < kTrMaxP; ++q)
+        sh[q] = q < a.P ? __uint_as_float(__hip_atomic_load(
+                              reinterpret_cast<const unsigned*>(slot + q * kBatchMax * O + tid),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        : 0.f;
+      float y = sb2[o];
+#pragma unroll
+      for (int q = 0; q < kTrMaxP; ++q)
+        if (q < a.P) y += sh[q];
+      const float diff = y - ys[tid];
+      const bool valid = b < Bc;
+      sg[tid] = valid ? ((diff > 0.f) ? 1.f : (diff < 0.f ? -1.f : 0.f)) / static_cast<float>(Bc * O) : 0.f;
+      if (valid) lsum = fabsf(diff);
     }
     lsum = wave_sum(lsum);
     if (lane == 0) s_red[wave] = lsum;
     __syncthreads();
-    // 5. dH = relu'(.) * g W2 ; then W2/b2 gradients (old W2 already consumed)
-    for (int e = tid; e < kBatchMax * HP; e += NT) {
-      const int b = e / HP, h = e % HP;
-      float s = 0.f;
-      if (shid[e] > 0.f)
-        for (int o = 0; o < O; ++o) s = fmaf(sg[b * O + o], sW2[o * HP + h], s);
-      sdh[e] = s;
+    if (g == 0 && tid == 0) {
+      float l = 0.f;
+      for (int w = 0; w < kTrWaves; ++w) l += s_red[w];
+      l /= static_cast<float>(Bc * O);
+      if (train) a.step_loss[static_cast<int64_t>(cur.e) * a.spe + cur.pos] = l;
+      else a.valid_loss[static_cast<int64_t>(cur.vk) * a.nbv + (cur.pos - a.spe)] = l;
     }
-    __syncthreads();
-    // 6. dW1^T = X^T dH (MFMA, K = batch) and the SGD step on the owned tiles;
-    //    VALU updates of b1/W2/b2
-    if (mw) {
-      auto grad_tile = [&](int t) {
-        const int td = td0 + t;
-        f32x16 acc;
+    if (train) {
+      // 5. dH = relu'(.) g W2 (old W2)
+      for (int e = tid; e < kBatchMax * 32; e += kTrNT) {
+        const int b = e >> 5, h = e & 31;
+        float s = 0.f;
+        if (shid[e] > 0.f)
+          for (int o = 0; o < O; ++o) s = fmaf(sg[b * O + o], sW2[o * 32 + h], s);
+        sdh[e] = s;
+      }
+      __syncthreads();
+      // 6. dW1^T = X^T dH on the own feature tiles (K = batch rows) and their
+      //    SGD step; W2 / b1 (own tile) and b2 (everywhere) on VALU
+      if (wave < nwu) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        for (int j = 0; j < kFT; ++j) {
+          const int td = wave + kTrWaves * j;
+          if (td < NTD) {
+            f32x16 acc;
 #pragma unroll
-        for (int s = 0; s < kBatchMax / 2; ++s) {
-          const int b = 2 * s + (lane >> 5);
-          const float xa = sx[b * SX + 32 * td + (lane & 31)];
-          const float db = sdh[b * HP + hcol];
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xa, db, acc, 0, 0, 0);
-        }
-        return acc;
-      };
-      if constexpr (REGT > 0) {
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-        for (int t = 0; t < REGT; ++t) {
-          if (t < ntiles) {
-            const f32x16 g = grad_tile(t);
+            for (int s2 = 0; s2 < kBatchMax / 2; ++s2) {
+              const int b = 2 * s2 + (lane >> 5);
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[b * SX + 32 * td + (lane & 31)],
+                                                         sdh[b * 32 + hl], acc, 0, 0, 0);
+            }
 #pragma unroll
-            for (int r = 0; r < 16; ++r) wreg[t][r] = fmaf(-a.lr, g[r], wreg[t][r]);
+            for (int r = 0; r < 16; ++r) wreg[j][r] = fmaf(-a.lr, acc[r], wreg[j][r]);
           }
         }
-      } else {
-        for (int t = 0; t < ntiles; ++t) {
-          const f32x16 g = grad_tile(t);
-          float* p = wt + static_cast<int64_t>(td0 + t) * kWave * 16;
-          f32x16 w = load_frag(p);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) w[r] = fmaf(-a.lr, g[r], w[r]);
-          store_frag(p, w);
-        }
       }
-    }
-    for (int e = tid; e < O * HP; e += NT) {
-      const int o = e / HP, h = e % HP;
-      if (h < a.H) {
+      for (int e = tid; e < O * 32; e += kTrNT) {
+        const int o = e >> 5, h = e & 31;
         float gsum = 0.f;
-        for (int b = 0; b < kBatchMax; ++b) gsum = fmaf(sg[b * O + o], shid[b * HP + h], gsum);
-        sW2[e] = fmaf(-a.lr, gsum, sW2[e]);
+        for (int b = 0; b < kBatchMax; ++b) gsum = fmaf(sg[b * O + o], shid[b * 32 + h], gsum);
+        if (h0 + h < a.H) sW2[e] = fmaf(-a.lr, gsum, sW2[e]);
+      }
+      if (tid < 32) {
+        float gsum = 0.f;
+        for (int b = 0; b < kBatchMax; ++b) gsum += sdh[b * 32 + tid];
+        if (h0 + tid < a.H) sb1[tid] = fmaf(-a.lr, gsum, sb1[tid]);
+      }
+      if (tid >= 64 && tid < 64 + O) {
+        const int o = tid - 64;
+        float gsum = 0.f;
+        for (int b = 0; b < kBatchMax; ++b) gsum += sg[b * O + o];
+        sb2[o] = fmaf(-a.lr, gsum, sb2[o]);
       }
     }
-    for (int h = tid; h < a.H; h += NT) {
-      float gsum = 0.f;
-      for (int b = 0; b < kBatchMax; ++b) gsum += sdh[b * HP + h];
-      sb1[h] = fmaf(-a.lr, gsum, sb1[h]);
-    }
-    for (int o = tid; o < O; o += NT) {
-      float gsum = 0.f;
-      for (int b = 0; b < kBatchMax; ++b) gsum += sg[b * O + o];
-      sb2[o] = fmaf(-a.lr, gsum, sb2[o]);
-    }
-    if (tid == 0) {
-      float l = 0.f;
-      for (int w = 0; w < kNW; ++w) l += s_red[w];
-      a.step_loss[step] = l / static_cast<float>(Bc * O);
-    }
+    // the next item's rows (loaded during this one) into the other buffer
+    store_rows((k + 1) & 1);
     __syncthreads();
+    cur = nx1;
+    nx1 = nx2;
+    tr_advance(a, nx2);
   }
 
-  // write the parameters back
-  if constexpr (REGT > 0) {
+  // write this tile's parameters back (b2 by workgroup 0)
 #pragma unroll
-    for (int t = 0; t < REGT; ++t)
-      if (t < ntiles) store_frag(wt + static_cast<int64_t>(td0 + t) * kWave * 16, wreg[t]);
+  for (int j = 0; j < kFT; ++j) {
+    const int td = wave + kTrWaves * j;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int h = h0 + hl, d = 32 * td + c_row(r, lane);
+      if (td < NTD && h < a.H && d < a.D) a.w1[static_cast<int64_t>(h) * a.D + d] = wreg[j][r];
+    }
   }
-  __threadfence_block();
-  __syncthreads();
-  for (int64_t e = tid; e < static_cast<int64_t>(a.H) * a.D; e += NT) {
-    const int h = static_cast<int>(e / a.D), d = static_cast<int>(e % a.D);
-    const int th = h >> 5, td = d >> 5, dr = d & 31;
-    // invert c_row: dr = (r&3) + 8*(r>>2) + 4*(lane>>5)
-    const int hl = (dr >> 2) & 1, r = (dr & 3) + 4 * (dr >> 3);
-    const int l = (h & 31) + 32 * hl;
-    a.w1[e] = a.w1t[((static_cast<int64_t>(th) * a.nTd + td) * kWave + l) * 16 + r];
+  for (int e = tid; e < O * 32; e += kTrNT) {
+    const int o = e >> 5, h = h0 + (e & 31);
+    if (h < a.H) a.w2[o * a.H + h] = sW2[e];
   }
-  for (int e = tid; e < O * a.H; e += NT) a.w2[e] = sW2[(e / a.H) * HP + e % a.H];
-  for (int h = tid; h < a.H; h += NT) a.b1[h] = sb1[h];
-  for (int o = tid; o < O; o += NT) a.b2[o] = sb2[o];
+  if (tid < 32 && h0 + tid < a.H) a.b1[h0 + tid] = sb1[tid];
+  if (g == 0 && tid < O) a.b2[tid] = sb2[tid];
 }
 
 // Forward (+ optional L1 per batch) — one workgroup per batch of rows.
@@ -603,29 +668,17 @@ __global__ __launch_bounds__(256) void mlp_bwd_params_kernel(const float* __rest
   }
 }
 
-template <int NT, int REGT>
-static int launch_train(const MlpArgs& a, size_t lds, hipStream_t stream) {
+template <int NTD>
+static int launch_train_mc(const TrainArgs& a, size_t lds, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<NT, REGT>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_mc_kernel<NTD>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  mlp_train_kernel<NT, REGT><<<1, NT, lds, stream>>>(a);
+  mlp_train_mc_kernel<NTD><<<a.P, kTrNT, lds, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
-}
-
-// W1 tiles in registers (8 waves, <= 5 tiles each) where they fit, else the
-// L2-tile kernel (the tools build's MMB_MLP_REG=0 forces the latter)
-constexpr int kRegWaves = 8, kRegTiles = 5;
-static int mlp_reg() {
-#ifdef MMB_DIAG
-  const char* e = getenv("MMB_MLP_REG");
-  return e ? atoi(e) : 1;
-#else
-  return 1;
-#endif
 }
 
 }  // namespace mmb
@@ -657,42 +710,56 @@ extern "C" int mmb_mlp_eval(const float* latents, const float* labels, const int
 }
 
 extern "C" size_t mmb_mlp_workspace_bytes(int d, int h) {
-  return static_cast<size_t>(ceil_div(h, 32)) * ceil_div(d, 32) * kWave * 16 * sizeof(float);
+  (void)d;
+  // arrival counter + abort word, then the double-buffered output shares
+  return 16 + sizeof(float) * 2 * static_cast<size_t>(ceil_div(h, 32)) * kBatchMax * kTrMaxO;
 }
 
 extern "C" int mmb_mlp_train(const float* latents, const float* labels, const int64_t* perm,
                              int64_t n_per_epoch, int n_epochs, int batch, int d, int h, int o,
                              float lr, float* w1, float* b1, float* w2, float* b2,
-                             float* step_loss, void* ws, hipStream_t stream) {
+                             float* step_loss, const float* v_latents, const float* v_labels,
+                             const int64_t* v_perm, int64_t n_valid, int valid_every, int epoch0,
+                             float* valid_loss, void* ws, int32_t* flag, hipStream_t stream) {
   MMB_REQUIRE(latents && labels && perm && w1 && b1 && w2 && b2 && step_loss && ws);
   MMB_REQUIRE(n_per_epoch > 0 && n_epochs >= 0 && batch >= 1 && batch <= kBatchMax);
-  MMB_REQUIRE(d > 0 && h > 0 && o >= 1 && o <= 32);
-  MMB_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0);
-  if (n_epochs == 0) return MMB_OK;
-  MlpArgs a{};
-  a.lat = latents; a.lab = labels; a.perm = perm; a.n_per_epoch = n_per_epoch;
-  a.n_epochs = n_epochs; a.B = batch; a.D = d; a.H = h; a.O = o; a.lr = lr;
-  a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.step_loss = step_loss;
-  a.w1t = static_cast<float*>(ws);
-  a.nTh = static_cast<int>(ceil_div(h, 32));
-  a.nTd = static_cast<int>(ceil_div(d, 32));
-  MMB_REQUIRE(a.nTh <= kMaxWaves);
-  bool reg = false;
-  if (mlp_reg() && a.nTh <= kRegWaves) {
-    const int g = std::min(kRegWaves / a.nTh, a.nTd);
-    reg = ceil_div(a.nTd, g) <= kRegTiles;
+  MMB_REQUIRE(d > 0 && d <= 32 * kTrWaves * kTrMaxFT && h > 0 && h <= 32 * kTrMaxP);
+  MMB_REQUIRE(o >= 1 && o <= kTrMaxO && epoch0 >= 0);
+  MMB_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0 && (reinterpret_cast<uintptr_t>(latents) & 15) == 0);
+  MMB_REQUIRE(d % 4 == 0);
+  if (v_latents) {
+    MMB_REQUIRE(v_labels && v_perm && valid_loss && n_valid > 0 && valid_every > 0);
+    MMB_REQUIRE((reinterpret_cast<uintptr_t>(v_latents) & 15) == 0);
   }
-  a.G = (reg ? kRegWaves : kMaxWaves) / a.nTh;
-  if (a.G > a.nTd) a.G = a.nTd;
-  a.DP = a.nTd * 32;
-  a.HP = a.nTh * 32;
-  const size_t lds = sizeof(float) * (4 * kBatchMax + static_cast<size_t>(kBatchMax) * (a.DP + 1) +
-                                      static_cast<size_t>(a.G) * kBatchMax * a.HP +
-                                      static_cast<size_t>(kBatchMax) * a.HP + o * a.HP + a.HP +
-                                      o + 2 * kBatchMax * o + kMaxWaves);
+  if (n_epochs == 0) return MMB_OK;
+  TrainArgs a{};
+  a.lat = latents; a.lab = labels; a.perm = perm; a.n = n_per_epoch; a.n_epochs = n_epochs;
+  a.vlat = v_latents; a.vlab = v_labels; a.vperm = v_perm; a.nv = v_latents ? n_valid : 0;
+  a.valid_every = v_latents ? valid_every : 1; a.epoch0 = epoch0; a.valid_loss = valid_loss;
+  a.B = batch; a.D = d; a.H = h; a.O = o; a.lr = lr;
+  a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.step_loss = step_loss; a.flag = flag;
+  a.nTd = static_cast<int>(ceil_div(d, 32));
+  a.P = static_cast<int>(ceil_div(h, 32));
+  a.spe = static_cast<int>(ceil_div(n_per_epoch, batch));
+  a.nbv = v_latents ? static_cast<int>(ceil_div(n_valid, batch)) : 0;
+  a.ctl = static_cast<unsigned*>(ws);
+  a.xbuf = reinterpret_cast<float*>(static_cast<char*>(ws) + 16);
+  const size_t lds = sizeof(float) * (6 * kBatchMax + 2 * static_cast<size_t>(kBatchMax) * (32 * a.nTd + 1) +
+                                      2 * kBatchMax * o + kTrWaves * kBatchMax * 32 +
+                                      kBatchMax * 32 + kBatchMax * o + o * 32 + 32 + o + kTrWaves);
   MMB_REQUIRE(lds <= 160 * 1024);
-  return reg ? launch_train<kRegWaves * kWave, kRegTiles>(a, lds, stream)
-             : launch_train<kMlpNT, 0>(a, lds, stream);
+  const hipError_t e = hipMemsetAsync(ws, 0, 16, stream);
+  if (e != hipSuccess) return static_cast<int>(e);
+  switch (a.nTd) {
+#define MMB_TRAIN_NTD(n) \
+    case n: return launch_train_mc<n>(a, lds, stream);
+    MMB_TRAIN_NTD(1) MMB_TRAIN_NTD(2) MMB_TRAIN_NTD(3) MMB_TRAIN_NTD(4) MMB_TRAIN_NTD(5)
+    MMB_TRAIN_NTD(6) MMB_TRAIN_NTD(7) MMB_TRAIN_NTD(8) MMB_TRAIN_NTD(9) MMB_TRAIN_NTD(10)
+    MMB_TRAIN_NTD(11) MMB_TRAIN_NTD(12) MMB_TRAIN_NTD(13) MMB_TRAIN_NTD(14) MMB_TRAIN_NTD(15)
+    MMB_TRAIN_NTD(16)
+#undef MMB_TRAIN_NTD
+    default: return MMB_EINVAL;
+  }
 }
 
 extern "C" int mmb_mlp_forward_train(const float* x, int64_t b, int d, int h, int o,

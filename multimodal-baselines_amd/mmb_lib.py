@@ -79,7 +79,8 @@ SIGNATURES = {
     "mmb_mlp_forward_train": (_I, [_P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_backward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_workspace_bytes": (_S, [_I, _I]),
-    "mmb_mlp_train": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P]),
+    "mmb_mlp_train": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P,
+                           _P, _P, _P, _L, _I, _I, _P, _P, _P, _P]),
     "mmb_word_pad": (_I, [_I]),
     "mmb_word_normalize": (_I, [_P, _L, _I, _P, _P]),
     "mmb_word_workspace_bytes": (_S, [_L, _I, _L]),

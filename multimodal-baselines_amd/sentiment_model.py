@@ -155,6 +155,30 @@ def _epoch_batches(loader):
     return batches
 
 
+def _epoch_perm(loader):
+    """The sample order of one pass over `loader`, consuming the global torch
+    RNG exactly as `for j, senti in loader` does -- for the reference's
+    loaders (shuffle=True, default RandomSampler, no generator): the
+    iterator's base seed, then the sampler's seed and its randperm
+    (dataloader.py _BaseDataLoaderIter.__init__, sampler.py
+    RandomSampler.__iter__), one int64 tensor instead of 40 batch lists.
+    Anything else takes _epoch_batches."""
+    from torch.utils.data import BatchSampler, RandomSampler
+
+    s = loader.sampler
+    n = len(loader.dataset)
+    if (type(s) is RandomSampler and s.generator is None and not s.replacement
+            and loader.generator is None and s.num_samples == n
+            and type(loader.batch_sampler) is BatchSampler and not loader.drop_last):
+        torch.empty((), dtype=torch.int64).random_()  # the iterator's _base_seed
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())
+        g = torch.Generator()
+        g.manual_seed(seed)
+        return torch.randperm(n, generator=g)
+    batches = _epoch_batches(loader)
+    return torch.cat(batches) if batches else torch.zeros(0, dtype=torch.int64)
+
+
 def _labels(loader, dev):
     y = loader.dataset.sentiment.to(dev, torch.float32)
     return y.reshape(y.shape[0], -1).contiguous()
@@ -202,7 +226,15 @@ def train_sentiment(args, model, train_data, train_latents, valid_data, valid_la
                     model_loader, valid_niter=10, verbose=False, model_save_path=None):
     """sentiment_model.py:76-163: SGD on mean L1 over shuffled batches of 32,
     validation every `valid_niter` epochs, optional early stopping with
-    patience 10 / 3 trials / lr decay and best-model reload."""
+    patience 10 / 3 trials / lr decay and best-model reload.
+
+    The epochs AND the validation passes run inside mmb_mlp_train: without
+    early stopping the whole run is one launch and one read-back; with it,
+    one launch per stretch of epochs ending at a validation (the host's
+    early-stopping decision -- checkpoint, reload, lr decay, stop -- needs
+    that validation loss before the next epoch).  The sample orders are drawn
+    from the global torch RNG in the reference's order (each epoch's training
+    pass, then the validation pass where i % valid_niter == 0)."""
     n_epochs = args["n_sentiment_epochs"]
     lr = args["sentiment_lr"]
     patience = 10
@@ -214,10 +246,45 @@ def train_sentiment(args, model, train_data, train_latents, valid_data, valid_la
     optimizer = optim.SGD(model.parameters(), lr=lr)  # state_dict-compatible checkpoints
     lat = train_latents.detach().to(dev, torch.float32).contiguous()
     lab = _labels(train_data, dev)
-    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, dtype=torch.float32,
-                     device=dev)
     B = train_data.batch_size
     spe = (n_samples + B - 1) // B
+    n_valid = len(valid_data.dataset)
+    vlat = valid_latents.detach().to(dev, torch.float32).contiguous()
+    vlab = _labels(valid_data, dev)
+    in_kernel = valid_data.batch_size == B and n_valid > 0
+    nbv = (n_valid + B - 1) // B if in_kernel else 0
+    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, dtype=torch.float32,
+                     device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def run(i, block, lr):
+        """Epochs i .. i + block - 1: per-step losses [block, spe] and the
+        per-batch losses of each validation in the stretch (host arrays)."""
+        perms, vperms = [], []
+        for e in range(i, i + block):
+            perms.append(_epoch_perm(train_data))
+            if in_kernel and e % valid_niter == 0:
+                vperms.append(_epoch_perm(valid_data))
+        perm = torch.cat(perms).to(dev)
+        step_loss = torch.empty(spe * block, dtype=torch.float32, device=dev)
+        if in_kernel and vperms:
+            vperm = torch.cat(vperms).to(dev)
+            vloss = torch.empty(len(vperms) * nbv, dtype=torch.float32, device=dev)
+            vargs = (L.ptr(vlat), L.ptr(vlab), L.ptr(vperm), n_valid, valid_niter, i, L.ptr(vloss))
+        else:
+            vloss = None
+            vargs = (None, None, None, 0, 1, i, None)
+        L.call("mmb_mlp_train", L.ptr(lat), L.ptr(lab), L.ptr(perm), n_samples, block, B, d, h, o,
+               float(lr), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(step_loss), *vargs,
+               L.ptr(ws), L.ptr(flag), L.stream_ptr())
+        out = torch.cat([step_loss, vloss]) if vloss is not None else step_loss
+        host = out.cpu().numpy()  # the one read-back of the stretch
+        if int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT:
+            raise RuntimeError("mmb_mlp_train: the exchange between its workgroups timed out; "
+                               "the regressor's parameters are invalid")
+        sl = host[:spe * block].reshape(block, spe)
+        vl = host[spe * block:].reshape(len(vperms), nbv) if vloss is not None else None
+        return sl, vl
 
     train_losses, valid_losses = [], []
     n_bad = 0
@@ -225,21 +292,30 @@ def train_sentiment(args, model, train_data, train_latents, valid_data, valid_la
     i = 0
     last_epoch_loss = 0.0
     while i < n_epochs:
-        block = 1 if i % valid_niter == 0 else min(valid_niter - i % valid_niter, n_epochs - i)
-        perm = torch.cat([torch.cat(_epoch_batches(train_data)) for _ in range(block)]).to(dev)
-        step_loss = torch.empty(spe * block, dtype=torch.float32, device=dev)
-        L.call("mmb_mlp_train", L.ptr(lat), L.ptr(lab), L.ptr(perm), n_samples, block, B, d, h, o,
-               float(lr), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(step_loss), L.ptr(ws),
-               L.stream_ptr())
-        sl = step_loss.cpu().numpy().reshape(block, spe)
+        if args["early_stopping"]:  # stop at the next validation: the host decides there
+            block = 1 if i % valid_niter == 0 else min(valid_niter - i % valid_niter + 1,
+                                                       n_epochs - i)
+        else:
+            block = n_epochs - i
+        if not in_kernel:
+            block = 1 if i % valid_niter == 0 else min(valid_niter - i % valid_niter, n_epochs - i)
+        sl, vl = run(i, block, lr)
+        stop = False
+        k = 0
         for e in range(block):
+            ep = i + e
             train_losses.append(_f32_mean_of(sl[e], spe))
-        last_epoch_loss = float(np.float32(np.sum(sl[-1], dtype=np.float32)))
-        if i % valid_niter == 0:
-            bl, _, _, _ = _evaluate(valid_data, model, valid_latents, dev)
-            bl = bl.cpu().numpy()
-            avg_valid_loss = _f32_mean_of(bl, len(bl))
-            print("Epoch {}: {} (avg val loss {})".format(i, train_losses[-1], avg_valid_loss))
+            last_epoch_loss = float(np.float32(np.sum(sl[e], dtype=np.float32)))
+            if ep % valid_niter != 0:
+                continue
+            if in_kernel:
+                avg_valid_loss = _f32_mean_of(vl[k], nbv)
+            else:
+                bl, _, _, _ = _evaluate(valid_data, model, valid_latents, dev)
+                bl = bl.cpu().numpy()
+                avg_valid_loss = _f32_mean_of(bl, len(bl))
+            k += 1
+            print("Epoch {}: {} (avg val loss {})".format(ep, train_losses[-1], avg_valid_loss))
             is_better = len(valid_losses) == 0 or avg_valid_loss < min(valid_losses)
             valid_losses.append(avg_valid_loss)
             if args["early_stopping"]:
@@ -267,9 +343,10 @@ def train_sentiment(args, model, train_data, train_latents, valid_data, valid_la
                             n_bad = 0
                         else:
                             print("early stopping...")
-                            i += block
-                            break
+                            stop = True
         i += block
+        if stop:
+            break
     print("Epoch {}: {}".format(i - 1, last_epoch_loss / n_samples))
     return train_losses, valid_losses
 

@@ -31,9 +31,61 @@ def _train_steps(gpu, x, y, w1, b1, w2, b2, lr, perm=None, epochs=1, batch=32):
     spe = (n + batch - 1) // batch
     sl = torch.empty(spe * epochs, dtype=torch.float32, device=gpu)
     ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
+    flag = torch.zeros(1, dtype=torch.int32, device=gpu)
     L.call("mmb_mlp_train", L.ptr(lat), L.ptr(lab), L.ptr(perm), n, epochs, batch, d, h, o,
-           float(lr), *[L.ptr(p) for p in P], L.ptr(sl), L.ptr(ws), L.stream_ptr())
+           float(lr), *[L.ptr(p) for p in P], L.ptr(sl), None, None, None, 0, 1, 0, None,
+           L.ptr(ws), L.ptr(flag), L.stream_ptr())
+    assert int(flag.item()) == 0
     return [p.cpu().numpy() for p in P], sl.cpu().numpy()
+
+
+@pytest.mark.parametrize("h,o,every", [(100, 1, 2), (150, 3, 1)])
+def test_in_launch_validation_equals_eval_kernel(gpu, h, o, every):
+    """mmb_mlp_train's validation passes (the weights of that moment, its own
+    sample order per validation) equal mmb_mlp_eval run between separate
+    training launches; the parameters after the one launch equal the
+    chained launches' bit for bit."""
+    rng = np.random.default_rng(h + o)
+    n, nv, d, B, epochs, lr = 130, 71, 300, 32, 4, 0.05
+    x = torch.tensor(rng.standard_normal((n, d)).astype(np.float32), device=gpu)
+    y = torch.tensor(rng.uniform(-3, 3, (n, o)).astype(np.float32), device=gpu)
+    xv = torch.tensor(rng.standard_normal((nv, d)).astype(np.float32), device=gpu)
+    yv = torch.tensor(rng.uniform(-3, 3, (nv, o)).astype(np.float32), device=gpu)
+    torch.manual_seed(h)
+    init = [p.detach() for p in SM.SentimentModel(d, h, o).parameters()]
+    perm = torch.cat([torch.randperm(n) for _ in range(epochs)]).to(gpu)
+    nval = len([e for e in range(epochs) if e % every == 0])
+    vperm = torch.cat([torch.randperm(nv) for _ in range(nval)]).to(gpu)
+    spe, nbv = -(-n // B), -(-nv // B)
+    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
+    flag = torch.zeros(1, dtype=torch.int32, device=gpu)
+    P1 = [p.clone().to(gpu).contiguous() for p in init]
+    sl1 = torch.empty(spe * epochs, device=gpu)
+    vl1 = torch.empty(nval * nbv, device=gpu)
+    L.call("mmb_mlp_train", L.ptr(x), L.ptr(y), L.ptr(perm), n, epochs, B, d, h, o, float(lr),
+           *[L.ptr(p) for p in P1], L.ptr(sl1), L.ptr(xv), L.ptr(yv), L.ptr(vperm), nv, every, 0,
+           L.ptr(vl1), L.ptr(ws), L.ptr(flag), L.stream_ptr())
+    P2 = [p.clone().to(gpu).contiguous() for p in init]
+    sl2, vl2 = [], []
+    k = 0
+    for e in range(epochs):
+        s = torch.empty(spe, device=gpu)
+        L.call("mmb_mlp_train", L.ptr(x), L.ptr(y), L.ptr(perm[e * n:(e + 1) * n].contiguous()), n,
+               1, B, d, h, o, float(lr), *[L.ptr(p) for p in P2], L.ptr(s), None, None, None, 0, 1,
+               0, None, L.ptr(ws), L.ptr(flag), L.stream_ptr())
+        sl2.append(s)
+        if e % every == 0:
+            bl = torch.empty(nbv, device=gpu)
+            L.call("mmb_mlp_eval", L.ptr(xv), L.ptr(yv), L.ptr(vperm[k * nv:(k + 1) * nv].contiguous()),
+                   nv, B, d, h, o, *[L.ptr(p) for p in P2], L.ptr(bl), None, L.stream_ptr())
+            vl2.append(bl)
+            k += 1
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 0
+    for a, b in zip(P1, P2):
+        assert torch.equal(a, b)
+    assert torch.equal(sl1, torch.cat(sl2))
+    np.testing.assert_allclose(vl1.cpu().numpy(), torch.cat(vl2).cpu().numpy(), rtol=2e-6, atol=1e-7)
 
 
 def test_one_sgd_step(gpu, golden):

@@ -43,6 +43,34 @@ def test_loader_emulation_consumes_rng_like_iteration(n, bs):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,bs,shuffle", [(1284, 32, True), (229, 32, True), (5, 32, True),
+                                          (33, 32, False)])
+def test_epoch_perm_consumes_rng_like_iteration(n, bs, shuffle):
+    """_epoch_perm (one randperm per pass, the fast path of the one-launch
+    training loop) yields the rows of real DataLoader iteration in order and
+    leaves the global RNG where iteration leaves it -- interleaved with a
+    second loader, as the reference's train / validation passes are."""
+    data = SM.SentimentData(np.arange(n, dtype=np.float32), torch.device("cpu"))
+    loader = DataLoader(data, batch_size=bs, shuffle=shuffle)
+    other = DataLoader(SM.SentimentData(np.arange(7, dtype=np.float32), torch.device("cpu")),
+                       batch_size=bs, shuffle=True)
+    torch.manual_seed(11)
+    real = []
+    for _ in range(3):
+        real.append(torch.cat([j.clone() for j, _ in loader]))
+        real.append(torch.cat([j.clone() for j, _ in other]))
+    after_real = torch.rand(4)
+    torch.manual_seed(11)
+    emu = []
+    for _ in range(3):
+        emu.append(SM._epoch_perm(loader))
+        emu.append(SM._epoch_perm(other))
+    after_emu = torch.rand(4)
+    assert torch.equal(after_real, after_emu)
+    for r, e in zip(real, emu):
+        assert torch.equal(r, e)
+
+
 def test_f32_epoch_mean_matches_tensor_arithmetic():
     vals = np.random.default_rng(0).random(41).astype(np.float32)
     acc = 0

@@ -69,7 +69,8 @@ def test_version_and_shape_helpers():
     assert mmb_lib.query("mmb_mm2_k", 300, 76, 48) == 864
     assert mmb_lib.query("mmb_mm2_ldw", 300) == 320
     assert mmb_lib.query("mmb_gram_workspace_bytes", 1_000_000, 300) > 0
-    assert mmb_lib.query("mmb_mlp_workspace_bytes", 300, 100) == 4 * 10 * 64 * 16 * 4
+    # arrival counter + abort word, then 2 x 4 hidden tiles x 32 rows x 16 outputs of f32 shares
+    assert mmb_lib.query("mmb_mlp_workspace_bytes", 300, 100) == 16 + 4 * 2 * 4 * 32 * 16
 
 
 @pytest.mark.parametrize("seed,rows,k", [(0, 300, 11), (0, 64, 11), (0, 1, 12), (7, 1000, 3)])
