@@ -670,11 +670,15 @@ __global__ __launch_bounds__(256) void mlp_bwd_params_kernel(const float* __rest
 
 template <int NTD>
 static int launch_train_mc(const TrainArgs& a, size_t lds, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_mc_kernel<NTD>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
+  // the dynamic LDS this launch needs (the kernel also has a static word, so
+  // the full 160 KB cannot be requested)
+  static size_t attr_set = 0;
+  if (lds > attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_mc_kernel<NTD>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             static_cast<int>(lds));
+    if (e != hipSuccess) return static_cast<int>(e);
+    attr_set = lds;
   }
   mlp_train_mc_kernel<NTD><<<a.P, kTrNT, lds, stream>>>(a);
   MMB_LAUNCH_CHECK();
@@ -747,7 +751,7 @@ extern "C" int mmb_mlp_train(const float* latents, const float* labels, const in
   const size_t lds = sizeof(float) * (6 * kBatchMax + 2 * static_cast<size_t>(kBatchMax) * (32 * a.nTd + 1) +
                                       2 * kBatchMax * o + kTrWaves * kBatchMax * 32 +
                                       kBatchMax * 32 + kBatchMax * o + o * 32 + 32 + o + kTrWaves);
-  MMB_REQUIRE(lds <= 160 * 1024);
+  MMB_REQUIRE(lds <= 156 * 1024);
   const hipError_t e = hipMemsetAsync(ws, 0, 16, stream);
   if (e != hipSuccess) return static_cast<int>(e);
   switch (a.nTd) {
