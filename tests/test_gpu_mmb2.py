@@ -761,14 +761,24 @@ def _split_check(gen, sp, sif_out, mm2_out, pc, rows, x, ref_rows=None, ref_pc=N
     the real POM valid split (s1/s2 = 24)."""
     E, wt, ids = sp["table"], sp["weights"], sp["ids"]
     sif_ref = O.get_sentence_embeddings(E, wt, ids)
-    assert M.row_rel_err(sif_out.double().cpu().numpy(), sif_ref) < TOL
+    sif = sif_out.double().cpu().numpy()
+    # SIF rows: 1e-5 row-relative of the reference's f32 path -- or, where the
+    # transcripts are long (POM: up to 1357 tokens, the a2 rows f32 sums of
+    # ~370 table rows before a PC removal that cancels ~95 % of them), within
+    # 3x the reference's OWN distance from the exact (f64) evaluation: two f32
+    # summation orders of the same rows then differ by about that much
+    exact = O.get_sentence_embeddings(E.astype(np.float64), wt, ids)
+    e_ref, e_gpu = M.row_rel_err(sif_ref, exact), M.row_rel_err(sif, exact)
+    print(f"SIF row-rel: gpu vs reference {M.row_rel_err(sif, sif_ref):.2e}, gpu vs exact "
+          f"{e_gpu:.2e}, reference vs exact {e_ref:.2e}")
+    assert M.row_rel_err(sif, sif_ref) < TOL or e_gpu <= 3 * e_ref
     got = pc.cpu().numpy()
     assert np.abs(got - O.compute_pc(x.double().cpu().numpy())).max() < 1e-12
     pc_ref = O.compute_pc(O.get_weighted_average(E, ids, O.seq2weight(ids, np.ones(ids.shape), wt)))
     assert np.abs(got - pc_ref).max() < 1e-7
     if ref_pc is not None:  # the reference's own run (g11)
         assert np.abs(got - ref_pc).max() < 1e-7
-        assert M.row_rel_err(sif_out.double().cpu().numpy()[::8], ref_rows) < TOL
+        assert np.array_equal(sif_ref[::8], ref_rows)  # the oracle IS the reference here
     r = rows
     sw = O.seq2weight(ids[r], np.ones(ids[r].shape), wt)
     text = E[ids[r]]
