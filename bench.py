@@ -525,7 +525,7 @@ def regressor_config(dev, cpu_epochs=40):
     y = torch.tensor(lab[0], device=dev).reshape(-1, 1).contiguous()
     perm = torch.cat([torch.randperm(sizes[0]) for _ in range(epochs)]).to(dev)
     sl = torch.empty(steps, device=dev)
-    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", 300, H) // 4 + 4, device=dev)
+    ws = torch.zeros(L.query("mmb_mlp_workspace_bytes", 300, H) // 4 + 4, device=dev)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     L.call("mmb_mlp_train", L.ptr(x), L.ptr(y), L.ptr(perm), sizes[0], epochs, B, 300, H, 1,

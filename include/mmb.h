@@ -126,10 +126,12 @@ int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n
  * exchanged in-launch (write-through stores + an arrival counter), and every
  * workgroup runs the identical CholeskyQR; workgroup 0 runs the final
  * Rayleigh-Ritz step.  ws: mmb_pc_solve_mc_ws_bytes(d) bytes, 16-byte
- * aligned, owned by the call until it completes (its first 16 bytes are
- * zeroed by a memset the call enqueues).  A workgroup that waits ~1 s for the
- * others gives up and sets MMB_FLAG_SYNC_TIMEOUT in *flag (nullable); pc_out
- * is then invalid.
+ * aligned, owned by the call until it completes; its first 16 bytes (arrival
+ * counter, abort word) must be ZERO when the caller first hands it over, and
+ * a completed solve leaves them zero -- no memset is enqueued, so the call is
+ * safe to capture into a graph and replay.  A workgroup that waits ~1 s for
+ * the others gives up and sets MMB_FLAG_SYNC_TIMEOUT in *flag (nullable);
+ * pc_out is then NaN and ws must be re-zeroed before the next call.
  * replaces: sif_functions.compute_pc /root/reference/sif_functions.py:58-67 */
 size_t mmb_pc_solve_mc_ws_bytes(int d);
 int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
@@ -339,9 +341,10 @@ int mmb_mlp_eval(const float* latents, const float* labels, const int64_t* perm,
  * (epoch0 + e) % valid_every == 0 the per-batch mean L1 of the validation rows
  * v_perm[k * n_valid ...] (k = the k-th such epoch of this launch) with the
  * weights of that moment go to valid_loss[k * ceil(n_valid / batch) + j].
- * ws: scratch of mmb_mlp_workspace_bytes(d, h) bytes (16-B aligned); flag
- * (nullable) gets MMB_FLAG_SYNC_TIMEOUT if the workgroups' exchange stalls
- * (~1 s; the parameters are then invalid).  d % 4 == 0, d <= 512, h <= 512,
+ * ws: scratch of mmb_mlp_workspace_bytes(d, h) bytes (16-B aligned), ZEROED
+ * by the caller before its first use (a completed launch leaves it zeroed);
+ * flag (nullable) gets MMB_FLAG_SYNC_TIMEOUT if the workgroups' exchange
+ * stalls (~1 s; the parameters are then invalid and ws must be re-zeroed).  d % 4 == 0, d <= 512, h <= 512,
  * n_out <= 16.
  * replaces: sentiment_model.train_sentiment loop incl. its validation passes
  *   /root/reference/sentiment_model.py:76-127                               */

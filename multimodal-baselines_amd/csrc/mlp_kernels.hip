@@ -70,7 +70,7 @@ struct TrainArgs {
   float* b2;
   float* step_loss;
   float* xbuf;    // [2][P][32 * O] output shares
-  unsigned* ctl;  // arrival counter, abort word (zeroed by the launcher)
+  unsigned* ctl;  // arrival counter, abort word (zero at entry; left zero)
   int32_t* flag;
 };
 
@@ -376,6 +376,13 @@ __global__ __launch_bounds__(kTrNT) void mlp_train_mc_kernel(TrainArgs a) {
     tr_advance(a, nx2);
   }
 
+  // the last workgroup past its final exchange returns the counter to 0 (the
+  // next launch then needs no memset to find it there)
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == static_cast<unsigned>(a.P) * (xc + 1) - 1)
+      __hip_atomic_store(a.ctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // write this tile's parameters back (b2 by workgroup 0)
 #pragma unroll
   for (int j = 0; j < kFT; ++j) {
@@ -752,8 +759,8 @@ extern "C" int mmb_mlp_train(const float* latents, const float* labels, const in
                                       2 * kBatchMax * o + kTrWaves * kBatchMax * 32 +
                                       kBatchMax * 32 + kBatchMax * o + o * 32 + 32 + o + kTrWaves);
   MMB_REQUIRE(lds <= 156 * 1024);
-  const hipError_t e = hipMemsetAsync(ws, 0, 16, stream);
-  if (e != hipSuccess) return static_cast<int>(e);
+  // the control words are zero when ws is first handed over and the last
+  // workgroup leaves them zero (no memset node: see mmb_pc_solve_mc)
   switch (a.nTd) {
 #define MMB_TRAIN_NTD(n) \
     case n: return launch_train_mc<n>(a, lds, stream);

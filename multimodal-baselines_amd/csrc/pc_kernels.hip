@@ -1522,8 +1522,10 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
 // of the scaled block; the block entering the tail still gets CholeskyQR2.
 // ws: [2][T][512] doubles of tiles (double-buffered by round parity: a round
 // r + 2 write needs every workgroup past round r + 1's wait, hence done
-// reading round r), then the arrival counter and the abort word (zeroed by
-// the launcher before every launch).
+// reading round r), then the arrival counter and the abort word (zero when
+// the caller first hands ws over; workgroup 0 returns the counter to zero
+// once every workgroup has made its last arrival, so a launch -- eager or a
+// graph replay -- leaves ws ready for the next one).
 constexpr int kPmPw = 15;  // waves holding G (wave 15 runs the Cholesky meanwhile)
 constexpr int kPmKs = 6;   // k-steps of G per wave: ceil(kP16MaxD / 4 / kPmPw)
 constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
@@ -1774,7 +1776,15 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!(last && t != 0)) {
-          if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) s_abort = 1;
+          if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) {
+            s_abort = 1;
+          } else if (last) {
+            // every workgroup has made its last arrival: the counter is free
+            // again, so the next launch finds it at 0 even where the launcher's
+            // memset is not what it reads first (graph replays, r04: the
+            // second replay of a captured step saw the last launch's count)
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
           // acquire: the gather below reads the other workgroups' tiles only
           // after their arrivals were observed (the __syncthreads that follows
           // releases the other waves of this workgroup)
@@ -2290,8 +2300,10 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
                               static_cast<int>(p16_lds_bytes(kP16MaxD)));
     attr = true;
   }
-  const hipError_t e = hipMemsetAsync(ctl, 0, 16, stream);
-  if (e != hipSuccess) return static_cast<int>(e);
+  // no memset node here: the counter / abort words must be zero when the
+  // caller first hands ws over, and a completed solve leaves them zero (a
+  // captured 16-byte hipMemsetAsync wrote garbage into the abort word on
+  // graph replays, r04)
   pc_solve_mc_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
                                                               pc_out, xbuf, ctl, flag);
   MMB_LAUNCH_CHECK();

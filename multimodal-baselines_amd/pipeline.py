@@ -191,8 +191,8 @@ def solve_workspace(d: int, device) -> torch.Tensor:
     it completes, and calls on one stream are ordered."""
     key = (d, str(device), L.stream_ptr())
     ws = _solve_ws.get(key)
-    if ws is None:
-        ws = torch.empty(L.query("mmb_pc_solve_mc_ws_bytes", d), dtype=torch.uint8, device=device)
+    if ws is None:  # zeroed once: a completed solve leaves its control words zero
+        ws = torch.zeros(L.query("mmb_pc_solve_mc_ws_bytes", d), dtype=torch.uint8, device=device)
         if len(_solve_ws) > 16:
             _solve_ws.clear()
         _solve_ws[key] = ws
@@ -220,6 +220,7 @@ def pc_solve(G: torch.Tensor, z0: torch.Tensor, npc: int, transposed: bool,
         L.call("mmb_pc_solve_mc", L.ptr(G), d, L.ptr(z0), k, npc, n_iter, int(transposed),
                L.ptr(pc), L.ptr(ws), L.ptr(flag), L.stream_ptr())
         if own and int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT:
+            ws[:16].zero_()  # an aborted solve leaves its control words set
             raise RuntimeError("mmb_pc_solve_mc: a bounded hand-over between the solver's "
                                "workgroups timed out; the PC is invalid (NaN)")
     else:
@@ -646,7 +647,7 @@ class FusedStep:
             self.proj.enable_pieces()
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
         self.pc_buf = torch.empty((npc, self.d), dtype=torch.float64, device=dev)
-        self.solve_ws = (torch.empty(L.query("mmb_pc_solve_mc_ws_bytes", self.d), dtype=torch.uint8,
+        self.solve_ws = (torch.zeros(L.query("mmb_pc_solve_mc_ws_bytes", self.d), dtype=torch.uint8,
                                      device=dev) if self.d <= PC_SOLVE_MC_MAX_D else None)
         self.sif = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
         self.mmb2 = torch.empty((self.n, self.d), dtype=torch.float32, device=dev)
@@ -719,6 +720,8 @@ class FusedStep:
             t = torch.stack([(flag[0] & b) != 0 for b in bits]).to(torch.int32)
             self.allreduce(t)
             flag = sum((t[i] > 0).to(torch.int32) * b for i, b in enumerate(bits)).reshape(1)
+        if int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT and self.solve_ws is not None:
+            self.solve_ws[:16].zero_()  # an aborted solve leaves its control words set
         check_flag(flag, self.V, zero_weights=True)
         if getattr(self, "pc", None) is not None:
             check_pc_finite(self.pc)

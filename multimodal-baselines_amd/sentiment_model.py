@@ -253,8 +253,8 @@ def train_sentiment(args, model, train_data, train_latents, valid_data, valid_la
     vlab = _labels(valid_data, dev)
     in_kernel = valid_data.batch_size == B and n_valid > 0
     nbv = (n_valid + B - 1) // B if in_kernel else 0
-    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, dtype=torch.float32,
-                     device=dev)
+    ws = torch.zeros(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, dtype=torch.float32,
+                     device=dev)  # zeroed once: the launch leaves its control words zero
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def run(i, block, lr):

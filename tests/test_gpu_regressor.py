@@ -30,7 +30,7 @@ def _train_steps(gpu, x, y, w1, b1, w2, b2, lr, perm=None, epochs=1, batch=32):
     perm = torch.as_tensor(perm, dtype=torch.int64, device=gpu)
     spe = (n + batch - 1) // batch
     sl = torch.empty(spe * epochs, dtype=torch.float32, device=gpu)
-    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
+    ws = torch.zeros(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
     flag = torch.zeros(1, dtype=torch.int32, device=gpu)
     L.call("mmb_mlp_train", L.ptr(lat), L.ptr(lab), L.ptr(perm), n, epochs, batch, d, h, o,
            float(lr), *[L.ptr(p) for p in P], L.ptr(sl), None, None, None, 0, 1, 0, None,
@@ -57,7 +57,7 @@ def test_in_launch_validation_equals_eval_kernel(gpu, h, o, every):
     nval = len([e for e in range(epochs) if e % every == 0])
     vperm = torch.cat([torch.randperm(nv) for _ in range(nval)]).to(gpu)
     spe, nbv = -(-n // B), -(-nv // B)
-    ws = torch.empty(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
+    ws = torch.zeros(L.query("mmb_mlp_workspace_bytes", d, h) // 4 + 4, device=gpu)
     flag = torch.zeros(1, dtype=torch.int32, device=gpu)
     P1 = [p.clone().to(gpu).contiguous() for p in init]
     sl1 = torch.empty(spe * epochs, device=gpu)

@@ -248,6 +248,7 @@ def check_timeouts(dev):
     finally:
         assert lib.mmb_diag_pc_wait_iters(1 << 20) == 0
     flag.zero_()
+    P.solve_workspace(300, dev)[:16].zero_()  # an aborted solve leaves its control words set
     pc1 = P.pc_solve(G, z0, 1, False, flag=flag)
     torch.cuda.synchronize()
     assert int(flag.item()) == 0 and torch.equal(pc0, pc1)
