@@ -300,6 +300,32 @@ int mmb_mm2_project_x3_rmpc(const void* s_split, const float* num, const float* 
                             const void* wsplit, int ldw, const float* c0, int64_t n, int k, int d,
                             float* out, const double* pc, float* sif_out, hipStream_t stream);
 
+/* MMB2 at narrow frame widths (MOSI) in ONE kernel, a1-a8's stream and the
+ * projection fused: the text rows of the merged projection are applied per
+ * vocabulary row (text cache: P[v] = E_v Wm_t1 + E_v^2 Wm_t2, f64 rounded
+ * once; the 32 words of smallest SIF weight kept in LDS), so only the
+ * audio / visual frame sums (K = kq(A) + kq(Vd) <= 256) meet the f16 x3 MFMA,
+ * inside the same launch; the frame sums never reach HBM.  Writes x (the a2
+ * rows, bit-identical to mmb_mm2_stream's), aux, the MMB2 rows and (colmax
+ * non-null) the column bounds of x for mmb_gram_i8.
+ *   mmb_mm2_text_cache: cache of mmb_mm2_text_cache_bytes(v, d) bytes (16-B
+ *   aligned) from the word table, the f32 weight table and the merged Wm
+ *   (mmb_mm2_prepare); rebuild it when any of them changes.  v <= 16384.
+ *   wpieces: the piece-ordered weight split (mmb_mm2_split_pieces).
+ * replaces: sif2.calc_weights + estimate_embedding_overall_gpu2
+ *   /root/reference/sif2.py:103-114,164-208 with the text gather of
+ *   /root/reference/simplesif.py:862-871 and sif_functions.py:28-56      */
+size_t mmb_mm2_text_cache_bytes(int64_t v, int d);
+int mmb_mm2_text_cache(const float* table, int64_t v, int d, const float* wtab32, const float* wm,
+                       int ldw, void* cache, hipStream_t stream);
+int mmb_mm2_stream_project_narrow_supported(int t, int d, int a, int vd, int64_t v);
+int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* table, int64_t v,
+                                  const float* wtab32, const void* text_cache, const float* audio,
+                                  const float* visual, int64_t n, int t, int d, int a, int vd,
+                                  const void* wpieces, const float* c0, float* num_out,
+                                  float* aux_out, float* mmb2_out, int32_t* flag, uint32_t* colmax,
+                                  void* colmax_ws, hipStream_t stream);
+
 /* ---------------------------------------------------------------- a10/a11
  * SentimentModel(d -> h -> o): y = squeeze(W2 relu(W1 x + b1) + b2).
  * Forward for rows idx[0..b) (idx nullable = 0..b) of latents [*, d].

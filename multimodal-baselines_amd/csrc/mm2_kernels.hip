@@ -1911,3 +1911,90 @@ extern "C" int mmb_mm2_split_pieces(const float* wm, int d, int a, int vd, int l
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
+
+// ------------------------------------------------------------------ text cache (r04)
+// The MOSI-width fused step (mmb_mm2_stream_project_narrow) projects the text
+// sums per vocabulary row instead of per utterance: the text rows of Wm enter
+// the MMB2 numerator only through sum_t E_t Wm_text1 + sum_t E_t^2 Wm_text2 =
+// sum_t P[id_t] with
+//   P[v][j] = sum_f E[v][f] Wm[f][j] + E[v][f]^2 Wm[D + f][j]     (j <= D)
+// (exact algebra; column D carries the total weight), so an utterance gathers
+// one P row per token beside its table row, and the per-utterance GEMM shrinks
+// to the audio / visual sums (K = 2 (A + Vd) instead of 2 (D + A + Vd)).  P is
+// computed in f64 and rounded once.  The cache also ranks the words by weight:
+// the kTextHot smallest SIF weights a / (a + p(w)) are the most frequent words
+// (the pad id 0 too where its weight is 0), whose E and P rows the fused
+// kernel keeps in LDS.
+//   cache layout: P [v][kTextLdp] f32 | hot_slot1 [v] int32 (slot + 1, 0 = not
+//   hot) | hot_ids [kTextHot] int32
+constexpr int kTextLdp = 304;   // P row stride (floats): d + 1 <= 304, 16-byte rows
+constexpr int kTextHot = 32;    // words whose rows live in LDS
+constexpr int64_t kTextMaxV = 16384;
+
+__global__ __launch_bounds__(320) void mm2_text_table_kernel(const float* __restrict__ E, int D,
+                                                             const float* __restrict__ wm, int ldw,
+                                                             float* __restrict__ ptab) {
+  __shared__ double se[kTextLdp], se2[kTextLdp];
+  const int64_t v = blockIdx.x;
+  for (int f = threadIdx.x; f < D; f += blockDim.x) {
+    const double e = E[v * D + f];
+    se[f] = e;
+    se2[f] = e * e;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < kTextLdp; j += blockDim.x) {
+    double acc = 0.0;
+    if (j <= D) {
+      for (int f = 0; f < D; ++f) {
+        acc = fma(se[f], static_cast<double>(wm[static_cast<int64_t>(f) * ldw + j]), acc);
+        acc = fma(se2[f], static_cast<double>(wm[static_cast<int64_t>(D + f) * ldw + j]), acc);
+      }
+    }
+    ptab[v * kTextLdp + j] = static_cast<float>(acc);
+  }
+}
+
+// rank of each word among the weights (ascending; ties: lower id first):
+// hot_slot1[v] = rank + 1 for the k smallest, else 0; hot_ids[rank] = v
+__global__ __launch_bounds__(1024) void text_hot_kernel(const float* __restrict__ wtab, int V, int k,
+                                                        int32_t* __restrict__ hot_slot1,
+                                                        int32_t* __restrict__ hot_ids) {
+  __shared__ float sw[1024];
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  const float wv = v < V ? wtab[v] : 0.f;
+  int rank = 0;
+  for (int u0 = 0; u0 < V; u0 += 1024) {
+    __syncthreads();
+    if (u0 + static_cast<int>(threadIdx.x) < V) sw[threadIdx.x] = wtab[u0 + threadIdx.x];
+    __syncthreads();
+    const int n = min(1024, V - u0);
+    for (int j = 0; j < n; ++j) {
+      const float wu = sw[j];
+      rank += (wu < wv || (wu == wv && u0 + j < v)) ? 1 : 0;
+    }
+  }
+  if (v < V) {
+    hot_slot1[v] = rank < k ? rank + 1 : 0;
+    if (rank < k) hot_ids[rank] = v;
+  }
+}
+
+extern "C" size_t mmb_mm2_text_cache_bytes(int64_t v, int d) {
+  (void)d;
+  return sizeof(float) * static_cast<size_t>(v) * kTextLdp + sizeof(int32_t) * (v + kTextHot);
+}
+
+extern "C" int mmb_mm2_text_cache(const float* table, int64_t v, int d, const float* wtab32,
+                                  const float* wm, int ldw, void* cache, hipStream_t stream) {
+  MMB_REQUIRE(table && wtab32 && wm && cache && v > 0 && v <= kTextMaxV);
+  MMB_REQUIRE(d > 0 && d + 1 <= kTextLdp && ldw > d && (reinterpret_cast<uintptr_t>(cache) & 15) == 0);
+  float* ptab = static_cast<float*>(cache);
+  int32_t* hot_slot1 = reinterpret_cast<int32_t*>(ptab + static_cast<size_t>(v) * kTextLdp);
+  int32_t* hot_ids = hot_slot1 + v;
+  mm2_text_table_kernel<<<static_cast<unsigned>(v), 320, 0, stream>>>(table, d, wm, ldw, ptab);
+  MMB_LAUNCH_CHECK();
+  text_hot_kernel<<<static_cast<unsigned>(ceil_div(v, 1024)), 1024, 0, stream>>>(
+      wtab32, static_cast<int>(v), static_cast<int>(std::min<int64_t>(v, kTextHot)), hot_slot1, hot_ids);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}

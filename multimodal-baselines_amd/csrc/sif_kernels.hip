@@ -2553,3 +2553,483 @@ extern "C" int mmb_diag_fused_probe(unsigned long long* host_out, int* rate_khz)
   return e == hipSuccess ? MMB_OK : static_cast<int>(e);
 }
 #endif
+
+// ------------------------------------------------------------------ narrow fused (r04)
+// SIF + closed-form MMB2 at narrow frame widths (MOSI: COVAREP A = 76, FACET
+// Vd = 48, V = 3016) in ONE kernel: the two-kernel step wrote the frame sums
+// s (fp16 hi | lo of 2 (D + A + Vd) = 848 sums, 3.4 KB per utterance) to HBM
+// and read them back in a K = 864 projection.  Here the text sums never
+// form: the text rows of Wm are applied per vocabulary row (the text cache,
+// mmb_mm2_text_cache: P[v] = E_v Wm_t1 + E_v^2 Wm_t2, column D the total
+// weight), so an utterance's text term is sum_t P[id_t], gathered beside its
+// table rows, and only the audio / visual sums [Sa | Saa | Sv | Svv] (K =
+// kq(A) + kq(Vd) <= 256) go through the f16 x3 MFMA -- in the same launch.
+//
+// One persistent 512-thread workgroup per CU, batches of 32 utterances:
+//   stream phase: every wave runs 4 utterances as utt_narrow_kernel does
+//     (packed frame instructions issued first, ids one utterance ahead,
+//     buffer-descriptor loads), its text rows from LDS for the 32 words of
+//     smallest weight (the most frequent; ~58 % of Zipf(1.1) tokens at
+//     V = 3016) and from L2 otherwise; it writes x (the a2 row, bit-identical
+//     to the narrow kernel's: the same f32 operations in the same order),
+//     aux, its column bounds, and into LDS the row's text term T (x-sum + sum
+//     of P) and its audio / visual sums as fp16 hi | lo (power-of-2 row scale);
+//   MFMA phase (after a barrier): [32 x K] x [K x 320] as fp16 x3 products
+//     (v_mfma_f32_16x16x32_f16, the fused kernel's projector arithmetic; B =
+//     the audio / visual chunks of the piece-ordered weight image, from L2);
+//   epilogue: y = acc * scales + T + c0 into the T rows (LDS), then per row
+//     the division by the total weight (column D) and the L2 norm, the MMB2
+//     row written with 16-byte stores.
+// LDS: hot E rows 38.4 KB + hot P rows 38.9 KB + T 38.9 KB + A 32 KB.
+constexpr int kNFThreads = 512;
+constexpr int kNFWaves = kNFThreads / kWave;
+constexpr int kNFRows = 32;                 // utterances per batch
+constexpr int kNFPerWave = kNFRows / kNFWaves;
+constexpr int kNFHot = 32;                  // = mm2_kernels.hip kTextHot
+constexpr int kNFLdp = 304;                 // = kTextLdp (P row stride, floats)
+constexpr int kNFK = 256;                   // K of the audio / visual GEMM (max)
+constexpr int kNFLdw = 320;                 // projection columns
+constexpr int kNFCT = kNFLdw / 16;          // 16-column tiles (20)
+constexpr size_t kNFLds = sizeof(float) * (kNFHot * 300 + kNFHot * kNFLdp + kNFRows * kNFLdp) +
+                          sizeof(_Float16) * kNFRows * 2 * kNFK + sizeof(float) * 3 * kNFRows;
+
+struct NarrowFusedArgs {
+  StreamArgs s;        // ids, table, V, wtab, audio, visual, N, L, D, A, Vd, num_out, aux_out, flag, cmax_part
+  const float* ptab;   // [V][kNFLdp]
+  const int32_t* hot_slot1;  // [V]
+  const int32_t* hot_ids;    // [n_hot]
+  int n_hot;
+  const _Float16* img;       // piece-ordered weight image (mmb_mm2_split_pieces)
+  const float* col_inv;
+  const float* c0;
+  float* out;                // MMB2 rows [N][D]
+  int cb_av;                 // first audio chunk of the image (kq(D) / 32)
+  int kq_a, kq_v;            // K rows of the audio / visual pieces (multiples of 32)
+  int64_t nb;                // batches
+};
+
+template <int UNR, int GA_MAX, int GV_MAX>
+__global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_narrow_fused_kernel(
+    NarrowFusedArgs f) {
+  extern __shared__ __attribute__((aligned(16))) float nf_lds[];
+  float* hotE = nf_lds;                                   // [kNFHot][300]
+  float* hotP = hotE + kNFHot * 300;                      // [kNFHot][kNFLdp]
+  float* sT = hotP + kNFHot * kNFLdp;                     // [32][kNFLdp]
+  _Float16* sA = reinterpret_cast<_Float16*>(sT + kNFRows * kNFLdp);  // [32][2][kNFK] swizzled
+  float* s_irs = reinterpret_cast<float*>(sA + kNFRows * 2 * kNFK);   // [32] 1 / row scale
+  float* s_cnt = s_irs + kNFRows;                         // [32]
+  float* s_ok = s_cnt + kNFRows;                          // [32] 1 = a row of this batch
+
+  const StreamArgs& a = f.s;
+  constexpr int CT = 2;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int64_t wid = static_cast<int64_t>(blockIdx.x) * kNFWaves + wave;
+  const int L = a.L, D = a.D;
+  const int UT = D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
+  const int UP = (D + 4) >> 2;  // P units holding columns 0..D
+  const int PA = kWave / UA, PV = kWave / UV;
+  const int GA = (L + PA - 1) / PA, GV = (L + PV - 1) / PV;
+
+  // the hot words' E and P rows into LDS
+  for (int e = tid; e < f.n_hot * 75; e += kNFThreads) {
+    const int k = e / 75, u = e - k * 75;
+    const int64_t v = f.hot_ids[k];
+    if (4 * u < D) *reinterpret_cast<float4*>(hotE + k * 300 + 4 * u) = ld4(a.table + v * D + 4 * u);
+  }
+  for (int e = tid; e < f.n_hot * (kNFLdp / 4); e += kNFThreads) {
+    const int k = e / (kNFLdp / 4), u = e - k * (kNFLdp / 4);
+    *reinterpret_cast<float4*>(hotP + k * kNFLdp + 4 * u) =
+        ld4(f.ptab + static_cast<int64_t>(f.hot_ids[k]) * kNFLdp + 4 * u);
+  }
+
+  int vt[CT], vp[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    vt[c] = 16 * min(lane + kWave * c, UT - 1);
+    vp[c] = 16 * min(lane + kWave * c, UP - 1);
+  }
+  const int tbytes = static_cast<int>(a.V * D * 4);
+  const int pbytes = static_cast<int>(a.V * kNFLdp * 4);
+  const auto trsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.table), 0, tbytes, 0x00020000);
+  const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f.ptab), 0, pbytes, 0x00020000);
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wtab), 0,
+                                                       static_cast<int>(a.V * 4), 0x00020000);
+  const auto hrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(f.hot_slot1), 0,
+                                                       static_cast<int>(a.V * 4), 0x00020000);
+  const int voa = ((lane / UA) * a.A + 4 * (lane % UA)) * 4;
+  const int vov = ((lane / UV) * a.Vd + 4 * (lane % UV)) * 4;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 cmx[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) cmx[c] = z4;
+
+  // utterance u of this wave in batch j: row 32 (blockIdx.x + gridDim.x j) + 4 wave + u
+  auto row_of = [&](int64_t j, int u) -> int64_t {
+    return kNFRows * (static_cast<int64_t>(blockIdx.x) + static_cast<int64_t>(gridDim.x) * j) +
+           kNFPerWave * wave + u;
+  };
+  auto ld_id = [&](int64_t i) -> int { return (i < a.N && lane < L) ? a.ids[i * L + lane] : -1; };
+  auto resolve = [&](int raw, int& rid, float& w, int& hs) {
+    rid = -1;
+    w = 0.f;
+    hs = 0;
+    if (lane < L) {
+      int64_t id = raw;
+      const bool in = id >= 0 && id < a.V;
+      w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                        wrsrc, in ? static_cast<int>(id) * 4 : static_cast<int>(a.V * 4), 0, 0));
+      if (id < 0) id += a.V;
+      if (id < 0 || id >= a.V) {
+        if (a.flag) atomicOr(a.flag, MMB_FLAG_ID_RANGE);
+      } else {
+        rid = static_cast<int>(id);
+        hs = __builtin_amdgcn_raw_buffer_load_b32(hrsrc, rid * 4, 0, 0);
+      }
+    }
+  };
+
+  int rid_n, hs_n, raw = -1;
+  float w_n;
+  resolve(ld_id(row_of(0, 0)), rid_n, w_n, hs_n);
+  __syncthreads();  // hot rows in LDS
+  for (int64_t j = 0; j < f.nb; j += 1) {
+    if (blockIdx.x + static_cast<int64_t>(gridDim.x) * j >= f.nb) break;
+    // ------------------------------------------------------------ stream phase
+    for (int u = 0; u < kNFPerWave; ++u) {
+      const int64_t i = row_of(j, u);
+      const int r = kNFPerWave * wave + u;  // row in the batch
+      const bool live = i < a.N;
+      const int rid = rid_n, hs = hs_n;
+      const float w = w_n;
+      const int64_t inext = u + 1 < kNFPerWave ? row_of(j, u + 1) : row_of(j + 1, 0);
+      raw = ld_id(inext);
+      const int64_t ic = live ? i : 0;
+      const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.audio + ic * L * a.A), 0,
+                                                           live ? L * a.A * 4 : 0, 0x00020000);
+      const auto vrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.visual + ic * L * a.Vd), 0,
+                                                           live ? L * a.Vd * 4 : 0, 0x00020000);
+      float4 sa = z4, saa = z4, sv = z4, svv = z4;
+      auto frames = [&](auto gmax, auto rsrc, int vo, int W, int U, int P, int g0, float4& s1, float4& s2) {
+        constexpr int GM = decltype(gmax)::value;
+        float4 v[GM];
+#pragma unroll
+        for (int g = 0; g < GM; ++g)
+          v[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, (g0 + g) * P * W * 4, 2));
+        const bool mine = lane < P * U;
+        return [=, &s1, &s2]() {
+#pragma unroll
+          for (int g = 0; g < GM; ++g) {
+            if (mine) {
+              add4(s1, v[g]);
+              sq4(s2, v[g]);
+            }
+          }
+        };
+      };
+      using GAc = std::integral_constant<int, GA_MAX>;
+      using GVc = std::integral_constant<int, GV_MAX>;
+      auto acc_a = frames(GAc{}, arsrc, voa, a.A, UA, PA, 0, sa, saa);
+      auto acc_v = frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, 0, sv, svv);
+
+      // text: utt_narrow_kernel's x sums (same operations, same order) and
+      // the P rows of the text term; hot words from LDS
+      float4 num[CT], tp[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) num[c] = tp[c] = z4;
+      auto row = [&](int t, float4 (&ve)[CT], float4 (&vq)[CT]) {
+        const int rr = __builtin_amdgcn_readlane(rid, t);
+        const int hh = __builtin_amdgcn_readlane(hs, t);
+        if (hh > 0) {
+          const float* he = hotE + (hh - 1) * 300;
+          const float* hp = hotP + (hh - 1) * kNFLdp;
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            ve[c] = *reinterpret_cast<const float4*>(he + (vt[c] >> 2));
+            vq[c] = *reinterpret_cast<const float4*>(hp + (vp[c] >> 2));
+          }
+        } else {
+          const int so = rr >= 0 ? rr * D * 4 : tbytes;
+          const int sp = rr >= 0 ? rr * kNFLdp * 4 : pbytes;
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            ve[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
+            vq[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, vp[c], sp, 0));
+          }
+        }
+      };
+      auto accum = [&](int t, const float4 (&ve)[CT], const float4 (&vq)[CT]) {
+        const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          fma4(num[c], wt, ve[c]);
+          add4(tp[c], vq[c]);
+        }
+      };
+      int t = 0;
+      for (; t + UNR <= L; t += UNR) {
+        float4 ve[UNR][CT], vq[UNR][CT];
+#pragma unroll
+        for (int q = 0; q < UNR; ++q) row(t + q, ve[q], vq[q]);
+#pragma unroll
+        for (int q = 0; q < UNR; ++q) accum(t + q, ve[q], vq[q]);
+      }
+      for (; t < L; ++t) {
+        float4 ve[CT], vq[CT];
+        row(t, ve, vq);
+        accum(t, ve, vq);
+      }
+      acc_a();
+      acc_v();
+      const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+      const float sw = wave_sum(w);
+      if (live && lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+      for (int g0 = GA_MAX; g0 < GA; g0 += GA_MAX) frames(GAc{}, arsrc, voa, a.A, UA, PA, g0, sa, saa)();
+      for (int g0 = GV_MAX; g0 < GV; g0 += GV_MAX) frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, g0, sv, svv)();
+      auto slots = [&](float4& acc, int U, int P) {
+        float4 rs = acc;
+        for (int q = 1; q < P; ++q) {
+          const int src = min(lane + q * U, kWave - 1);
+          float4 o;
+          o.x = __shfl(acc.x, src, kWave);
+          o.y = __shfl(acc.y, src, kWave);
+          o.z = __shfl(acc.z, src, kWave);
+          o.w = __shfl(acc.w, src, kWave);
+          add4(rs, o);
+        }
+        acc = rs;
+      };
+      slots(sa, UA, PA);
+      slots(saa, UA, PA);
+      slots(sv, UV, PV);
+      slots(svv, UV, PV);
+      if (lane >= UA) sa = saa = z4;
+      if (lane >= UV) sv = svv = z4;
+      const float m = fmaxf(fmaxf(amax4(sa), amax4(saa)), fmaxf(amax4(sv), amax4(svv)));
+      const float rsc = row_scale(wave_max(m));
+      resolve(raw, rid_n, w_n, hs_n);  // the next utterance's
+      // x (the a2 row), column bounds, aux; the text term T into LDS
+      float* trow = sT + r * kNFLdp;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int uu = lane + kWave * c;
+        if (uu < UT) {
+          const float4 xr = div4(num[c], cnt);
+          if (live) {
+            st4(a.num_out + i * D + 4 * uu, xr);
+            cmx[c] = bmax4(cmx[c], xr);
+          }
+          float4 tv = num[c];
+          add4(tv, tp[c]);
+          *reinterpret_cast<float4*>(trow + 4 * uu) = tv;
+        } else if (uu < kNFLdp / 4) {  // column D: the total weight sum w + sum P[D]; pads 0
+          const float add = uu == UT ? sw : 0.f;
+          const bool held = uu < UP;
+          *reinterpret_cast<float4*>(trow + 4 * uu) =
+              make_float4(held ? tp[c].x + add : 0.f, held ? tp[c].y : 0.f, held ? tp[c].z : 0.f,
+                          held ? tp[c].w : 0.f);
+        }
+      }
+      // [Sa | Saa | 0 | Sv | Svv] as fp16 hi | lo, row-scaled, swizzled per row
+      {
+        _Float16* arow = sA + r * 2 * kNFK;
+        const int q = r & 15;
+        auto put = [&](int k, float4 v) {  // 4 consecutive K at k (k % 4 == 0)
+          const int grp = k >> 3, o = ((grp ^ q) << 3) + (k & 7);
+          split_store4(arow + o, arow + kNFK + o, v, rsc);
+        };
+        for (int k = 4 * lane; k < kNFK; k += 4 * kWave) put(k, z4);  // zero the row (pads)
+        __builtin_amdgcn_wave_barrier();
+        if (lane < UA) {
+          put(4 * lane, sa);
+          put(a.A + 4 * lane, saa);
+        }
+        if (lane < UV) {
+          put(f.kq_a + 4 * lane, sv);
+          put(f.kq_a + a.Vd + 4 * lane, svv);
+        }
+      }
+      if (lane == 0) {
+        s_irs[r] = 1.f / rsc;
+        s_cnt[r] = cnt;
+        s_ok[r] = live ? 1.f : 0.f;
+        if (live) {
+          a.aux_out[i] = cnt;
+          a.aux_out[a.N + i] = sw;
+          a.aux_out[2 * a.N + i] = rsc;
+        }
+      }
+    }
+    __syncthreads();
+    // ------------------------------------------------------------ MFMA phase
+    {
+      const int q = lane & 15, g = lane >> 4;
+      constexpr int CH = 2 * kNFLdw * 32, PL = kNFLdw * 32;  // image chunk / plane (halves)
+      const int nch = (f.kq_a + f.kq_v) / 32;
+      const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.img), 0,
+                                                           (f.cb_av + nch) * CH * 2, 0x00020000);
+      // this wave's column tiles: wave, wave + 8, wave + 16 (< 20)
+      constexpr int kMaxT = (kNFCT + kNFWaves - 1) / kNFWaves;  // 3
+      f32x4 acc[2][kMaxT];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int tt = 0; tt < kMaxT; ++tt) acc[rt][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      int boff[kMaxT];
+#pragma unroll
+      for (int tt = 0; tt < kMaxT; ++tt) {
+        const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+        boff[tt] = col * 32 + ((g ^ x3_swz(col)) << 3);
+      }
+      const int ntt = wave + kNFWaves * 2 < kNFCT ? 3 : 2;
+      for (int c = 0; c < nch; ++c) {
+        const int so = (f.cb_av + c) * CH * 2;
+        half8 bh[kMaxT], bl[kMaxT];
+#pragma unroll
+        for (int tt = 0; tt < kMaxT; ++tt) {
+          if (tt < ntt) {
+            bh[tt] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[tt] * 2, so, 0));
+            bl[tt] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (boff[tt] + PL) * 2, so, 0));
+          }
+        }
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          const int rr = 16 * rt + q;
+          const int o = (((4 * c + g) ^ q) << 3);
+          const half8 ah = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + o);
+          const half8 al = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + kNFK + o);
+#pragma unroll
+          for (int tt = 0; tt < kMaxT; ++tt) {
+            if (tt < ntt) {
+              acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[tt], acc[rt][tt], 0, 0, 0);
+              acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[tt], acc[rt][tt], 0, 0, 0);
+              acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[tt], acc[rt][tt], 0, 0, 0);
+            }
+          }
+        }
+      }
+      // y = acc * (col scale * row scale) + T + c0, in place in the T rows
+      // (lane value (rt, tt, jj): row 16 rt + 4 g + jj, column 16 ct + q)
+#pragma unroll
+      for (int tt = 0; tt < kMaxT; ++tt) {
+        if (tt < ntt) {
+          const int col = 16 * (wave + kNFWaves * tt) + q;
+          if (col < kNFLdp) {
+            const float ci = f.col_inv[col], cc = f.c0[col];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                const int rr = 16 * rt + 4 * g + jj;
+                float* tp = sT + rr * kNFLdp + col;
+                *tp = acc[rt][tt][jj] * (ci * s_irs[rr]) + *tp + cc;
+              }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ------------------------------------------------------------ epilogue
+    // wave w finishes rows 4 w .. 4 w + 3: / total (column D), L2 norm, store
+#pragma unroll
+    for (int u = 0; u < kNFPerWave; ++u) {
+      const int r = kNFPerWave * wave + u;
+      const int64_t i = row_of(j, u);
+      const float* trow = sT + r * kNFLdp;
+      const float rt = 1.f / trow[D];
+      float4 y[CT];
+      float ss = 0.f;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int uu = lane + kWave * c;
+        y[c] = *reinterpret_cast<const float4*>(trow + 4 * min(uu, UT - 1));
+        y[c] = make_float4(y[c].x * rt, y[c].y * rt, y[c].z * rt, y[c].w * rt);
+        if (uu < UT) ss += y[c].x * y[c].x + y[c].y * y[c].y + y[c].z * y[c].z + y[c].w * y[c].w;
+      }
+      const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
+      if (s_ok[r] != 0.f) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const int uu = lane + kWave * c;
+          if (uu < UT) st4(f.out + i * D + 4 * uu, make_float4(y[c].x * inv, y[c].y * inv, y[c].z * inv, y[c].w * inv));
+        }
+      }
+    }
+    __syncthreads();  // the T / A rows are rewritten by the next batch
+  }
+  if (a.cmax_part) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int uu = lane + kWave * c;
+      if (uu < UT) st4(a.cmax_part + wid * D + 4 * uu, cmx[c]);
+    }
+  }
+}
+
+// the narrow fused kernel's shapes: gathered ids, a weight table, 256 < d <
+// 304 (d % 4), frame rows of 4..128 floats (two or more per instruction,
+// A % 4 == Vd % 4 == 0), kq(A) + kq(Vd) <= 256, t <= 64, V <= 16384 (the
+// text cache)
+extern "C" int mmb_mm2_stream_project_narrow_supported(int t, int d, int a_, int vd, int64_t v) {
+  const int kq = (2 * a_ + 31) / 32 * 32 + (2 * vd + 31) / 32 * 32;
+  return t > 0 && t <= kWave && d > 256 && d < kNFLdp && d % 4 == 0 && a_ >= 4 && vd >= 4 &&
+         a_ <= 128 && vd <= 128 && a_ % 4 == 0 && vd % 4 == 0 && kq <= kNFK && v > 0 && v <= 16384 &&
+         v * kNFLdp * 4 < (int64_t{1} << 31) && static_cast<int64_t>(t) * (a_ > vd ? a_ : vd) * 4 < (int64_t{1} << 31);
+}
+
+extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* table, int64_t v,
+                                             const float* wtab32, const void* text_cache,
+                                             const float* audio, const float* visual, int64_t n,
+                                             int t, int d, int a_, int vd, const void* wpieces,
+                                             const float* c0, float* num_out, float* aux_out,
+                                             float* mmb2_out, int32_t* flag, uint32_t* colmax,
+                                             void* colmax_ws, hipStream_t stream) {
+  MMB_REQUIRE(n >= 0 && mmb_mm2_stream_project_narrow_supported(t, d, a_, vd, v));
+  MMB_REQUIRE(ids && table && wtab32 && text_cache && audio && visual && num_out && aux_out &&
+              mmb2_out && wpieces && c0);
+  MMB_REQUIRE(colmax == nullptr || colmax_ws != nullptr);
+  MMB_REQUIRE(aligned16(table) && aligned16(text_cache) && aligned16(audio) && aligned16(visual) &&
+              aligned16(num_out) && aligned16(mmb2_out) && aligned16(wpieces));
+  if (n == 0) {
+    if (colmax) {
+      const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return MMB_OK;
+  }
+  NarrowFusedArgs f{};
+  StreamArgs& s = f.s;
+  s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.audio = audio; s.visual = visual;
+  s.N = n; s.L = t; s.D = d; s.A = a_; s.Vd = vd; s.Kp = mmb_mm2_k(d, a_, vd);
+  s.num_out = num_out; s.aux_out = aux_out; s.flag = flag; s.s_half = 1;
+  s.cmax_part = colmax ? static_cast<float*>(colmax_ws) : nullptr;
+  f.ptab = static_cast<const float*>(text_cache);
+  f.hot_slot1 = reinterpret_cast<const int32_t*>(f.ptab + static_cast<size_t>(v) * kNFLdp);
+  f.hot_ids = f.hot_slot1 + v;
+  f.n_hot = static_cast<int>(v < kNFHot ? v : kNFHot);
+  const int kq_t = (2 * d + 31) / 32 * 32;
+  f.kq_a = (2 * a_ + 31) / 32 * 32;
+  f.kq_v = (2 * vd + 31) / 32 * 32;
+  f.cb_av = kq_t / 32;
+  f.img = static_cast<const _Float16*>(wpieces);
+  f.col_inv = reinterpret_cast<const float*>(f.img + 2 * static_cast<size_t>(kNFLdw) * (kq_t + f.kq_a + f.kq_v));
+  f.c0 = c0;
+  f.out = mmb2_out;
+  f.nb = ceil_div(n, kNFRows);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<4, 7, 4>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
+    attr = true;
+  }
+  int64_t grid = stream_cu_count(stream);
+  if (colmax && grid > kCmaxRows / kNFWaves) grid = kCmaxRows / kNFWaves;
+  if (grid > f.nb) grid = f.nb;
+  utt_narrow_fused_kernel<4, 7, 4><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
+  MMB_LAUNCH_CHECK();
+  if (!colmax) return MMB_OK;
+  colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(
+      static_cast<const float*>(colmax_ws), static_cast<int>(grid) * kNFWaves, d, colmax);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}

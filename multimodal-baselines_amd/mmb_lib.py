@@ -68,6 +68,11 @@ SIGNATURES = {
     "mmb_mm2_stream_project": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P,
                                     _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mm2_prepare": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
+    "mmb_mm2_text_cache_bytes": (_S, [_L, _I]),
+    "mmb_mm2_text_cache": (_I, [_P, _L, _I, _P, _P, _I, _P, _P]),
+    "mmb_mm2_stream_project_narrow_supported": (_I, [_I, _I, _I, _I, _L]),
+    "mmb_mm2_stream_project_narrow": (_I, [_P, _P, _L, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P,
+                                           _P, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mm2_split_bytes": (_S, [_I, _I, _I]),
     "mmb_mm2_split_pieces_bytes": (_S, [_I, _I, _I]),
     "mmb_mm2_split_pieces": (_I, [_P, _I, _I, _I, _I, _P, _P]),

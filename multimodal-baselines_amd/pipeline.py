@@ -367,7 +367,11 @@ class MMB2Projection:
     def _versions(self):
         # storage address + version counter of every parameter: an optimiser
         # step (in place) bumps the counter, `p.data = t` moves the address
-        return tuple((t.data_ptr(), t._version) for ps in self._live() for t in ps)
+        # (and of the word / weight tables behind the text cache)
+        live = [t for ps in self._live() for t in ps]
+        if getattr(self, "text_src", None) is not None:
+            live += list(self.text_src)
+        return tuple((t.data_ptr(), t._version) for t in live)
 
     def invalidate(self):
         """Force a re-merge at the next refresh_if_changed(): needed after
@@ -384,7 +388,29 @@ class MMB2Projection:
         if getattr(self, "wpieces", None) is not None:
             L.call("mmb_mm2_split_pieces", L.ptr(self.wm), self.d, self.a, self.vd, self.ldw,
                    L.ptr(self.wpieces), L.stream_ptr())
+        if getattr(self, "text_cache", None) is not None:
+            self._build_text_cache()
         self._seen = self._versions()
+
+    def enable_text_cache(self, table: torch.Tensor, wtab32: torch.Tensor):
+        """Also keep the text cache of the narrow fused step
+        (mmb_mm2_text_cache: P = E Wm_t1 + E^2 Wm_t2 per word, f64 rounded
+        once, and the hot-word ranks), rebuilt with every re-merge and when
+        the word or weight table changes."""
+        if getattr(self, "text_cache", None) is None or self.text_src[0] is not table:
+            self.enable_pieces()
+            V = table.shape[0]
+            nbytes = L.query("mmb_mm2_text_cache_bytes", V, self.d)
+            self.text_cache = torch.empty((nbytes + 15) // 16 * 16, dtype=torch.uint8,
+                                          device=table.device)
+            self.text_src = (table, wtab32)
+            self._build_text_cache()
+            self._seen = self._versions()
+
+    def _build_text_cache(self):
+        table, wtab32 = self.text_src
+        L.call("mmb_mm2_text_cache", L.ptr(table), table.shape[0], self.d, L.ptr(wtab32),
+               L.ptr(self.wm), self.ldw, L.ptr(self.text_cache), L.stream_ptr())
 
     def enable_pieces(self):
         """Also keep the piece-ordered split of wm (mmb_mm2_split_pieces), the
@@ -462,6 +488,31 @@ def stream_project_supported(t: int, d: int, a: int, vd: int) -> bool:
     """Shapes the fused stream + projection kernel takes (t <= 64 frames,
     256 <= d < 320, widths % 4, k <= 1920): the bench / MOSI-like configs."""
     return bool(L.query("mmb_mm2_stream_project_supported", t, d, a, vd))
+
+
+def narrow_fused_supported(t: int, d: int, a: int, vd: int, v: int) -> bool:
+    """Shapes of the narrow fused kernel (mmb_mm2_stream_project_narrow):
+    MOSI-like frame widths (4..128, kq(A) + kq(Vd) <= 256), 256 < d < 304,
+    t <= 64, a word table of <= 16384 rows (its text cache)."""
+    return bool(L.query("mmb_mm2_stream_project_narrow_supported", t, d, a, vd, v))
+
+
+def mm2_stream_project_narrow(n, t, d, a, vd, audio, visual, proj: "MMB2Projection", ids32,
+                              table, wtab32, flag=None, out=None, colmax=None, colmax_ws=None):
+    """a1-a8 at narrow frame widths in ONE kernel (mmb_mm2_stream_project_narrow):
+    x, aux, the MMB2 rows (and the column bounds).  Returns (x, aux, mmb2)."""
+    dev = audio.device
+    if out is None:
+        out = (torch.empty((n, d), dtype=torch.float32, device=dev),
+               torch.empty((3, n), dtype=torch.float32, device=dev),
+               torch.empty((n, d), dtype=torch.float32, device=dev))
+    num, aux, mmb2 = out
+    proj.enable_text_cache(table, wtab32)
+    L.call("mmb_mm2_stream_project_narrow", L.ptr(ids32), L.ptr(table), table.shape[0],
+           L.ptr(wtab32), L.ptr(proj.text_cache), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
+           L.ptr(proj.wpieces), L.ptr(proj.c0), L.ptr(num), L.ptr(aux), L.ptr(mmb2), L.ptr(flag),
+           L.ptr(colmax), L.ptr(colmax_ws), L.stream_ptr())
+    return num, aux, mmb2
 
 
 def mm2_stream_project(n, t, d, a, vd, audio, visual, proj: "MMB2Projection", ids32=None,
@@ -620,7 +671,7 @@ class FusedStep:
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
                  side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True,
                  gram_kind: str | None = None, stream_project: bool | None = None,
-                 check_each_run: bool = False):
+                 narrow_fused: bool | None = None, check_each_run: bool = False):
         self.inp = inputs
         self.check_each_run = check_each_run
         self.ids = inputs["ids"]
@@ -642,9 +693,21 @@ class FusedStep:
             stream_project = fused_pays(self.a, self.vd) if env is None else env != "0"
         self.stream_project = (bool(stream_project) and (chunks or 1) == 1 and self.s_half
                                and stream_project_supported(self.t, self.d, self.a, self.vd))
-        self.s = None if self.stream_project else s_buffer(self.n, kp, self.s_half, dev)
+        # narrow frame widths (MOSI): stream and projection in ONE kernel with
+        # the per-word text cache (mmb_mm2_stream_project_narrow), one chunk;
+        # MMB_NARROW_FUSED=0 / 1 forces the two kernels / the fused one
+        if narrow_fused is None:
+            env = os.environ.get("MMB_NARROW_FUSED")
+            narrow_fused = True if env is None else env != "0"
+        self.narrow_fused = (bool(narrow_fused) and not self.stream_project and (chunks or 1) == 1
+                             and self.s_half
+                             and narrow_fused_supported(self.t, self.d, self.a, self.vd, self.V))
+        self.s = (None if (self.stream_project or self.narrow_fused)
+                  else s_buffer(self.n, kp, self.s_half, dev))
         if self.stream_project:
             self.proj.enable_pieces()
+        if self.narrow_fused:
+            self.proj.enable_text_cache(self.table, inputs["wtab"])
         self.G = torch.empty((self.d, self.d), dtype=torch.float64, device=dev)
         self.pc_buf = torch.empty((npc, self.d), dtype=torch.float64, device=dev)
         self.solve_ws = (torch.zeros(L.query("mmb_pc_solve_mc_ws_bytes", self.d), dtype=torch.uint8,
@@ -669,7 +732,8 @@ class FusedStep:
         # aux is planar per chunk: chunk [r0, r1) owns flat[3 r0 : 3 r1] as [3][r1 - r0]
         self.aux_flat = torch.empty((3 * self.n,), dtype=torch.float32, device=dev)
         self.gram_parts = len(self.bounds) > 1 and self.d % 4 == 0 and self.d <= 320
-        self.fused_remove = fuse_remove and len(self.bounds) == 1 and npc == 1 and self.s_half
+        self.fused_remove = (fuse_remove and len(self.bounds) == 1 and npc == 1 and self.s_half
+                             and not self.narrow_fused)
         # Gram of the one-chunk step: "i8" (mmb_gram_i8, int8 digits of the
         # column-bounded fixed-point x, ~1e-10 of exact; the bounds come from
         # the stream kernel) or "f64" (mmb_gram, exact f64 products).
@@ -802,6 +866,24 @@ class FusedStep:
         nb = len(self.bounds)
         with mark("mm2_prepare"):
             self.proj.refresh_if_changed()
+        if self.narrow_fused:
+            inp = self.inp
+            with mark("mm2_stream_project_narrow"):
+                mm2_stream_project_narrow(self.n, self.t, self.d, self.a, self.vd, inp["audio"],
+                                          inp["visual"], self.proj, self.ids, self.table,
+                                          inp["wtab"], flag=self.flag,
+                                          out=(self.x, self.aux_of(0), self.mmb2),
+                                          colmax=self.colmax, colmax_ws=self.colmax_ws)
+            with mark("gram"):
+                if self.gram_i8:
+                    gram_i8(self.x, self.colmax, self.G, ws=self.gws)
+                else:
+                    gram(self.x, None, self.G, ws=self.gws)
+            pc = self._solve(trace, mark)
+            with mark("pc_remove"):
+                remove_pc(self.x, None, pc, out=self.sif)
+            self.pc = pc
+            return self.sif, self.mmb2
         if self.stream_project:
             inp = self.inp
             with mark("mm2_stream_project"):

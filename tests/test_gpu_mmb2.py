@@ -123,6 +123,12 @@ def test_compensated_arithmetic_vs_reference_fp32(gpu, golden, case):
     e_p32 = _row_errs(p32.astype(np.float64), ref64).max()
     assert e_drop <= FP32_RATIO * e_ref and e_fused <= FP32_RATIO * e_ref, (e_drop, e_fused, e_ref)
     assert max(e_drop, e_fused) <= 1.1 * e_p32, (e_drop, e_fused, e_p32)
+    if P.narrow_fused_supported(t, 300, A, Vd, E.shape[0]):
+        # the narrow fused step (per-word text projection, f64-rounded P rows)
+        nf = P.FusedStep(inputs, gen.to(gpu).networks())
+        assert nf.narrow_fused
+        e_nf = _row_errs(nf.run(check=True)[1].cpu().numpy().astype(np.float64), ref64).max()
+        assert e_nf <= FP32_RATIO * e_ref, (e_nf, e_ref)
 
 
 def test_compensated_arithmetic_vs_fp32_on_config3_sample(gpu):
@@ -660,10 +666,11 @@ def test_stream_project_repeatable_and_unit_rows(gpu):
     assert (norms - 1).abs().max().item() < 1e-5
 
 
-def test_default_step_at_mosi_widths_is_two_kernel(gpu):
-    """configs[1] frame widths (COVAREP 76, FACET 48): FusedStep's default is
-    the two-kernel step (pipeline.fused_pays), its rows within the bar of the
-    CPU oracle (SIF) and of the reference's gpu2 restatement (MMB2)."""
+def test_default_step_at_mosi_widths_is_narrow_fused(gpu):
+    """configs[1] frame widths (COVAREP 76, FACET 48, V = 3016): FusedStep's
+    default is the narrow fused kernel (r04; the wide-frame fused kernel does
+    not pay here, pipeline.fused_pays), its rows within the bar of the CPU
+    oracle (SIF) and of the reference's gpu2 restatement (MMB2)."""
     from oracle import sif_oracle as O
 
     N, T, A, Vd, V = 3000, 20, 76, 48, 3016
@@ -671,10 +678,10 @@ def test_default_step_at_mosi_widths_is_two_kernel(gpu):
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
     step = P.FusedStep(inp, gen.networks())
-    assert not step.stream_project and step.s is not None
+    assert not step.stream_project and step.narrow_fused and step.s is None
     trace = {}
     s1, m1 = step.run(trace=trace, check=True)
-    assert "mm2_stream" in trace and "mm2_stream_project" not in trace
+    assert "mm2_stream_project_narrow" in trace and "mm2_stream" not in trace
     E = inp["table"].cpu().numpy()
     wt = inp["wtab"].cpu().numpy().astype(np.float64)
     ids = inp["ids"].cpu().numpy().astype(np.int64)
@@ -849,3 +856,89 @@ def test_step_graph_follows_weight_updates(gpu):
     s2, m2 = fresh.run(check=True)
     assert torch.equal(s1, s2) and torch.equal(m1, m2) and not torch.equal(m0, m1)
     assert torch.equal(s0, s1)
+
+
+@pytest.mark.parametrize("N,T,A,Vd,V", [(3000, 20, 76, 48, 3016), (1, 20, 76, 48, 3016),
+                                        (31, 20, 76, 48, 3016), (1001, 40, 76, 48, 3016),
+                                        (517, 64, 128, 100, 5000), (64, 7, 20, 8, 300),
+                                        (259, 33, 44, 124, 16384), (5, 1, 76, 48, 3016),
+                                        (77, 20, 76, 48, 17)])
+def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
+    """The narrow fused kernel (mmb_mm2_stream_project_narrow: per-word text
+    projection from the text cache, hot words from LDS, 32-utterance batches,
+    the audio / visual GEMM in-launch) against the two-kernel narrow step
+    (utt_narrow_kernel -> HBM s -> mmb_mm2_project_x3) on the same inputs:
+    x, count and weight sum bit-identical (the same text operations in the
+    same order; hot rows are the same bytes), hence the same Gram and PC; the
+    MMB2 rows to f32 rounding (another grouping of the same closed form) and
+    both within the bar of the CPU oracle.  Partial and single-row batches,
+    T from 1 to 64, frame widths 8-128, fewer words than LDS slots (V = 17),
+    the largest cached vocabulary (16384), wrapped negative ids."""
+    from oracle import sif_oracle as O
+
+    rng = np.random.default_rng(N + T)
+    inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=90 + T, device=gpu)
+    if N > 10:
+        r = torch.as_tensor(rng.integers(0, N, 5), device=gpu)
+        inp["ids"][r, 0] = -3  # wraps to V - 3, like numpy fancy indexing
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
+    a = P.FusedStep(inp, gen.networks(), narrow_fused=True)
+    b = P.FusedStep(inp, gen.networks(), narrow_fused=False)
+    assert a.narrow_fused and not b.narrow_fused and a.gram_i8 == b.gram_i8
+    s1, m1 = [t.clone() for t in a.run()]
+    s2, m2 = b.run()
+    torch.cuda.synchronize()
+    assert int(a.flag.item()) == int(b.flag.item()) == 0
+    assert torch.equal(a.x, b.x) and torch.equal(a.aux[:2], b.aux[:2])
+    assert torch.equal(a.G, b.G) and torch.equal(a.pc, b.pc)
+    assert M.row_rel_err(m1.cpu().numpy(), m2.cpu().numpy()) < 2e-6
+    xmax = a.x.abs().max().item()
+    assert (s1 - s2).abs().max().item() <= 1e-6 * xmax
+    norms = torch.linalg.norm(m1.double(), dim=1)
+    assert (norms - 1).abs().max().item() < 1e-5
+    if N == 1:
+        return
+    E = inp["table"].cpu().numpy()
+    wt = inp["wtab"].cpu().numpy().astype(np.float64)
+    ids = inp["ids"].cpu().numpy().astype(np.int64)
+    rows = np.sort(rng.choice(N, min(N, 256), replace=False))
+    assert M.row_rel_err(s1.cpu().numpy(), O.get_sentence_embeddings(E, wt, ids)) < TOL
+    audio, visual = inp["audio"].cpu().numpy()[rows], inp["visual"].cpu().numpy()[rows]
+    idr = ids[rows]
+    sw = np.where(idr >= 0, wt.astype(np.float32)[idr], 0).astype(np.float32)
+    ref = M.estimate_embedding_overall_gpu2(M.concat_inputs(E[idr], audio, visual),
+                                            M.params_from_module(gen.cpu()), sw, E[idr])
+    assert M.row_rel_err(m1.cpu().numpy()[rows], ref) < TOL
+
+
+def test_narrow_fused_column_bounds_flags_and_weight_updates(gpu):
+    """The narrow fused kernel's column bounds (mmb_gram_i8's input) equal the
+    narrow stream kernel's; an out-of-range id is flagged (IndexError from
+    check()); a zero-weight utterance raises ValueError like the reference; a
+    generator update re-merges Wm AND rebuilds the text cache (the replayed
+    rows equal a fresh step's)."""
+    N, T, A, Vd, V = 40_000, 20, 76, 48, 3016
+    inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=95, device=gpu)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
+    a = P.FusedStep(inp, gen.networks(), narrow_fused=True)
+    b = P.FusedStep(inp, gen.networks(), narrow_fused=False)
+    assert a.gram_i8 and b.gram_i8
+    a.run(check=True)
+    b.run(check=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.colmax, b.colmax) and torch.equal(a.G, b.G)
+    with torch.no_grad():
+        gen.embed2out["textaudio"]["mu"].weight.mul_(1.25)
+    _, m1 = [t.clone() for t in a.run(check=True)]
+    _, m2 = P.FusedStep(inp, gen.networks(), narrow_fused=True).run(check=True)
+    assert torch.equal(m1, m2)
+    bad = {k: v.clone() if k == "ids" else v for k, v in inp.items()}
+    bad["ids"][7, 3] = V + 5
+    with pytest.raises(IndexError):
+        P.FusedStep(bad, gen.networks(), narrow_fused=True).run(check=True)
+    zw = {k: v.clone() if k in ("ids", "wtab") else v for k, v in inp.items()}
+    zw["wtab"][zw["ids"][11]] = 0.0  # every token of utterance 11 now weighs 0
+    with pytest.raises(ValueError):
+        P.FusedStep(zw, gen.networks(), narrow_fused=True).run(check=True)
