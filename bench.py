@@ -222,7 +222,10 @@ def run_workload(P, inp, gen, steps, warmup, allreduce=None, world=1, rank=0):
 def stream_phase(phase_ms):
     """The step's dominant (HBM-bound) phase: the fused stream + projection
     kernel, or the stream kernel of the two-kernel step."""
-    return "mm2_stream_project" if "mm2_stream_project" in phase_ms else "mm2_stream"
+    for ph in ("mm2_stream_project", "mm2_stream_project_narrow"):
+        if ph in phase_ms:
+            return ph
+    return "mm2_stream"
 
 
 def stream_roofline(phase_ms, traces, steps, kbytes, U, kernel, traffic_key, T):
@@ -260,6 +263,17 @@ def mfma_rooflines(step, phase_ms, U, D):
             "flop_per_utt": flop, "ms": round(ms, 4),
             "note": "fp16 x3 products issued beside the stream inside one kernel; the kernel is "
                     "HBM-bound, so this is the MFMA work it hides, not a ceiling"}
+    if "mm2_stream_project_narrow" in phase_ms:
+        k_av = 2 * (step.a + step.vd)
+        flop = 3 * 2 * k_av * (D + 1)
+        ms = phase_ms["mm2_stream_project_narrow"]
+        tf = flop * U / (ms / 1e3) / 1e12
+        out["mm2_stream_project_narrow (batch GEMM)"] = {
+            "bound": "hbm / latency (the fused kernel)", "achieved": round(tf, 2),
+            "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(tf / F16_MFMA_PEAK_TFS, 5),
+            "flop_per_utt": flop, "ms": round(ms, 4),
+            "note": "fp16 x3 products of the audio / visual sums (the text rows of the projection "
+                    "are applied per word in the text cache) inside the streaming kernel"}
     proj_ms = phase_ms.get("mm2_project+pc_remove", phase_ms.get("mm2_project+gram"))
     if proj_ms and step.s_half:
         flop = 3 * 2 * k_alg * (D + 1)
@@ -328,8 +342,22 @@ def time_fp32_projection(P, step, reps=3):
             "note": "mmb_mm2_project: fp32-input MFMA (exact f32 products), no fused removal"}
 
 
+def narrow_fused_bytes(L, D, A, Vd):
+    """Algorithmic bytes per utterance of mmb_mm2_stream_project_narrow: ids,
+    gathered weights, text rows AND their text-cache P rows (4 (D + 4) B,
+    L2-resident at MOSI's V), audio and visual frames read; the a2 row, the
+    MMB2 row and aux written -- no frame sums leave the chip."""
+    return 4 * L + 4 * L + 4 * D * L + 4 * (D + 4) * L + 4 * (A + Vd) * L + 4 * D + 4 * D + 12
+
+
 def dominant_kernel(step, T, D, text_rows=None):
     """(algorithmic bytes per utterance, name) of the step's HBM-bound kernel."""
+    if getattr(step, "narrow_fused", False):
+        return (narrow_fused_bytes(T, D, step.a, step.vd),
+                "utt_narrow_fused_kernel (mmb_mm2_stream_project_narrow: 8 waves per CU stream "
+                "32-utterance batches -- packed frame rows, text rows and their per-word "
+                "projections P, the 32 most frequent words from LDS -- then the audio / visual "
+                "fp16 x3 GEMM and the row epilogue in the same launch)")
     if step.stream_project:
         return (fused_kernel_bytes(T, D, step.a, step.vd, text_rows=text_rows),
                 "utt_fused_kernel (mmb_mm2_stream_project: 4 streaming waves, one per "
@@ -629,21 +657,23 @@ def per_rank_steps(P, inp, gen, steps, warmup, sizes):
     return out
 
 
-def table_resident_roofline(roof, kb, U, D, T):
-    """configs[1] (MOSI shape): the 3.6 MB word table is L2 / Infinity-Cache
-    resident (its rows are 24 KB of the 38.7 KB per utterance), so on all
+def table_resident_roofline(roof, kb, U, D, T, narrow_fused=False):
+    """configs[1] (MOSI shape): the 3.6 MB word table (and the narrow fused
+    kernel's 3.7 MB text cache) is L2 / Infinity-Cache resident (its rows are
+    24 KB -- 48 KB with the P rows -- of the bytes per utterance), so on all
     algorithmic bytes the stream kernel runs above the HBM peak.  The HBM
     roofline is restated in place on the bytes HBM must deliver (text rows
     excluded); the all-bytes rate is kept beside it as *_incl_table."""
-    hbm_b = kb - 4 * D * T
+    hbm_b = kb - 4 * D * T - (4 * (D + 4) * T if narrow_fused else 0)
     hbm_ach = hbm_b * U / (roof["avg_launch_ms"] / 1e3) / 1e9
     roof.update({"achieved_incl_table": roof["achieved"], "frac_incl_table": roof["frac"],
                  "algorithmic_bytes_per_utt_incl_table": roof["algorithmic_bytes_per_utt"],
                  "achieved": round(hbm_ach, 1), "frac": round(hbm_ach / HBM_PEAK_GBS, 4),
                  "algorithmic_bytes_per_utt": hbm_b,
                  "bytes_note": "achieved / frac on the HBM bytes (ids, weights, frames read; a2 "
-                               "row, frame sums, aux written); the word-table rows come from "
-                               "L2 / Infinity Cache (*_incl_table counts them)"})
+                               "row and aux written, and the frame sums (two-kernel step) or the "
+                               "MMB2 row (narrow fused kernel)); the word-table and text-cache "
+                               "rows come from L2 / Infinity Cache (*_incl_table counts them)"})
     return roof
 
 
@@ -749,7 +779,7 @@ def mosi_mmb2_config(P, models, synth, dev, steps, warmup, U=1_000_000):
     kb, kname = dominant_kernel(step, T, D)
     roof = stream_roofline(ph, traces, steps, kb, U, kname + f", T = {T}, A = {A}, Vd = {Vd}",
                            "mosi", T)
-    table_resident_roofline(roof, kb, U, D, T)
+    table_resident_roofline(roof, kb, U, D, T, narrow_fused=step.narrow_fused)
     out = {"workload": f"configs[1] MOSI-shaped: T = {T}, A = {A} (COVAREP 74 + 2 pos), Vd = {Vd} "
                        f"(FACET 46 + 2 pos), V = {V}, Zipf(1.1) ids, U(-1, 1) frames, SIF(+PC "
                        "removal) + closed-form MMB2",
@@ -1130,7 +1160,7 @@ def main():
     kb, kname = dominant_kernel(step, T, D, text_rows=text_rows)
     roof = stream_roofline(phase_ms, traces, args.steps, kb, utts_per_launch, kname, kind, T)
     if kind == "mosi":
-        table_resident_roofline(roof, kb, utts_per_launch, D, T)
+        table_resident_roofline(roof, kb, utts_per_launch, D, T, narrow_fused=step.narrow_fused)
     pb = path_bytes(T, D, A, Vd, text_rows=text_rows)
     mfma = mfma_rooflines(step, phase_ms, U, D)
     wl = {"synthetic": "configs[3]: synthetic utterances x 40 tokens/frames x 3 modalities x "
