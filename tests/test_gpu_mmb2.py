@@ -860,8 +860,8 @@ def test_step_graph_follows_weight_updates(gpu):
 
 @pytest.mark.parametrize("N,T,A,Vd,V", [(3000, 20, 76, 48, 3016), (1, 20, 76, 48, 3016),
                                         (31, 20, 76, 48, 3016), (1001, 40, 76, 48, 3016),
-                                        (517, 64, 128, 100, 5000), (64, 7, 20, 8, 300),
-                                        (259, 33, 44, 124, 16384), (5, 1, 76, 48, 3016),
+                                        (517, 64, 64, 56, 5000), (64, 7, 20, 8, 300),
+                                        (259, 33, 44, 76, 16384), (5, 1, 76, 48, 3016),
                                         (77, 20, 76, 48, 17)])
 def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
     """The narrow fused kernel (mmb_mm2_stream_project_narrow: per-word text
@@ -873,8 +873,13 @@ def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
     MMB2 rows to f32 rounding (another grouping of the same closed form) and
     both within the bar of the CPU oracle.  Partial and single-row batches,
     T from 1 to 64, frame widths 8-128, fewer words than LDS slots (V = 17),
-    the largest cached vocabulary (16384), wrapped negative ids."""
+    the largest cached vocabulary (16384), wrapped negative ids.  (Wider
+    frames -- kq(A) + kq(Vd) > 256 -- and larger vocabularies keep the
+    two-kernel step: narrow_fused_supported.)"""
     from oracle import sif_oracle as O
+
+    assert not P.narrow_fused_supported(T, 300, 128, 100, V)
+    assert not P.narrow_fused_supported(T, 300, A, Vd, 16385)
 
     rng = np.random.default_rng(N + T)
     inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=90 + T, device=gpu)
