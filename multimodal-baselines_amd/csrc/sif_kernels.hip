@@ -965,8 +965,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 // rows of at most 32 units (two or more rows per instruction), T <= 64
 static bool narrow_ok(const StreamArgs& a) {
   return a.ids && a.wtab && !a.w_dense && a.s_half && a.D > 256 && a.D <= 512 &&
-         a.A <= 128 && a.Vd <= 128 && a.L <= kWave && a.V * a.D * 4 < (int64_t{1} << 31) &&
-         a.L * std::max(a.A, a.Vd) * 4 < (int64_t{1} << 31);
+         a.A <= 128 && a.Vd <= 128 && a.L <= kWave && a.V * a.D * 4 < (int64_t{1} << 31);
 }
 
 // colmax[f] = max over the P partial rows (float bits; non-negative floats
@@ -1715,7 +1714,6 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
         constexpr bool TEXT = M == 0;
         const int W = wdt[M], UW = W >> 2;
         const int ngr = (L + UNR - 1) / UNR, ng = nrows * ngr;
-        const float* src = TEXT ? (gather ? a.table : a.text_dense) : (M == 1 ? a.audio : a.visual);
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         const bool has_next = M < 2 || nnr > 0;
         if constexpr (M == 2) {
@@ -2581,6 +2579,16 @@ extern "C" int mmb_diag_fused_probe(unsigned long long* host_out, int* rate_khz)
 //     the division by the total weight (column D) and the L2 norm, the MMB2
 //     row written with 16-byte stores.
 // LDS: hot E rows 38.4 KB + hot P rows 38.9 KB + T 38.9 KB + A 32 KB.
+#ifndef NF_UNR
+#define NF_UNR 3
+#endif
+#ifndef NF_HU
+#define NF_HU 1
+#endif
+#ifndef NF_ABL  // timing-only ablations (tools/ab_libs): 1 no MFMA, 2 no frames, 4 no text,
+                // 8 no a2 / aux stores, 16 no MMB2 stores, 32 no id / weight loads
+#define NF_ABL 0
+#endif
 constexpr int kNFThreads = 512;
 constexpr int kNFWaves = kNFThreads / kWave;
 constexpr int kNFRows = 32;                 // utterances per batch
@@ -2589,7 +2597,7 @@ constexpr int kNFHot = 32;                  // = mm2_kernels.hip kTextHot
 constexpr int kNFLdp = 304;                 // = kTextLdp (P row stride, floats)
 constexpr int kNFK = 256;                   // K of the audio / visual GEMM (max)
 constexpr int kNFLdw = 320;                 // projection columns
-constexpr int kNFCT = kNFLdw / 16;          // 16-column tiles (20)
+constexpr int kNFCT = kNFLdp / 16;          // 16-column tiles of y and the total (19)
 constexpr size_t kNFLds = sizeof(float) * (kNFHot * 300 + kNFHot * kNFLdp + kNFRows * kNFLdp) +
                           sizeof(_Float16) * kNFRows * 2 * kNFK + sizeof(float) * 3 * kNFRows;
 
@@ -2608,7 +2616,7 @@ struct NarrowFusedArgs {
   int64_t nb;                // batches
 };
 
-template <int UNR, int GA_MAX, int GV_MAX>
+template <int UNR, int HU, int GA_MAX, int GV_MAX>
 __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_narrow_fused_kernel(
     NarrowFusedArgs f) {
   extern __shared__ __attribute__((aligned(16))) float nf_lds[];
@@ -2669,12 +2677,17 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     return kNFRows * (static_cast<int64_t>(blockIdx.x) + static_cast<int64_t>(gridDim.x) * j) +
            kNFPerWave * wave + u;
   };
-  auto ld_id = [&](int64_t i) -> int { return (i < a.N && lane < L) ? a.ids[i * L + lane] : -1; };
+  auto ld_id = [&](int64_t i) -> int {
+    if (NF_ABL & 32) return (i < a.N && lane < L) ? static_cast<int>((lane * 131 + i) % a.V) : -1;
+    return (i < a.N && lane < L) ? a.ids[i * L + lane] : -1;
+  };
   auto resolve = [&](int raw, int& rid, float& w, int& hs) {
     rid = -1;
     w = 0.f;
     hs = 0;
-    if (lane < L) {
+    if (NF_ABL & 32) {
+      if (raw >= 0) rid = raw, w = 1.f;
+    } else if (lane < L) {
       int64_t id = raw;
       const bool in = id >= 0 && id < a.V;
       w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
@@ -2689,7 +2702,56 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     }
   };
 
-  int rid_n, hs_n, raw = -1;
+  // MFMA phase: this wave's column tiles wave, wave + 8, wave + 16 (< 20);
+  // lane (q, g) holds row / column q, K group g of a 16 x 32 fragment
+  const int q = lane & 15, g = lane >> 4;
+  constexpr int CH = 2 * kNFLdw * 32, PL = kNFLdw * 32;  // image chunk / plane (halves)
+  constexpr int kMaxT = (kNFCT + kNFWaves - 1) / kNFWaves;  // 3
+  const int nch = (f.kq_a + f.kq_v) / 32;
+  const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.img), 0,
+                                                       (f.cb_av + nch) * CH * 2, 0x00020000);
+  int boff[kMaxT];
+#pragma unroll
+  for (int tt = 0; tt < kMaxT; ++tt) {
+    const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+    boff[tt] = col * 32 + ((g ^ x3_swz(col)) << 3);
+  }
+  const int ntt = wave + kNFWaves * 2 < kNFCT ? 3 : 2;
+  float cinv[kMaxT], cc0[kMaxT];  // the tiles' column scales and c0
+#pragma unroll
+  for (int tt = 0; tt < kMaxT; ++tt) {
+    const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+    const bool held = tt < ntt && col < kNFLdp;
+    cinv[tt] = held ? f.col_inv[col] : 0.f;
+    cc0[tt] = held ? f.c0[col] : 0.f;
+  }
+  auto ld_b = [&](int c, half8 (&bh)[kMaxT], half8 (&bl)[kMaxT]) {
+    const int so = (f.cb_av + c) * CH * 2;
+#pragma unroll
+    for (int tt = 0; tt < kMaxT; ++tt) {
+      if (tt < ntt) {
+        bh[tt] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[tt] * 2, so, 0));
+        bl[tt] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (boff[tt] + PL) * 2, so, 0));
+      }
+    }
+  };
+
+  auto frame_rsrc = [&](int64_t i, const float* base, int W) {
+    const bool live = i < a.N;
+    const int64_t ic = live ? i : 0;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + ic * L * W), 0, live ? L * W * 4 : 0,
+                                             0x00020000);
+  };
+  auto take = [](uint64_t& m) -> int {  // next token of a (uniform) mask, -1 = none
+    const int t = m ? __builtin_ctzll(m) : -1;
+    m &= m - 1;
+    return t;
+  };
+
+  // the A rows' pads (K past each piece) stay zero: zeroed once here
+  for (int e = tid; e < kNFRows * 2 * kNFK / 8; e += kNFThreads)
+    reinterpret_cast<float4*>(sA)[e] = z4;
+  int rid_n, hs_n, raw = -1;  // the next utterance's ids, weights, hot slots
   float w_n;
   resolve(ld_id(row_of(0, 0)), rid_n, w_n, hs_n);
   __syncthreads();  // hot rows in LDS
@@ -2702,17 +2764,13 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       const bool live = i < a.N;
       const int rid = rid_n, hs = hs_n;
       const float w = w_n;
-      const int64_t inext = u + 1 < kNFPerWave ? row_of(j, u + 1) : row_of(j + 1, 0);
-      raw = ld_id(inext);
-      const int64_t ic = live ? i : 0;
-      const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.audio + ic * L * a.A), 0,
-                                                           live ? L * a.A * 4 : 0, 0x00020000);
-      const auto vrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.visual + ic * L * a.Vd), 0,
-                                                           live ? L * a.Vd * 4 : 0, 0x00020000);
+      raw = ld_id(u + 1 < kNFPerWave ? row_of(j, u + 1) : row_of(j + 1, 0));
+      const auto arsrc = frame_rsrc(i, a.audio, a.A);
+      const auto vrsrc = frame_rsrc(i, a.visual, a.Vd);
       float4 sa = z4, saa = z4, sv = z4, svv = z4;
       auto frames = [&](auto gmax, auto rsrc, int vo, int W, int U, int P, int g0, float4& s1, float4& s2) {
         constexpr int GM = decltype(gmax)::value;
-        float4 v[GM];
+        float4 v[GM > 0 ? GM : 1];
 #pragma unroll
         for (int g = 0; g < GM; ++g)
           v[g] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, (g0 + g) * P * W * 4, 2));
@@ -2729,33 +2787,29 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       };
       using GAc = std::integral_constant<int, GA_MAX>;
       using GVc = std::integral_constant<int, GV_MAX>;
-      auto acc_a = frames(GAc{}, arsrc, voa, a.A, UA, PA, 0, sa, saa);
-      auto acc_v = frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, 0, sv, svv);
+      using G0 = std::integral_constant<int, 0>;
+      auto acc_a = frames(std::conditional_t<(NF_ABL & 2) != 0, G0, GAc>{}, arsrc, voa, a.A, UA, PA, 0, sa, saa);
+      auto acc_v = frames(std::conditional_t<(NF_ABL & 2) != 0, G0, GVc>{}, vrsrc, vov, a.Vd, UV, PV, 0, sv, svv);
 
-      // text: utt_narrow_kernel's x sums (same operations, same order) and
-      // the P rows of the text term; hot words from LDS
+      // text: the x sums (w E) and the P rows of the text term over the
+      // utterance's valid tokens -- hot words (LDS) while the first group of
+      // cold words (global loads) is in flight, then the cold groups.  The
+      // order (hot tokens, then cold, each by position) is not
+      // utt_narrow_kernel's: x agrees with it to f32 rounding.
       float4 num[CT], tp[CT];
 #pragma unroll
       for (int c = 0; c < CT; ++c) num[c] = tp[c] = z4;
-      auto row = [&](int t, float4 (&ve)[CT], float4 (&vq)[CT]) {
-        const int rr = __builtin_amdgcn_readlane(rid, t);
-        const int hh = __builtin_amdgcn_readlane(hs, t);
-        if (hh > 0) {
-          const float* he = hotE + (hh - 1) * 300;
-          const float* hp = hotP + (hh - 1) * kNFLdp;
+      const bool tok = lane < L && rid >= 0;
+      uint64_t cold = (NF_ABL & 4) ? 0 : __builtin_amdgcn_ballot_w64(tok && hs == 0);
+      uint64_t hot = (NF_ABL & 4) ? 0 : __builtin_amdgcn_ballot_w64(tok && hs > 0);
+      auto cold_row = [&](int t, float4 (&ve)[CT], float4 (&vq)[CT]) {
+        const int rr = t >= 0 ? __builtin_amdgcn_readlane(rid, t) : -1;
+        const int so = rr >= 0 ? rr * D * 4 : tbytes;  // none: out of range, reads 0
+        const int sp = rr >= 0 ? rr * kNFLdp * 4 : pbytes;
 #pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            ve[c] = *reinterpret_cast<const float4*>(he + (vt[c] >> 2));
-            vq[c] = *reinterpret_cast<const float4*>(hp + (vp[c] >> 2));
-          }
-        } else {
-          const int so = rr >= 0 ? rr * D * 4 : tbytes;
-          const int sp = rr >= 0 ? rr * kNFLdp * 4 : pbytes;
-#pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            ve[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
-            vq[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, vp[c], sp, 0));
-          }
+        for (int c = 0; c < CT; ++c) {
+          ve[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
+          vq[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, vp[c], sp, 0));
         }
       };
       auto accum = [&](int t, const float4 (&ve)[CT], const float4 (&vq)[CT]) {
@@ -2766,22 +2820,48 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
           add4(tp[c], vq[c]);
         }
       };
-      int t = 0;
-      for (; t + UNR <= L; t += UNR) {
+      {
         float4 ve[UNR][CT], vq[UNR][CT];
+        int tq[UNR];
 #pragma unroll
-        for (int q = 0; q < UNR; ++q) row(t + q, ve[q], vq[q]);
+        for (int q = 0; q < UNR; ++q) {
+          tq[q] = take(cold);
+          cold_row(tq[q], ve[q], vq[q]);
+        }
+        while (hot) {
+          float4 he[HU][CT], hq[HU][CT];
+          int th[HU];
 #pragma unroll
-        for (int q = 0; q < UNR; ++q) accum(t + q, ve[q], vq[q]);
+          for (int q = 0; q < HU; ++q) {
+            th[q] = take(hot);
+            const int hh = th[q] >= 0 ? __builtin_amdgcn_readlane(hs, th[q]) - 1 : 0;
+            const float* pe = hotE + hh * 300;
+            const float* pq = hotP + hh * kNFLdp;
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+              he[q][c] = *reinterpret_cast<const float4*>(pe + (vt[c] >> 2));
+              hq[q][c] = *reinterpret_cast<const float4*>(pq + (vp[c] >> 2));
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < HU; ++q)
+            if (th[q] >= 0) accum(th[q], he[q], hq[q]);
+        }
+        acc_a();
+        acc_v();
+        for (;;) {
+#pragma unroll
+          for (int q = 0; q < UNR; ++q)
+            if (tq[q] >= 0) accum(tq[q], ve[q], vq[q]);
+          if (!cold) break;
+#pragma unroll
+          for (int q = 0; q < UNR; ++q) {
+            tq[q] = take(cold);
+            cold_row(tq[q], ve[q], vq[q]);
+          }
+        }
       }
-      for (; t < L; ++t) {
-        float4 ve[CT], vq[CT];
-        row(t, ve, vq);
-        accum(t, ve, vq);
-      }
-      acc_a();
-      acc_v();
-      const float cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
+      const float cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w != 0.f)));
       const float sw = wave_sum(w);
       if (live && lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
       for (int g0 = GA_MAX; g0 < GA; g0 += GA_MAX) frames(GAc{}, arsrc, voa, a.A, UA, PA, g0, sa, saa)();
@@ -2809,14 +2889,15 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       const float rsc = row_scale(wave_max(m));
       resolve(raw, rid_n, w_n, hs_n);  // the next utterance's
       // x (the a2 row), column bounds, aux; the text term T into LDS
+      const float rc = 1.f / cnt;
       float* trow = sT + r * kNFLdp;
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
         const int uu = lane + kWave * c;
         if (uu < UT) {
-          const float4 xr = div4(num[c], cnt);
+          const float4 xr = make_float4(num[c].x * rc, num[c].y * rc, num[c].z * rc, num[c].w * rc);
           if (live) {
-            st4(a.num_out + i * D + 4 * uu, xr);
+            if (!(NF_ABL & 8)) st4(a.num_out + i * D + 4 * uu, xr);
             cmx[c] = bmax4(cmx[c], xr);
           }
           float4 tv = num[c];
@@ -2838,8 +2919,6 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
           const int grp = k >> 3, o = ((grp ^ q) << 3) + (k & 7);
           split_store4(arow + o, arow + kNFK + o, v, rsc);
         };
-        for (int k = 4 * lane; k < kNFK; k += 4 * kWave) put(k, z4);  // zero the row (pads)
-        __builtin_amdgcn_wave_barrier();
         if (lane < UA) {
           put(4 * lane, sa);
           put(a.A + 4 * lane, saa);
@@ -2853,45 +2932,27 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         s_irs[r] = 1.f / rsc;
         s_cnt[r] = cnt;
         s_ok[r] = live ? 1.f : 0.f;
-        if (live) {
+        if (live && !(NF_ABL & 8)) {
           a.aux_out[i] = cnt;
           a.aux_out[a.N + i] = sw;
           a.aux_out[2 * a.N + i] = rsc;
         }
       }
     }
+    // the first image chunk's B fragments load across the barrier
+    half8 bh[kMaxT], bl[kMaxT];
+    ld_b(0, bh, bl);
     __syncthreads();
     // ------------------------------------------------------------ MFMA phase
     {
-      const int q = lane & 15, g = lane >> 4;
-      constexpr int CH = 2 * kNFLdw * 32, PL = kNFLdw * 32;  // image chunk / plane (halves)
-      const int nch = (f.kq_a + f.kq_v) / 32;
-      const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.img), 0,
-                                                           (f.cb_av + nch) * CH * 2, 0x00020000);
-      // this wave's column tiles: wave, wave + 8, wave + 16 (< 20)
-      constexpr int kMaxT = (kNFCT + kNFWaves - 1) / kNFWaves;  // 3
       f32x4 acc[2][kMaxT];
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
         for (int tt = 0; tt < kMaxT; ++tt) acc[rt][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      int boff[kMaxT];
-#pragma unroll
-      for (int tt = 0; tt < kMaxT; ++tt) {
-        const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
-        boff[tt] = col * 32 + ((g ^ x3_swz(col)) << 3);
-      }
-      const int ntt = wave + kNFWaves * 2 < kNFCT ? 3 : 2;
-      for (int c = 0; c < nch; ++c) {
-        const int so = (f.cb_av + c) * CH * 2;
-        half8 bh[kMaxT], bl[kMaxT];
-#pragma unroll
-        for (int tt = 0; tt < kMaxT; ++tt) {
-          if (tt < ntt) {
-            bh[tt] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[tt] * 2, so, 0));
-            bl[tt] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, (boff[tt] + PL) * 2, so, 0));
-          }
-        }
+      for (int c = 0; c < ((NF_ABL & 1) ? 0 : nch); ++c) {
+        half8 nh[kMaxT], nl[kMaxT];  // chunk c + 1, in flight during chunk c
+        if (c + 1 < nch) ld_b(c + 1, nh, nl);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
           const int rr = 16 * rt + q;
@@ -2907,6 +2968,11 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
             }
           }
         }
+#pragma unroll
+        for (int tt = 0; tt < kMaxT; ++tt) {
+          bh[tt] = nh[tt];
+          bl[tt] = nl[tt];
+        }
       }
       // y = acc * (col scale * row scale) + T + c0, in place in the T rows
       // (lane value (rt, tt, jj): row 16 rt + 4 g + jj, column 16 ct + q)
@@ -2915,7 +2981,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         if (tt < ntt) {
           const int col = 16 * (wave + kNFWaves * tt) + q;
           if (col < kNFLdp) {
-            const float ci = f.col_inv[col], cc = f.c0[col];
+            const float ci = cinv[tt], cc = cc0[tt];
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -2947,7 +3013,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         if (uu < UT) ss += y[c].x * y[c].x + y[c].y * y[c].y + y[c].z * y[c].z + y[c].w * y[c].w;
       }
       const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
-      if (s_ok[r] != 0.f) {
+      if (s_ok[r] != 0.f && !(NF_ABL & 16)) {
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
           const int uu = lane + kWave * c;
@@ -3018,14 +3084,14 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   f.nb = ceil_div(n, kNFRows);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<4, 7, 4>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, 7, 4>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
     attr = true;
   }
   int64_t grid = stream_cu_count(stream);
   if (colmax && grid > kCmaxRows / kNFWaves) grid = kCmaxRows / kNFWaves;
   if (grid > f.nb) grid = f.nb;
-  utt_narrow_fused_kernel<4, 7, 4><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
+  utt_narrow_fused_kernel<NF_UNR, NF_HU, 7, 4><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
   MMB_LAUNCH_CHECK();
   if (!colmax) return MMB_OK;
   colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(

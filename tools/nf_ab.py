@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Timing of one build of the narrow fused kernel (mmb_mm2_stream_project_narrow)
+on the MOSI bench workload (1M utterances, T 20, A 76, Vd 48, V 3016): the
+kernel's mean launch time over --steps FusedStep runs, the step time, and the
+a2 rows against the two-kernel step's (row-relative).  One library per
+process (tools/ab_libs/build_nf.sh builds the knob variants):
+
+    python tools/nf_ab.py --lib tools/ab_libs/libmmb_nf_4_1.so
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multimodal-baselines_amd"))
+sys.path.insert(0, ROOT)
+import mmb_lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--check", action="store_true")
+    args = ap.parse_args()
+    mmb_lib.load(os.path.abspath(args.lib))
+    import torch
+    import models
+    import pipeline as P
+    import synth
+    dev = torch.device("cuda:0")
+    inp = synth.device_workload(args.n, 20, 3016, D=300, A=76, Vd=48, seed=4000, device=dev)
+    torch.manual_seed(0)
+    gen = models.AudioVisualGeneratorMultimodal(300, 76, 48, norm=None).to(dev)
+    step = P.FusedStep(inp, gen.networks(), narrow_fused=True)
+    for _ in range(3):
+        step.run()
+    torch.cuda.synchronize()
+    traces = [dict() for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step.run(trace=traces[k])
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    try:
+        step.check()
+    except Exception as e:  # timing-only ablations (NF_ABL) compute no valid step
+        print(f"# {os.path.basename(args.lib)} check: {type(e).__name__}", flush=True)
+    kn = "mm2_stream_project_narrow"
+    kms = sum(a.elapsed_time(b) for tr in traces for a, b in tr.get(kn, ())) / args.steps
+    line = f"{os.path.basename(args.lib)} kernel_ms {kms:.4f} step_ms {ms:.4f}"
+    if args.check:
+        b = P.FusedStep(inp, gen.networks(), narrow_fused=False)
+        b.run(check=True)
+        torch.cuda.synchronize()
+        dx = ((step.x - b.x).abs().amax(1) / b.x.abs().amax(1).clamp_min(1e-30)).max().item()
+        line += f" x_row_rel {dx:.2e}"
+    print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
