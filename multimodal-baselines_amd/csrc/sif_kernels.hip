@@ -2592,7 +2592,6 @@ extern "C" int mmb_diag_fused_probe(unsigned long long* host_out, int* rate_khz)
 constexpr int kNFThreads = 512;
 constexpr int kNFWaves = kNFThreads / kWave;
 constexpr int kNFRows = 32;                 // utterances per batch
-constexpr int kNFPerWave = kNFRows / kNFWaves;
 constexpr int kNFHot = 32;                  // = mm2_kernels.hip kTextHot
 constexpr int kNFLdp = 304;                 // = kTextLdp (P row stride, floats)
 constexpr int kNFK = 256;                   // K of the audio / visual GEMM (max)
@@ -2613,7 +2612,8 @@ struct NarrowFusedArgs {
   float* out;                // MMB2 rows [N][D]
   int cb_av;                 // first audio chunk of the image (kq(D) / 32)
   int kq_a, kq_v;            // K rows of the audio / visual pieces (multiples of 32)
-  int64_t nb;                // batches
+  int rpw;                   // utterances per wave and batch (4; 1 or 2 for small N)
+  int64_t nb;                // batches of 8 rpw rows
 };
 
 template <int UNR, int HU, int GA_MAX, int GV_MAX>
@@ -2672,10 +2672,12 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 #pragma unroll
   for (int c = 0; c < CT; ++c) cmx[c] = z4;
 
-  // utterance u of this wave in batch j: row 32 (blockIdx.x + gridDim.x j) + 4 wave + u
+  // utterance u of this wave in batch j: row 8 rpw (blockIdx.x + gridDim.x j) + rpw wave + u
+  const int rpw = f.rpw;
+  const int nrt = (kNFWaves * rpw + 15) / 16;  // MFMA row tiles holding rows of the batch
   auto row_of = [&](int64_t j, int u) -> int64_t {
-    return kNFRows * (static_cast<int64_t>(blockIdx.x) + static_cast<int64_t>(gridDim.x) * j) +
-           kNFPerWave * wave + u;
+    return kNFWaves * rpw * (static_cast<int64_t>(blockIdx.x) + static_cast<int64_t>(gridDim.x) * j) +
+           rpw * wave + u;
   };
   auto ld_id = [&](int64_t i) -> int {
     if (NF_ABL & 32) return (i < a.N && lane < L) ? static_cast<int>((lane * 131 + i) % a.V) : -1;
@@ -2758,13 +2760,13 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   for (int64_t j = 0; j < f.nb; j += 1) {
     if (blockIdx.x + static_cast<int64_t>(gridDim.x) * j >= f.nb) break;
     // ------------------------------------------------------------ stream phase
-    for (int u = 0; u < kNFPerWave; ++u) {
+    for (int u = 0; u < rpw; ++u) {
       const int64_t i = row_of(j, u);
-      const int r = kNFPerWave * wave + u;  // row in the batch
+      const int r = rpw * wave + u;  // row in the batch
       const bool live = i < a.N;
       const int rid = rid_n, hs = hs_n;
       const float w = w_n;
-      raw = ld_id(u + 1 < kNFPerWave ? row_of(j, u + 1) : row_of(j + 1, 0));
+      raw = ld_id(u + 1 < rpw ? row_of(j, u + 1) : row_of(j + 1, 0));
       const auto arsrc = frame_rsrc(i, a.audio, a.A);
       const auto vrsrc = frame_rsrc(i, a.visual, a.Vd);
       float4 sa = z4, saa = z4, sv = z4, svv = z4;
@@ -2955,16 +2957,18 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         if (c + 1 < nch) ld_b(c + 1, nh, nl);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
-          const int rr = 16 * rt + q;
-          const int o = (((4 * c + g) ^ q) << 3);
-          const half8 ah = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + o);
-          const half8 al = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + kNFK + o);
+          if (rt < nrt) {
+            const int rr = 16 * rt + q;
+            const int o = (((4 * c + g) ^ q) << 3);
+            const half8 ah = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + o);
+            const half8 al = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + kNFK + o);
 #pragma unroll
-          for (int tt = 0; tt < kMaxT; ++tt) {
-            if (tt < ntt) {
-              acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[tt], acc[rt][tt], 0, 0, 0);
-              acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[tt], acc[rt][tt], 0, 0, 0);
-              acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[tt], acc[rt][tt], 0, 0, 0);
+            for (int tt = 0; tt < kMaxT; ++tt) {
+              if (tt < ntt) {
+                acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[tt], acc[rt][tt], 0, 0, 0);
+                acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[tt], acc[rt][tt], 0, 0, 0);
+                acc[rt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[tt], acc[rt][tt], 0, 0, 0);
+              }
             }
           }
         }
@@ -2988,7 +2992,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
               for (int jj = 0; jj < 4; ++jj) {
                 const int rr = 16 * rt + 4 * g + jj;
                 float* tp = sT + rr * kNFLdp + col;
-                *tp = acc[rt][tt][jj] * (ci * s_irs[rr]) + *tp + cc;
+                if (rt < nrt) *tp = acc[rt][tt][jj] * (ci * s_irs[rr]) + *tp + cc;
               }
           }
         }
@@ -2996,10 +3000,9 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     }
     __syncthreads();
     // ------------------------------------------------------------ epilogue
-    // wave w finishes rows 4 w .. 4 w + 3: / total (column D), L2 norm, store
-#pragma unroll
-    for (int u = 0; u < kNFPerWave; ++u) {
-      const int r = kNFPerWave * wave + u;
+    // wave w finishes rows rpw w .. rpw w + rpw - 1: / total (column D), L2 norm, store
+    for (int u = 0; u < rpw; ++u) {
+      const int r = rpw * wave + u;
       const int64_t i = row_of(j, u);
       const float* trow = sT + r * kNFLdp;
       const float rt = 1.f / trow[D];
@@ -3081,7 +3084,12 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   f.col_inv = reinterpret_cast<const float*>(f.img + 2 * static_cast<size_t>(kNFLdw) * (kq_t + f.kq_a + f.kq_v));
   f.c0 = c0;
   f.out = mmb2_out;
-  f.nb = ceil_div(n, kNFRows);
+  // 4 utterances per wave (32-row batches) once that fills every CU; small N
+  // (dataset splits) fewer per wave: more workgroups, a shorter chain each
+  const int64_t cus = stream_cu_count(stream);
+  f.rpw = 4;
+  while (f.rpw > 1 && ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw) < cus) f.rpw /= 2;
+  f.nb = ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, 7, 4>),

@@ -613,8 +613,9 @@ def test_stream_project_matches_two_kernel_step(gpu, N, T, A, Vd):
     inp = synth.device_workload(N, T, V, A=A, Vd=Vd, seed=61, device=gpu)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
-    a = P.FusedStep(inp, gen.networks(), stream_project=True)
-    b = P.FusedStep(inp, gen.networks(), stream_project=False)
+    # the int8 Gram (its column bounds compared below) at every N
+    a = P.FusedStep(inp, gen.networks(), stream_project=True, gram_kind="i8")
+    b = P.FusedStep(inp, gen.networks(), stream_project=False, gram_kind="i8")
     assert a.stream_project and a.s is None and not b.stream_project
     trace = {}
     s1, m1 = [t.clone() for t in a.run(trace=trace)]
@@ -862,6 +863,7 @@ def test_step_graph_follows_weight_updates(gpu):
                                         (31, 20, 76, 48, 3016), (1001, 40, 76, 48, 3016),
                                         (517, 64, 64, 56, 5000), (64, 7, 20, 8, 300),
                                         (259, 33, 44, 76, 16384), (5, 1, 76, 48, 3016),
+                                        (6000, 20, 76, 48, 3016),
                                         (77, 20, 76, 48, 17)])
 def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
     """The narrow fused kernel (mmb_mm2_stream_project_narrow: per-word text
@@ -874,7 +876,8 @@ def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
     to f32 rounding (another grouping of the same closed form) and both
     within the bar of the CPU oracle.  Partial and single-row batches,
     T from 1 to 64, frame widths 8-128, fewer words than LDS slots (V = 17),
-    the largest cached vocabulary (16384), wrapped negative ids.  (Wider
+    the largest cached vocabulary (16384), wrapped negative ids; 1, 2 and 4
+    utterances per wave and batch (N below ~4k, ~4-8k, larger).  (Wider
     frames -- kq(A) + kq(Vd) > 256 -- and larger vocabularies keep the
     two-kernel step: narrow_fused_supported.)"""
     from oracle import sif_oracle as O
