@@ -1912,6 +1912,8 @@ extern "C" int mmb_mm2_split_pieces(const float* wm, int d, int a, int vd, int l
   return MMB_OK;
 }
 
+namespace mmb {
+
 // ------------------------------------------------------------------ text cache (r04)
 // The MOSI-width fused step (mmb_mm2_stream_project_narrow) projects the text
 // sums per vocabulary row instead of per utterance: the text rows of Wm enter
@@ -1978,6 +1980,8 @@ __global__ __launch_bounds__(1024) void text_hot_kernel(const float* __restrict_
     if (rank < k) hot_ids[rank] = v;
   }
 }
+
+}  // namespace mmb
 
 extern "C" size_t mmb_mm2_text_cache_bytes(int64_t v, int d) {
   (void)d;

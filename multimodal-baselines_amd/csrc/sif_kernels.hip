@@ -2552,6 +2552,8 @@ extern "C" int mmb_diag_fused_probe(unsigned long long* host_out, int* rate_khz)
 }
 #endif
 
+namespace mmb {
+
 // ------------------------------------------------------------------ narrow fused (r04)
 // SIF + closed-form MMB2 at narrow frame widths (MOSI: COVAREP A = 76, FACET
 // Vd = 48, V = 3016) in ONE kernel: the two-kernel step wrote the frame sums
@@ -3039,6 +3041,8 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 // 304 (d % 4), frame rows of 4..128 floats (two or more per instruction,
 // A % 4 == Vd % 4 == 0), kq(A) + kq(Vd) <= 256, t <= 64, V <= 16384 (the
 // text cache)
+}  // namespace mmb
+
 extern "C" int mmb_mm2_stream_project_narrow_supported(int t, int d, int a_, int vd, int64_t v) {
   const int kq = (2 * a_ + 31) / 32 * 32 + (2 * vd + 31) / 32 * 32;
   return t > 0 && t <= kWave && d > 256 && d < kNFLdp && d % 4 == 0 && a_ >= 4 && vd >= 4 &&
