@@ -2582,7 +2582,7 @@ namespace mmb {
 //     row written with 16-byte stores.
 // LDS: hot E rows 38.4 KB + hot P rows 38.9 KB + T 38.9 KB + A 32 KB.
 #ifndef NF_UNR
-#define NF_UNR 3
+#define NF_UNR 2
 #endif
 #ifndef NF_HU
 #define NF_HU 1
@@ -2591,16 +2591,29 @@ namespace mmb {
                 // 8 no a2 / aux stores, 16 no MMB2 stores, 32 no id / weight loads
 #define NF_ABL 0
 #endif
-constexpr int kNFThreads = 512;
-constexpr int kNFWaves = kNFThreads / kWave;
-constexpr int kNFRows = 32;                 // utterances per batch
+#ifndef NF_GA  // audio / visual frame loads issued with the text loads
+#define NF_GA 7
+#endif
+#ifndef NF_GV
+#define NF_GV 4
+#endif
+#ifndef NF_WAVES  // 8 (2 per SIMD, 32-row batches) or 12 (3 per SIMD, 36-row batches)
+#define NF_WAVES 8
+#endif
+constexpr int kNFWaves = NF_WAVES;
+constexpr int kNFThreads = kNFWaves * kWave;
+constexpr int kNFRpw = kNFWaves == 8 ? 4 : 3;  // utterances per wave and batch (at most)
+constexpr int kNFRows = kNFWaves * kNFRpw;     // rows of a batch (at most)
+constexpr int kNFRT = (kNFRows + 15) / 16;     // MFMA row tiles
 constexpr int kNFHot = 32;                  // = mm2_kernels.hip kTextHot
 constexpr int kNFLdp = 304;                 // = kTextLdp (P row stride, floats)
 constexpr int kNFK = 256;                   // K of the audio / visual GEMM (max)
 constexpr int kNFLdw = 320;                 // projection columns
 constexpr int kNFCT = kNFLdp / 16;          // 16-column tiles of y and the total (19)
-constexpr size_t kNFLds = sizeof(float) * (kNFHot * 300 + kNFHot * kNFLdp + kNFRows * kNFLdp) +
-                          sizeof(_Float16) * kNFRows * 2 * kNFK + sizeof(float) * 3 * kNFRows;
+constexpr size_t kNFLdsRows = sizeof(float) * (kNFHot * 300 + kNFHot * kNFLdp + kNFRows * kNFLdp) +
+                              sizeof(_Float16) * kNFRows * 2 * kNFK + sizeof(float) * 3 * kNFRows;
+static_assert(kNFLdsRows % 16 == 0, "the frame-slot scratch is float4-aligned");
+constexpr size_t kNFLds = kNFLdsRows + 16 * kWave * kNFWaves;  // + 1 KB per wave: frame-slot sums
 
 struct NarrowFusedArgs {
   StreamArgs s;        // ids, table, V, wtab, audio, visual, N, L, D, A, Vd, num_out, aux_out, flag, cmax_part
@@ -2619,16 +2632,17 @@ struct NarrowFusedArgs {
 };
 
 template <int UNR, int HU, int GA_MAX, int GV_MAX>
-__global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void utt_narrow_fused_kernel(
+__global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFWaves / 4, kNFWaves / 4))) void utt_narrow_fused_kernel(
     NarrowFusedArgs f) {
   extern __shared__ __attribute__((aligned(16))) float nf_lds[];
   float* hotE = nf_lds;                                   // [kNFHot][300]
   float* hotP = hotE + kNFHot * 300;                      // [kNFHot][kNFLdp]
   float* sT = hotP + kNFHot * kNFLdp;                     // [32][kNFLdp]
-  _Float16* sA = reinterpret_cast<_Float16*>(sT + kNFRows * kNFLdp);  // [32][2][kNFK] swizzled
-  float* s_irs = reinterpret_cast<float*>(sA + kNFRows * 2 * kNFK);   // [32] 1 / row scale
-  float* s_cnt = s_irs + kNFRows;                         // [32]
-  float* s_ok = s_cnt + kNFRows;                          // [32] 1 = a row of this batch
+  _Float16* sA = reinterpret_cast<_Float16*>(sT + kNFRows * kNFLdp);  // [rows][2][kNFK] swizzled
+  float* s_irs = reinterpret_cast<float*>(sA + kNFRows * 2 * kNFK);   // [rows] 1 / row scale
+  float* s_cnt = s_irs + kNFRows;                         // [rows]
+  float* s_ok = s_cnt + kNFRows;                          // [rows] 1 = a row of this batch
+  float4* s_scr = reinterpret_cast<float4*>(s_ok + kNFRows);  // [waves][64] frame-slot sums
 
   const StreamArgs& a = f.s;
   constexpr int CT = 2;
@@ -2676,7 +2690,8 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
 
   // utterance u of this wave in batch j: row 8 rpw (blockIdx.x + gridDim.x j) + rpw wave + u
   const int rpw = f.rpw;
-  const int nrt = (kNFWaves * rpw + 15) / 16;  // MFMA row tiles holding rows of the batch
+  const int nbr = kNFWaves * rpw;  // rows of a batch
+  const int nrt = (nbr + 15) / 16;  // MFMA row tiles holding them
   auto row_of = [&](int64_t j, int u) -> int64_t {
     return kNFWaves * rpw * (static_cast<int64_t>(blockIdx.x) + static_cast<int64_t>(gridDim.x) * j) +
            rpw * wave + u;
@@ -2710,7 +2725,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   // lane (q, g) holds row / column q, K group g of a 16 x 32 fragment
   const int q = lane & 15, g = lane >> 4;
   constexpr int CH = 2 * kNFLdw * 32, PL = kNFLdw * 32;  // image chunk / plane (halves)
-  constexpr int kMaxT = (kNFCT + kNFWaves - 1) / kNFWaves;  // 3
+  constexpr int kMaxT = (kNFCT + kNFWaves - 1) / kNFWaves;  // 3 (8 waves) or 2 (12)
   const int nch = (f.kq_a + f.kq_v) / 32;
   const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.img), 0,
                                                        (f.cb_av + nch) * CH * 2, 0x00020000);
@@ -2720,7 +2735,8 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
     boff[tt] = col * 32 + ((g ^ x3_swz(col)) << 3);
   }
-  const int ntt = wave + kNFWaves * 2 < kNFCT ? 3 : 2;
+  static_assert(kMaxT == 2 || kMaxT == 3, "column tiles per wave");
+  const int ntt = wave + kNFWaves * (kMaxT - 1) < kNFCT ? kMaxT : kMaxT - 1;  // this wave's column tiles
   float cinv[kMaxT], cc0[kMaxT];  // the tiles' column scales and c0
 #pragma unroll
   for (int tt = 0; tt < kMaxT; ++tt) {
@@ -2870,27 +2886,27 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       if (live && lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
       for (int g0 = GA_MAX; g0 < GA; g0 += GA_MAX) frames(GAc{}, arsrc, voa, a.A, UA, PA, g0, sa, saa)();
       for (int g0 = GV_MAX; g0 < GV; g0 += GV_MAX) frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, g0, sv, svv)();
-      auto slots = [&](float4& acc, int U, int P) {
-        float4 rs = acc;
-        for (int q = 1; q < P; ++q) {
-          const int src = min(lane + q * U, kWave - 1);
-          float4 o;
-          o.x = __shfl(acc.x, src, kWave);
-          o.y = __shfl(acc.y, src, kWave);
-          o.z = __shfl(acc.z, src, kWave);
-          o.w = __shfl(acc.w, src, kWave);
-          add4(rs, o);
+      // The A row [Sa | Saa | 0 | Sv | Svv] (K = 4 lane .. 4 lane + 3 on lane
+      // `lane`): each frame sum's P row slots added up through this wave's 1
+      // KB of LDS (one write, P reads by the lanes holding that piece; slot 0
+      // first, as the shuffle reduction of utt_narrow_kernel); pads 0
+      float4* scr = s_scr + wave * kWave;
+      float4 av = z4;
+      auto gather = [&](const float4& acc, int U, int P, int u0) {
+        __builtin_amdgcn_wave_barrier();  // the previous piece's reads are issued
+        scr[lane] = acc;
+        __builtin_amdgcn_wave_barrier();
+        const int l = lane - u0;
+        if (l >= 0 && l < U) {
+          av = scr[l];
+          for (int q = 1; q < P; ++q) add4(av, scr[l + q * U]);
         }
-        acc = rs;
       };
-      slots(sa, UA, PA);
-      slots(saa, UA, PA);
-      slots(sv, UV, PV);
-      slots(svv, UV, PV);
-      if (lane >= UA) sa = saa = z4;
-      if (lane >= UV) sv = svv = z4;
-      const float m = fmaxf(fmaxf(amax4(sa), amax4(saa)), fmaxf(amax4(sv), amax4(svv)));
-      const float rsc = row_scale(wave_max(m));
+      gather(sa, UA, PA, 0);
+      gather(saa, UA, PA, UA);
+      gather(sv, UV, PV, f.kq_a >> 2);
+      gather(svv, UV, PV, (f.kq_a >> 2) + UV);
+      const float rsc = row_scale(wave_max(amax4(av)));
       resolve(raw, rid_n, w_n, hs_n);  // the next utterance's
       // x (the a2 row), column bounds, aux; the text term T into LDS
       const float rc = 1.f / cnt;
@@ -2915,7 +2931,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
                           held ? tp[c].w : 0.f);
         }
       }
-      // [Sa | Saa | 0 | Sv | Svv] as fp16 hi | lo, row-scaled, swizzled per row
+      // the A row as fp16 hi | lo, row-scaled, swizzled per row
       {
         _Float16* arow = sA + r * 2 * kNFK;
         const int q = r & 15;
@@ -2923,14 +2939,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
           const int grp = k >> 3, o = ((grp ^ q) << 3) + (k & 7);
           split_store4(arow + o, arow + kNFK + o, v, rsc);
         };
-        if (lane < UA) {
-          put(4 * lane, sa);
-          put(a.A + 4 * lane, saa);
-        }
-        if (lane < UV) {
-          put(f.kq_a + 4 * lane, sv);
-          put(f.kq_a + a.Vd + 4 * lane, svv);
-        }
+        put(4 * lane, av);  // the whole row, pads included
       }
       if (lane == 0) {
         s_irs[r] = 1.f / rsc;
@@ -2949,18 +2958,19 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     __syncthreads();
     // ------------------------------------------------------------ MFMA phase
     {
-      f32x4 acc[2][kMaxT];
+      f32x4 acc[kNFRT][kMaxT];
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+      for (int rt = 0; rt < kNFRT; ++rt)
 #pragma unroll
         for (int tt = 0; tt < kMaxT; ++tt) acc[rt][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int c = 0; c < ((NF_ABL & 1) ? 0 : nch); ++c) {
         half8 nh[kMaxT], nl[kMaxT];  // chunk c + 1, in flight during chunk c
         if (c + 1 < nch) ld_b(c + 1, nh, nl);
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
+        for (int rt = 0; rt < kNFRT; ++rt) {
           if (rt < nrt) {
-            const int rr = 16 * rt + q;
+            // (36-row batches: rows past the last are clamped, their results unused)
+            const int rr = kNFRows % 16 == 0 ? 16 * rt + q : min(16 * rt + q, kNFRows - 1);
             const int o = (((4 * c + g) ^ q) << 3);
             const half8 ah = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + o);
             const half8 al = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + kNFK + o);
@@ -2989,12 +2999,12 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(2, 2
           if (col < kNFLdp) {
             const float ci = cinv[tt], cc = cc0[tt];
 #pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
+            for (int rt = 0; rt < kNFRT; ++rt)
 #pragma unroll
               for (int jj = 0; jj < 4; ++jj) {
                 const int rr = 16 * rt + 4 * g + jj;
                 float* tp = sT + rr * kNFLdp + col;
-                if (rt < nrt) *tp = acc[rt][tt][jj] * (ci * s_irs[rr]) + *tp + cc;
+                if (kNFRows % 16 == 0 ? rt < nrt : rr < nbr) *tp = acc[rt][tt][jj] * (ci * s_irs[rr]) + *tp + cc;
               }
           }
         }
@@ -3091,19 +3101,19 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   // 4 utterances per wave (32-row batches) once that fills every CU; small N
   // (dataset splits) fewer per wave: more workgroups, a shorter chain each
   const int64_t cus = stream_cu_count(stream);
-  f.rpw = 4;
-  while (f.rpw > 1 && ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw) < cus) f.rpw /= 2;
+  f.rpw = kNFRpw;
+  while (f.rpw > 1 && ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw) < cus) --f.rpw;
   f.nb = ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, 7, 4>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
     attr = true;
   }
   int64_t grid = stream_cu_count(stream);
   if (colmax && grid > kCmaxRows / kNFWaves) grid = kCmaxRows / kNFWaves;
   if (grid > f.nb) grid = f.nb;
-  utt_narrow_fused_kernel<NF_UNR, NF_HU, 7, 4><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
+  utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
   MMB_LAUNCH_CHECK();
   if (!colmax) return MMB_OK;
   colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(
