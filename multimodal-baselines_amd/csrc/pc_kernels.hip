@@ -633,9 +633,17 @@ __device__ unsigned long long g_pc_probe[64];
     __syncthreads();                                                       \
     if (threadIdx.x == 0 && blockIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
   } while (0)
+// one wave's own mark (no barrier): lane 0 of the calling wave, workgroup 0
+#define PC_WMARK(i)                                                               \
+  do {                                                                            \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
+  } while (0)
 #else
 #define PC_MARK(i) \
   do {             \
+  } while (0)
+#define PC_WMARK(i) \
+  do {              \
   } while (0)
 #endif
 constexpr int kMaxD = 512;
@@ -1147,6 +1155,7 @@ __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, do
   // in registers spilled to scratch, one reload per substitution step
   double* rl = sLi;
   bool bad = false;
+  PC_WMARK(31);
 #pragma unroll
   for (int j = 0; j < kMaxK; ++j) {
     if (j < k) {
@@ -1163,6 +1172,7 @@ __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, do
   }
   if (bad && lane == 0) *fail = 1;
   wave_lds_sync();
+  PC_WMARK(32);
   // column c = lane of Linv: forward substitution, L entries and the
   // reciprocal pivots read as LDS broadcasts
 #pragma unroll
@@ -1175,6 +1185,7 @@ __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, do
       x[i] = s * rl[kMaxK * kMaxK - kMaxK + i];
     }
   }
+  PC_WMARK(33);
   wave_lds_sync();  // every lane has read the pivots before sLi is written
   if (lane < k) {
 #pragma unroll
@@ -1579,6 +1590,7 @@ __device__ __forceinline__ void p16_rmul(const double* In, const double* M, doub
 __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* Li, double* M,
                                             double* d, int k, int lane, int* fail) {
   double w[kMaxK], x[kMaxK];
+  PC_WMARK(30);
 #pragma unroll
   for (int m = 0; m < kMaxK; ++m) w[m] = (lane < k && m < k) ? W[lane * k + m] : 0.0;
   const double di = rsqrt_f64(lane < k ? W[lane * k + lane] : 1.0);
@@ -1592,6 +1604,7 @@ __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* 
     for (int i = 0; i < kP16W; ++i) M[i * kP16W + lane] = (lane < k && i < k) ? x[i] * di : 0.0;
   }
   wave_lds_sync();
+  PC_WMARK(34);
 }
 
 __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,

@@ -56,7 +56,9 @@ int main() {
              us(44 + 2 * r, 45 + 2 * r), us(45 + 2 * r, 2 + 3 * r), us(3 + 3 * r, 4 + 3 * r));
       prev = 4 + 3 * r;
     }
-    printf(" | tail-rr %.1f eig %.1f out %.1f\n", us(40, 41), us(41, 42), us(42, 43));
+    printf(" | tail-rr %.1f eig %.1f out %.1f", us(40, 41), us(41, 42), us(42, 43));
+    printf(" | last eq-chol: equilibrate %.2f factor %.2f substitute %.2f store %.2f\n", us(30, 31),
+           us(31, 32), us(32, 33), us(33, 34));
   }
   int32_t hflag = 0;
   (void)hipMemcpy(&hflag, flag, 4, hipMemcpyDeviceToHost);
