@@ -2991,22 +2991,38 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
         }
       }
       // y = acc * (col scale * row scale) + T + c0, in place in the T rows
-      // (lane value (rt, tt, jj): row 16 rt + 4 g + jj, column 16 ct + q)
+      // (lane value (rt, tt, jj): row 16 rt + 4 g + jj, column 16 ct + q).
+      // Every T value and row scale is read before any update is written: in
+      // place, each read-modify-write waited for the previous one's store
+      // (the compiler cannot tell the rows apart)
+      static_assert(kNFCT * 16 <= kNFLdp, "the column tiles lie inside the T rows");
+      float irs[kNFRT][4], tv[kMaxT][kNFRT][4];
+#pragma unroll
+      for (int rt = 0; rt < kNFRT; ++rt)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) irs[rt][jj] = s_irs[min(16 * rt + 4 * g + jj, kNFRows - 1)];
+#pragma unroll
+      for (int tt = 0; tt < kMaxT; ++tt) {
+        const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+#pragma unroll
+        for (int rt = 0; rt < kNFRT; ++rt)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            tv[tt][rt][jj] = sT[min(16 * rt + 4 * g + jj, kNFRows - 1) * kNFLdp + col];
+      }
 #pragma unroll
       for (int tt = 0; tt < kMaxT; ++tt) {
         if (tt < ntt) {
           const int col = 16 * (wave + kNFWaves * tt) + q;
-          if (col < kNFLdp) {
-            const float ci = cinv[tt], cc = cc0[tt];
+          const float ci = cinv[tt], cc = cc0[tt];
 #pragma unroll
-            for (int rt = 0; rt < kNFRT; ++rt)
+          for (int rt = 0; rt < kNFRT; ++rt)
 #pragma unroll
-              for (int jj = 0; jj < 4; ++jj) {
-                const int rr = 16 * rt + 4 * g + jj;
-                float* tp = sT + rr * kNFLdp + col;
-                if (kNFRows % 16 == 0 ? rt < nrt : rr < nbr) *tp = acc[rt][tt][jj] * (ci * s_irs[rr]) + *tp + cc;
-              }
-          }
+            for (int jj = 0; jj < 4; ++jj) {
+              const int rr = 16 * rt + 4 * g + jj;
+              if (kNFRows % 16 == 0 ? rt < nrt : rr < nbr)
+                sT[rr * kNFLdp + col] = acc[rt][tt][jj] * (ci * irs[rt][jj]) + tv[tt][rt][jj] + cc;
+            }
         }
       }
     }
