@@ -306,11 +306,13 @@ int mmb_mm2_project_x3_rmpc(const void* s_split, const float* num, const float* 
  * once; the 32 words of smallest SIF weight kept in LDS), so only the
  * audio / visual frame sums (K = kq(A) + kq(Vd) <= 256) meet the f16 x3 MFMA,
  * inside the same launch; the frame sums never reach HBM.  Writes x (the a2
- * rows, bit-identical to mmb_mm2_stream's), aux, the MMB2 rows and (colmax
- * non-null) the column bounds of x for mmb_gram_i8.
+ * rows: mmb_mm2_stream's sums in another order -- hot words first -- so
+ * equal to f32 rounding), aux, the MMB2 rows and (colmax non-null) the
+ * column bounds of x for mmb_gram_i8.
  *   mmb_mm2_text_cache: cache of mmb_mm2_text_cache_bytes(v, d) bytes (16-B
  *   aligned) from the word table, the f32 weight table and the merged Wm
- *   (mmb_mm2_prepare); rebuild it when any of them changes.  v <= 16384.
+ *   (mmb_mm2_prepare); rebuild it when any of them changes (the launch reads
+ *   the token weights from the cache's copy of wtab32).  v <= 16384.
  *   wpieces: the piece-ordered weight split (mmb_mm2_split_pieces).
  * replaces: sif2.calc_weights + estimate_embedding_overall_gpu2
  *   /root/reference/sif2.py:103-114,164-208 with the text gather of

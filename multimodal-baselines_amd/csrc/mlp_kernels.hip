@@ -38,8 +38,6 @@ namespace mmb {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int kMlpNT = 1024;
-constexpr int kMaxWaves = kMlpNT / kWave;
 constexpr int kBatchMax = 32;  // one MFMA M-tile of batch rows
 
 __device__ __forceinline__ int c_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }

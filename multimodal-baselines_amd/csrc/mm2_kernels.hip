@@ -1928,7 +1928,8 @@ namespace mmb {
 // (the pad id 0 too where its weight is 0), whose E and P rows the fused
 // kernel keeps in LDS.
 //   cache layout: P [v][kTextLdp] f32 | hot_slot1 [v] int32 (slot + 1, 0 = not
-//   hot) | hot_ids [kTextHot] int32
+//   hot) | hot_ids [kTextHot] int32 | w [v] f32 (a copy of the weights: the
+//   fused kernel reads all of it through one buffer descriptor)
 constexpr int kTextLdp = 304;   // P row stride (floats): d + 1 <= 304, 16-byte rows
 constexpr int kTextHot = 32;    // words whose rows live in LDS
 constexpr int64_t kTextMaxV = 16384;
@@ -1960,7 +1961,8 @@ __global__ __launch_bounds__(320) void mm2_text_table_kernel(const float* __rest
 // hot_slot1[v] = rank + 1 for the k smallest, else 0; hot_ids[rank] = v
 __global__ __launch_bounds__(1024) void text_hot_kernel(const float* __restrict__ wtab, int V, int k,
                                                         int32_t* __restrict__ hot_slot1,
-                                                        int32_t* __restrict__ hot_ids) {
+                                                        int32_t* __restrict__ hot_ids,
+                                                        float* __restrict__ wcopy) {
   __shared__ float sw[1024];
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   const float wv = v < V ? wtab[v] : 0.f;
@@ -1978,6 +1980,7 @@ __global__ __launch_bounds__(1024) void text_hot_kernel(const float* __restrict_
   if (v < V) {
     hot_slot1[v] = rank < k ? rank + 1 : 0;
     if (rank < k) hot_ids[rank] = v;
+    wcopy[v] = wv;
   }
 }
 
@@ -1985,7 +1988,7 @@ __global__ __launch_bounds__(1024) void text_hot_kernel(const float* __restrict_
 
 extern "C" size_t mmb_mm2_text_cache_bytes(int64_t v, int d) {
   (void)d;
-  return sizeof(float) * static_cast<size_t>(v) * kTextLdp + sizeof(int32_t) * (v + kTextHot);
+  return sizeof(float) * static_cast<size_t>(v) * (kTextLdp + 1) + sizeof(int32_t) * (v + kTextHot);
 }
 
 extern "C" int mmb_mm2_text_cache(const float* table, int64_t v, int d, const float* wtab32,
@@ -1995,10 +1998,12 @@ extern "C" int mmb_mm2_text_cache(const float* table, int64_t v, int d, const fl
   float* ptab = static_cast<float*>(cache);
   int32_t* hot_slot1 = reinterpret_cast<int32_t*>(ptab + static_cast<size_t>(v) * kTextLdp);
   int32_t* hot_ids = hot_slot1 + v;
+  float* wcopy = reinterpret_cast<float*>(hot_ids + kTextHot);
   mm2_text_table_kernel<<<static_cast<unsigned>(v), 320, 0, stream>>>(table, d, wm, ldw, ptab);
   MMB_LAUNCH_CHECK();
   text_hot_kernel<<<static_cast<unsigned>(ceil_div(v, 1024)), 1024, 0, stream>>>(
-      wtab32, static_cast<int>(v), static_cast<int>(std::min<int64_t>(v, kTextHot)), hot_slot1, hot_ids);
+      wtab32, static_cast<int>(v), static_cast<int>(std::min<int64_t>(v, kTextHot)), hot_slot1, hot_ids,
+      wcopy);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

@@ -2674,13 +2674,13 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
     vp[c] = 16 * min(lane + kWave * c, UP - 1);
   }
   const int tbytes = static_cast<int>(a.V * D * 4);
-  const int pbytes = static_cast<int>(a.V * kNFLdp * 4);
+  // one descriptor over the whole text cache: P rows | hot slots | hot ids |
+  // the weights (mm2_kernels.hip); offset `cbytes` is past its end and reads 0
+  const int hbase = static_cast<int>(a.V * kNFLdp * 4);              // hot_slot1
+  const int wbase = hbase + static_cast<int>(a.V * 4) + 4 * kNFHot;  // the weight copy
+  const int cbytes = wbase + static_cast<int>(a.V * 4);
   const auto trsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.table), 0, tbytes, 0x00020000);
-  const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f.ptab), 0, pbytes, 0x00020000);
-  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.wtab), 0,
-                                                       static_cast<int>(a.V * 4), 0x00020000);
-  const auto hrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(f.hot_slot1), 0,
-                                                       static_cast<int>(a.V * 4), 0x00020000);
+  const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f.ptab), 0, cbytes, 0x00020000);
   const int voa = ((lane / UA) * a.A + 4 * (lane % UA)) * 4;
   const int vov = ((lane / UV) * a.Vd + 4 * (lane % UV)) * 4;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2710,13 +2710,13 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       int64_t id = raw;
       const bool in = id >= 0 && id < a.V;
       w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                        wrsrc, in ? static_cast<int>(id) * 4 : static_cast<int>(a.V * 4), 0, 0));
+                                        prsrc, in ? wbase + static_cast<int>(id) * 4 : cbytes, 0, 0));
       if (id < 0) id += a.V;
       if (id < 0 || id >= a.V) {
         if (a.flag) atomicOr(a.flag, MMB_FLAG_ID_RANGE);
       } else {
         rid = static_cast<int>(id);
-        hs = __builtin_amdgcn_raw_buffer_load_b32(hrsrc, rid * 4, 0, 0);
+        hs = __builtin_amdgcn_raw_buffer_load_b32(prsrc, hbase + rid * 4, 0, 0);
       }
     }
   };
@@ -2825,7 +2825,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       auto cold_row = [&](int t, float4 (&ve)[CT], float4 (&vq)[CT]) {
         const int rr = t >= 0 ? __builtin_amdgcn_readlane(rid, t) : -1;
         const int so = rr >= 0 ? rr * D * 4 : tbytes;  // none: out of range, reads 0
-        const int sp = rr >= 0 ? rr * kNFLdp * 4 : pbytes;
+        const int sp = rr >= 0 ? rr * kNFLdp * 4 : cbytes;
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
           ve[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
