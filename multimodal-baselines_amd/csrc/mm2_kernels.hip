@@ -1927,16 +1927,19 @@ namespace mmb {
 // the kTextHot smallest SIF weights a / (a + p(w)) are the most frequent words
 // (the pad id 0 too where its weight is 0), whose E and P rows the fused
 // kernel keeps in LDS.
-//   cache layout: P [v][kTextLdp] f32 | hot_slot1 [v] int32 (slot + 1, 0 = not
-//   hot) | hot_ids [kTextHot] int32 | w [v] f32 (a copy of the weights: the
-//   fused kernel reads all of it through one buffer descriptor)
-constexpr int kTextLdp = 304;   // P row stride (floats): d + 1 <= 304, 16-byte rows
+//   cache layout: rows [v][kTextLdq] f32 = E[v][0, d) | P[v][0, d] | 0 pad
+//   (the word's table row and its projection side by side: one token, one
+//   contiguous 2d + 4 floats) | hot_slot1 [v] int32 (slot + 1, 0 = not hot) |
+//   hot_ids [kTextHot] int32 | w [v] f32 (a copy of the weights: the fused
+//   kernel reads all of it through one buffer descriptor)
+constexpr int kTextLdp = 304;   // P columns kept (d + 1 <= 304)
+constexpr int kTextLdq = 608;   // cache row stride (floats): 2 d + 4 <= 608, 16-byte rows
 constexpr int kTextHot = 32;    // words whose rows live in LDS
 constexpr int64_t kTextMaxV = 16384;
 
 __global__ __launch_bounds__(320) void mm2_text_table_kernel(const float* __restrict__ E, int D,
                                                              const float* __restrict__ wm, int ldw,
-                                                             float* __restrict__ ptab) {
+                                                             float* __restrict__ rows) {
   __shared__ double se[kTextLdp], se2[kTextLdp];
   const int64_t v = blockIdx.x;
   for (int f = threadIdx.x; f < D; f += blockDim.x) {
@@ -1945,7 +1948,9 @@ __global__ __launch_bounds__(320) void mm2_text_table_kernel(const float* __rest
     se2[f] = e * e;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < kTextLdp; j += blockDim.x) {
+  float* row = rows + v * kTextLdq;
+  for (int f = threadIdx.x; f < D; f += blockDim.x) row[f] = E[v * D + f];
+  for (int j = threadIdx.x; j + D < kTextLdq; j += blockDim.x) {
     double acc = 0.0;
     if (j <= D) {
       for (int f = 0; f < D; ++f) {
@@ -1953,7 +1958,7 @@ __global__ __launch_bounds__(320) void mm2_text_table_kernel(const float* __rest
         acc = fma(se2[f], static_cast<double>(wm[static_cast<int64_t>(D + f) * ldw + j]), acc);
       }
     }
-    ptab[v * kTextLdp + j] = static_cast<float>(acc);
+    row[D + j] = static_cast<float>(acc);
   }
 }
 
@@ -1988,15 +1993,16 @@ __global__ __launch_bounds__(1024) void text_hot_kernel(const float* __restrict_
 
 extern "C" size_t mmb_mm2_text_cache_bytes(int64_t v, int d) {
   (void)d;
-  return sizeof(float) * static_cast<size_t>(v) * (kTextLdp + 1) + sizeof(int32_t) * (v + kTextHot);
+  return sizeof(float) * static_cast<size_t>(v) * (kTextLdq + 1) + sizeof(int32_t) * (v + kTextHot);
 }
 
 extern "C" int mmb_mm2_text_cache(const float* table, int64_t v, int d, const float* wtab32,
                                   const float* wm, int ldw, void* cache, hipStream_t stream) {
   MMB_REQUIRE(table && wtab32 && wm && cache && v > 0 && v <= kTextMaxV);
-  MMB_REQUIRE(d > 0 && d + 1 <= kTextLdp && ldw > d && (reinterpret_cast<uintptr_t>(cache) & 15) == 0);
+  MMB_REQUIRE(d > 0 && d % 4 == 0 && d + 1 <= kTextLdp && ldw > d &&
+              (reinterpret_cast<uintptr_t>(cache) & 15) == 0);
   float* ptab = static_cast<float*>(cache);
-  int32_t* hot_slot1 = reinterpret_cast<int32_t*>(ptab + static_cast<size_t>(v) * kTextLdp);
+  int32_t* hot_slot1 = reinterpret_cast<int32_t*>(ptab + static_cast<size_t>(v) * kTextLdq);
   int32_t* hot_ids = hot_slot1 + v;
   float* wcopy = reinterpret_cast<float*>(hot_ids + kTextHot);
   mm2_text_table_kernel<<<static_cast<unsigned>(v), 320, 0, stream>>>(table, d, wm, ldw, ptab);

@@ -2606,18 +2606,20 @@ constexpr int kNFRpw = kNFWaves == 8 ? 4 : 3;  // utterances per wave and batch 
 constexpr int kNFRows = kNFWaves * kNFRpw;     // rows of a batch (at most)
 constexpr int kNFRT = (kNFRows + 15) / 16;     // MFMA row tiles
 constexpr int kNFHot = 32;                  // = mm2_kernels.hip kTextHot
-constexpr int kNFLdp = 304;                 // = kTextLdp (P row stride, floats)
+constexpr int kNFLdp = 304;                 // = kTextLdp (T row stride, floats: y columns and the total)
+constexpr int kNFLdq = 608;                 // = kTextLdq (text cache row: E | P, floats)
+constexpr int kNFHotRow = 604;              // a hot word's E | P row in LDS (151 float4 units)
 constexpr int kNFK = 256;                   // K of the audio / visual GEMM (max)
 constexpr int kNFLdw = 320;                 // projection columns
 constexpr int kNFCT = kNFLdp / 16;          // 16-column tiles of y and the total (19)
-constexpr size_t kNFLdsRows = sizeof(float) * (kNFHot * 300 + kNFHot * kNFLdp + kNFRows * kNFLdp) +
+constexpr size_t kNFLdsRows = sizeof(float) * (kNFHot * kNFHotRow + kNFRows * kNFLdp) +
                               sizeof(_Float16) * kNFRows * 2 * kNFK + sizeof(float) * 3 * kNFRows;
 static_assert(kNFLdsRows % 16 == 0, "the frame-slot scratch is float4-aligned");
 constexpr size_t kNFLds = kNFLdsRows + 16 * kWave * kNFWaves;  // + 1 KB per wave: frame-slot sums
 
 struct NarrowFusedArgs {
   StreamArgs s;        // ids, table, V, wtab, audio, visual, N, L, D, A, Vd, num_out, aux_out, flag, cmax_part
-  const float* ptab;   // [V][kNFLdp]
+  const float* ptab;   // [V][kNFLdq]: E | P rows
   const int32_t* hot_slot1;  // [V]
   const int32_t* hot_ids;    // [n_hot]
   int n_hot;
@@ -2635,9 +2637,8 @@ template <int UNR, int HU, int GA_MAX, int GV_MAX>
 __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFWaves / 4, kNFWaves / 4))) void utt_narrow_fused_kernel(
     NarrowFusedArgs f) {
   extern __shared__ __attribute__((aligned(16))) float nf_lds[];
-  float* hotE = nf_lds;                                   // [kNFHot][300]
-  float* hotP = hotE + kNFHot * 300;                      // [kNFHot][kNFLdp]
-  float* sT = hotP + kNFHot * kNFLdp;                     // [32][kNFLdp]
+  float* hotEP = nf_lds;                                  // [kNFHot][kNFHotRow]: E | P
+  float* sT = hotEP + kNFHot * kNFHotRow;                 // [rows][kNFLdp]
   _Float16* sA = reinterpret_cast<_Float16*>(sT + kNFRows * kNFLdp);  // [rows][2][kNFK] swizzled
   float* s_irs = reinterpret_cast<float*>(sA + kNFRows * 2 * kNFK);   // [rows] 1 / row scale
   float* s_cnt = s_irs + kNFRows;                         // [rows]
@@ -2651,36 +2652,36 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   const int64_t wid = static_cast<int64_t>(blockIdx.x) * kNFWaves + wave;
   const int L = a.L, D = a.D;
   const int UT = D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
-  const int UP = (D + 4) >> 2;  // P units holding columns 0..D
   const int PA = kWave / UA, PV = kWave / UV;
   const int GA = (L + PA - 1) / PA, GV = (L + PV - 1) / PV;
 
-  // the hot words' E and P rows into LDS
-  for (int e = tid; e < f.n_hot * 75; e += kNFThreads) {
-    const int k = e / 75, u = e - k * 75;
-    const int64_t v = f.hot_ids[k];
-    if (4 * u < D) *reinterpret_cast<float4*>(hotE + k * 300 + 4 * u) = ld4(a.table + v * D + 4 * u);
-  }
-  for (int e = tid; e < f.n_hot * (kNFLdp / 4); e += kNFThreads) {
-    const int k = e / (kNFLdp / 4), u = e - k * (kNFLdp / 4);
-    *reinterpret_cast<float4*>(hotP + k * kNFLdp + 4 * u) =
-        ld4(f.ptab + static_cast<int64_t>(f.hot_ids[k]) * kNFLdp + 4 * u);
+  // the hot words' E | P rows into LDS
+  const int NU = 2 * (D >> 2) + 1;  // float4 units of a cache row: E (D / 4) then P (D / 4 + 1)
+  for (int e = tid; e < f.n_hot * NU; e += kNFThreads) {
+    const int k = e / NU, u = e - k * NU;
+    *reinterpret_cast<float4*>(hotEP + k * kNFHotRow + 4 * u) =
+        ld4(f.ptab + static_cast<int64_t>(f.hot_ids[k]) * kNFLdq + 4 * u);
   }
 
-  int vt[CT], vp[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    vt[c] = 16 * min(lane + kWave * c, UT - 1);
-    vp[c] = 16 * min(lane + kWave * c, UP - 1);
-  }
-  const int tbytes = static_cast<int>(a.V * D * 4);
-  // one descriptor over the whole text cache: P rows | hot slots | hot ids |
-  // the weights (mm2_kernels.hip); offset `cbytes` is past its end and reads 0
-  const int hbase = static_cast<int>(a.V * kNFLdp * 4);              // hot_slot1
+  // one descriptor over the whole text cache: E | P rows | hot slots | hot
+  // ids | the weights (mm2_kernels.hip); offset `cbytes` is past its end and
+  // reads 0
+  const int hbase = static_cast<int>(a.V * kNFLdq * 4);              // hot_slot1
   const int wbase = hbase + static_cast<int>(a.V * 4) + 4 * kNFHot;  // the weight copy
   const int cbytes = wbase + static_cast<int>(a.V * 4);
-  const auto trsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.table), 0, tbytes, 0x00020000);
   const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f.ptab), 0, cbytes, 0x00020000);
+  // a token's E | P row: unit u = lane + 64 c of slot c (E units [0, UT),
+  // P units [UT, NU)); slot 0 is all E, slot 1 E on lanes 64 + lane < UT and
+  // P above, slot 2 P or nothing
+  constexpr int CQ = 3;
+  int vu[CQ], hu[CQ];
+#pragma unroll
+  for (int c = 0; c < CQ; ++c) {
+    const int u = lane + kWave * c;
+    vu[c] = u < NU ? 16 * u : cbytes;  // past the cache: reads 0
+    hu[c] = 4 * min(u, NU - 1);
+  }
+  const bool e1 = kWave + lane < UT;  // slot 1 holds an E unit on this lane
   const int voa = ((lane / UA) * a.A + 4 * (lane % UA)) * 4;
   const int vov = ((lane / UV) * a.Vd + 4 * (lane % UV)) * 4;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2816,68 +2817,59 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       // cold words (global loads) is in flight, then the cold groups.  The
       // order (hot tokens, then cold, each by position) is not
       // utt_narrow_kernel's: x agrees with it to f32 rounding.
-      float4 num[CT], tp[CT];
+      float4 ac[CQ];  // slot sums: w E units, then P units (e1: slot 1 mixes them)
 #pragma unroll
-      for (int c = 0; c < CT; ++c) num[c] = tp[c] = z4;
+      for (int c = 0; c < CQ; ++c) ac[c] = z4;
       const bool tok = lane < L && rid >= 0;
       uint64_t cold = (NF_ABL & 4) ? 0 : __builtin_amdgcn_ballot_w64(tok && hs == 0);
       uint64_t hot = (NF_ABL & 4) ? 0 : __builtin_amdgcn_ballot_w64(tok && hs > 0);
-      auto cold_row = [&](int t, float4 (&ve)[CT], float4 (&vq)[CT]) {
+      auto cold_row = [&](int t, float4 (&v)[CQ]) {
         const int rr = t >= 0 ? __builtin_amdgcn_readlane(rid, t) : -1;
-        const int so = rr >= 0 ? rr * D * 4 : tbytes;  // none: out of range, reads 0
-        const int sp = rr >= 0 ? rr * kNFLdp * 4 : cbytes;
+        const int so = rr >= 0 ? rr * kNFLdq * 4 : cbytes;  // none: out of range, reads 0
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          ve[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(trsrc, vt[c], so, 0));
-          vq[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, vp[c], sp, 0));
-        }
+        for (int c = 0; c < CQ; ++c)
+          v[c] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prsrc, vu[c], so, 0));
       };
-      auto accum = [&](int t, const float4 (&ve)[CT], const float4 (&vq)[CT]) {
+      auto accum = [&](int t, const float4 (&v)[CQ]) {
         const float wt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), t));
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          fma4(num[c], wt, ve[c]);
-          add4(tp[c], vq[c]);
-        }
+        fma4(ac[0], wt, v[0]);
+        fma4(ac[1], e1 ? wt : 1.f, v[1]);  // 1 * p + s == p + s exactly
+        add4(ac[2], v[2]);
       };
       {
-        float4 ve[UNR][CT], vq[UNR][CT];
+        float4 vc[UNR][CQ];
         int tq[UNR];
 #pragma unroll
         for (int q = 0; q < UNR; ++q) {
           tq[q] = take(cold);
-          cold_row(tq[q], ve[q], vq[q]);
+          cold_row(tq[q], vc[q]);
         }
         while (hot) {
-          float4 he[HU][CT], hq[HU][CT];
+          float4 vh[HU][CQ];
           int th[HU];
 #pragma unroll
           for (int q = 0; q < HU; ++q) {
             th[q] = take(hot);
             const int hh = th[q] >= 0 ? __builtin_amdgcn_readlane(hs, th[q]) - 1 : 0;
-            const float* pe = hotE + hh * 300;
-            const float* pq = hotP + hh * kNFLdp;
+            const float* pr = hotEP + hh * kNFHotRow;
 #pragma unroll
-            for (int c = 0; c < CT; ++c) {
-              he[q][c] = *reinterpret_cast<const float4*>(pe + (vt[c] >> 2));
-              hq[q][c] = *reinterpret_cast<const float4*>(pq + (vp[c] >> 2));
-            }
+            for (int c = 0; c < CQ; ++c) vh[q][c] = *reinterpret_cast<const float4*>(pr + hu[c]);
           }
 #pragma unroll
           for (int q = 0; q < HU; ++q)
-            if (th[q] >= 0) accum(th[q], he[q], hq[q]);
+            if (th[q] >= 0) accum(th[q], vh[q]);
         }
         acc_a();
         acc_v();
         for (;;) {
 #pragma unroll
           for (int q = 0; q < UNR; ++q)
-            if (tq[q] >= 0) accum(tq[q], ve[q], vq[q]);
+            if (tq[q] >= 0) accum(tq[q], vc[q]);
           if (!cold) break;
 #pragma unroll
           for (int q = 0; q < UNR; ++q) {
             tq[q] = take(cold);
-            cold_row(tq[q], ve[q], vq[q]);
+            cold_row(tq[q], vc[q]);
           }
         }
       }
@@ -2911,24 +2903,32 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       // x (the a2 row), column bounds, aux; the text term T into LDS
       const float rc = 1.f / cnt;
       float* trow = sT + r * kNFLdp;
+      // T = sum w E + sum P: the P units into the T row first (unit UT, the
+      // total weight column, plus the weight sum; pads 0), then each E unit's
+      // lane adds its sum there
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
+      for (int c = 1; c < CQ; ++c) {
+        const int p = lane + kWave * c - UT;  // P unit of this slot
+        if (p >= 0 && p <= UT) {
+          float4 tv = ac[c];
+          if (p == UT) tv.x += sw;
+          *reinterpret_cast<float4*>(trow + 4 * p) = tv;
+        }
+      }
+      if (lane > UT && lane < kNFLdp / 4) *reinterpret_cast<float4*>(trow + 4 * lane) = z4;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
         const int uu = lane + kWave * c;
         if (uu < UT) {
-          const float4 xr = make_float4(num[c].x * rc, num[c].y * rc, num[c].z * rc, num[c].w * rc);
+          const float4 xr = make_float4(ac[c].x * rc, ac[c].y * rc, ac[c].z * rc, ac[c].w * rc);
           if (live) {
             if (!(NF_ABL & 8)) st4(a.num_out + i * D + 4 * uu, xr);
             cmx[c] = bmax4(cmx[c], xr);
           }
-          float4 tv = num[c];
-          add4(tv, tp[c]);
+          float4 tv = *reinterpret_cast<const float4*>(trow + 4 * uu);
+          add4(tv, ac[c]);
           *reinterpret_cast<float4*>(trow + 4 * uu) = tv;
-        } else if (uu < kNFLdp / 4) {  // column D: the total weight sum w + sum P[D]; pads 0
-          const float add = uu == UT ? sw : 0.f;
-          const bool held = uu < UP;
-          *reinterpret_cast<float4*>(trow + 4 * uu) =
-              make_float4(held ? tp[c].x + add : 0.f, held ? tp[c].y : 0.f, held ? tp[c].z : 0.f,
-                          held ? tp[c].w : 0.f);
         }
       }
       // the A row as fp16 hi | lo, row-scaled, swizzled per row
@@ -3073,7 +3073,7 @@ extern "C" int mmb_mm2_stream_project_narrow_supported(int t, int d, int a_, int
   const int kq = (2 * a_ + 31) / 32 * 32 + (2 * vd + 31) / 32 * 32;
   return t > 0 && t <= kWave && d > 256 && d < kNFLdp && d % 4 == 0 && a_ >= 4 && vd >= 4 &&
          a_ <= 128 && vd <= 128 && a_ % 4 == 0 && vd % 4 == 0 && kq <= kNFK && v > 0 && v <= 16384 &&
-         v * kNFLdp * 4 < (int64_t{1} << 31) && static_cast<int64_t>(t) * (a_ > vd ? a_ : vd) * 4 < (int64_t{1} << 31);
+         v * (kNFLdq + 2) * 4 + 4 * kNFHot < (int64_t{1} << 31) && static_cast<int64_t>(t) * (a_ > vd ? a_ : vd) * 4 < (int64_t{1} << 31);
 }
 
 extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* table, int64_t v,
@@ -3103,7 +3103,7 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   s.num_out = num_out; s.aux_out = aux_out; s.flag = flag; s.s_half = 1;
   s.cmax_part = colmax ? static_cast<float*>(colmax_ws) : nullptr;
   f.ptab = static_cast<const float*>(text_cache);
-  f.hot_slot1 = reinterpret_cast<const int32_t*>(f.ptab + static_cast<size_t>(v) * kNFLdp);
+  f.hot_slot1 = reinterpret_cast<const int32_t*>(f.ptab + static_cast<size_t>(v) * kNFLdq);
   f.hot_ids = f.hot_slot1 + v;
   f.n_hot = static_cast<int>(v < kNFHot ? v : kNFHot);
   const int kq_t = (2 * d + 31) / 32 * 32;
