@@ -2646,6 +2646,14 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   float4* s_scr = reinterpret_cast<float4*>(s_ok + kNFRows);  // [waves][64] frame-slot sums
 
   const StreamArgs& a = f.s;
+  // (holding these pointers in VGPRs instead -- fewer SGPR spills -- measured
+  // slower: 4.21 vs 4.08 ms)
+  float* const num_out = a.num_out;
+  float* const aux_out = a.aux_out;
+  float* const mmb_out = f.out;
+  const int32_t* const ids_v = a.ids;
+  int32_t* const flag_v = a.flag;
+  const int V = static_cast<int>(a.V);  // <= 16384 (the text cache)
   constexpr int CT = 2;
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -2666,9 +2674,9 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   // one descriptor over the whole text cache: E | P rows | hot slots | hot
   // ids | the weights (mm2_kernels.hip); offset `cbytes` is past its end and
   // reads 0
-  const int hbase = static_cast<int>(a.V * kNFLdq * 4);              // hot_slot1
-  const int wbase = hbase + static_cast<int>(a.V * 4) + 4 * kNFHot;  // the weight copy
-  const int cbytes = wbase + static_cast<int>(a.V * 4);
+  const int hbase = V * kNFLdq * 4;              // hot_slot1
+  const int wbase = hbase + V * 4 + 4 * kNFHot;  // the weight copy
+  const int cbytes = wbase + V * 4;
   const auto prsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f.ptab), 0, cbytes, 0x00020000);
   // a token's E | P row: unit u = lane + 64 c of slot c (E units [0, UT),
   // P units [UT, NU)); slot 0 is all E, slot 1 E on lanes 64 + lane < UT and
@@ -2693,13 +2701,14 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   const int rpw = f.rpw;
   const int nbr = kNFWaves * rpw;  // rows of a batch
   const int nrt = (nbr + 15) / 16;  // MFMA row tiles holding them
-  auto row_of = [&](int64_t j, int u) -> int64_t {
-    return kNFWaves * rpw * (static_cast<int64_t>(blockIdx.x) + static_cast<int64_t>(gridDim.x) * j) +
-           rpw * wave + u;
+  // 32-bit rows and batches (N < 2^31: the launcher checks), 64-bit offsets
+  const int N = static_cast<int>(a.N), nb = static_cast<int>(f.nb);
+  auto row_of = [&](int j, int u) -> int {
+    return nbr * (static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) * j) + rpw * wave + u;
   };
-  auto ld_id = [&](int64_t i) -> int {
-    if (NF_ABL & 32) return (i < a.N && lane < L) ? static_cast<int>((lane * 131 + i) % a.V) : -1;
-    return (i < a.N && lane < L) ? a.ids[i * L + lane] : -1;
+  auto ld_id = [&](int i) -> int {
+    if (NF_ABL & 32) return (i < N && lane < L) ? (lane * 131 + i) % V : -1;
+    return (i < N && lane < L) ? ids_v[static_cast<int64_t>(i) * L + lane] : -1;
   };
   auto resolve = [&](int raw, int& rid, float& w, int& hs) {
     rid = -1;
@@ -2708,15 +2717,14 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
     if (NF_ABL & 32) {
       if (raw >= 0) rid = raw, w = 1.f;
     } else if (lane < L) {
-      int64_t id = raw;
-      const bool in = id >= 0 && id < a.V;
-      w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                        prsrc, in ? wbase + static_cast<int>(id) * 4 : cbytes, 0, 0));
-      if (id < 0) id += a.V;
-      if (id < 0 || id >= a.V) {
-        if (a.flag) atomicOr(a.flag, MMB_FLAG_ID_RANGE);
+      int id = raw;
+      const bool in = id >= 0 && id < V;
+      w = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(prsrc, in ? wbase + id * 4 : cbytes, 0, 0));
+      if (id < 0) id += V;
+      if (id < 0 || id >= V) {
+        if (flag_v) atomicOr(flag_v, MMB_FLAG_ID_RANGE);
       } else {
-        rid = static_cast<int>(id);
+        rid = id;
         hs = __builtin_amdgcn_raw_buffer_load_b32(prsrc, hbase + rid * 4, 0, 0);
       }
     }
@@ -2757,8 +2765,8 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
     }
   };
 
-  auto frame_rsrc = [&](int64_t i, const float* base, int W) {
-    const bool live = i < a.N;
+  auto frame_rsrc = [&](int i, const float* base, int W) {
+    const bool live = i < N;
     const int64_t ic = live ? i : 0;
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + ic * L * W), 0, live ? L * W * 4 : 0,
                                              0x00020000);
@@ -2776,13 +2784,13 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   float w_n;
   resolve(ld_id(row_of(0, 0)), rid_n, w_n, hs_n);
   __syncthreads();  // hot rows in LDS
-  for (int64_t j = 0; j < f.nb; j += 1) {
-    if (blockIdx.x + static_cast<int64_t>(gridDim.x) * j >= f.nb) break;
+  for (int j = 0; j < nb; j += 1) {
+    if (static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) * j >= nb) break;
     // ------------------------------------------------------------ stream phase
     for (int u = 0; u < rpw; ++u) {
-      const int64_t i = row_of(j, u);
+      const int i = row_of(j, u);
       const int r = rpw * wave + u;  // row in the batch
-      const bool live = i < a.N;
+      const bool live = i < N;
       const int rid = rid_n, hs = hs_n;
       const float w = w_n;
       raw = ld_id(u + 1 < rpw ? row_of(j, u + 1) : row_of(j + 1, 0));
@@ -2875,7 +2883,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       }
       const float cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w != 0.f)));
       const float sw = wave_sum(w);
-      if (live && lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+      if (live && lane == 0 && cnt == 0.f && flag_v) atomicOr(flag_v, MMB_FLAG_ZERO_WEIGHTS);
       for (int g0 = GA_MAX; g0 < GA; g0 += GA_MAX) frames(GAc{}, arsrc, voa, a.A, UA, PA, g0, sa, saa)();
       for (int g0 = GV_MAX; g0 < GV; g0 += GV_MAX) frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, g0, sv, svv)();
       // The A row [Sa | Saa | 0 | Sv | Svv] (K = 4 lane .. 4 lane + 3 on lane
@@ -2923,7 +2931,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
         if (uu < UT) {
           const float4 xr = make_float4(ac[c].x * rc, ac[c].y * rc, ac[c].z * rc, ac[c].w * rc);
           if (live) {
-            if (!(NF_ABL & 8)) st4(a.num_out + i * D + 4 * uu, xr);
+            if (!(NF_ABL & 8)) st4(num_out + static_cast<int64_t>(i) * D + 4 * uu, xr);
             cmx[c] = bmax4(cmx[c], xr);
           }
           float4 tv = *reinterpret_cast<const float4*>(trow + 4 * uu);
@@ -2946,9 +2954,9 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
         s_cnt[r] = cnt;
         s_ok[r] = live ? 1.f : 0.f;
         if (live && !(NF_ABL & 8)) {
-          a.aux_out[i] = cnt;
-          a.aux_out[a.N + i] = sw;
-          a.aux_out[2 * a.N + i] = rsc;
+          aux_out[i] = cnt;
+          aux_out[static_cast<int64_t>(N) + i] = sw;
+          aux_out[2 * static_cast<int64_t>(N) + i] = rsc;
         }
       }
     }
@@ -3031,7 +3039,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
     // wave w finishes rows rpw w .. rpw w + rpw - 1: / total (column D), L2 norm, store
     for (int u = 0; u < rpw; ++u) {
       const int r = rpw * wave + u;
-      const int64_t i = row_of(j, u);
+      const int i = row_of(j, u);
       const float* trow = sT + r * kNFLdp;
       const float rt = 1.f / trow[D];
       float4 y[CT];
@@ -3048,7 +3056,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
           const int uu = lane + kWave * c;
-          if (uu < UT) st4(f.out + i * D + 4 * uu, make_float4(y[c].x * inv, y[c].y * inv, y[c].z * inv, y[c].w * inv));
+          if (uu < UT) st4(mmb_out + static_cast<int64_t>(i) * D + 4 * uu, make_float4(y[c].x * inv, y[c].y * inv, y[c].z * inv, y[c].w * inv));
         }
       }
     }
@@ -3083,7 +3091,7 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
                                              const float* c0, float* num_out, float* aux_out,
                                              float* mmb2_out, int32_t* flag, uint32_t* colmax,
                                              void* colmax_ws, hipStream_t stream) {
-  MMB_REQUIRE(n >= 0 && mmb_mm2_stream_project_narrow_supported(t, d, a_, vd, v));
+  MMB_REQUIRE(n >= 0 && n < (int64_t{1} << 31) - kNFRows && mmb_mm2_stream_project_narrow_supported(t, d, a_, vd, v));
   MMB_REQUIRE(ids && table && wtab32 && text_cache && audio && visual && num_out && aux_out &&
               mmb2_out && wpieces && c0);
   MMB_REQUIRE(colmax == nullptr || colmax_ws != nullptr);
