@@ -3041,7 +3041,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       const int r = rpw * wave + u;
       const int i = row_of(j, u);
       const float* trow = sT + r * kNFLdp;
-      const float rt = 1.f / trow[D];
+      const float rt = __builtin_amdgcn_rcpf(trow[D]);  // v_rcp_f32 (1 ulp): the MMB2 bar is 2e-6
       float4 y[CT];
       float ss = 0.f;
 #pragma unroll
@@ -3051,7 +3051,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
         y[c] = make_float4(y[c].x * rt, y[c].y * rt, y[c].z * rt, y[c].w * rt);
         if (uu < UT) ss += y[c].x * y[c].x + y[c].y * y[c].y + y[c].z * y[c].z + y[c].w * y[c].w;
       }
-      const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
+      const float inv = __builtin_amdgcn_rsqf(wave_sum_dpp_f32(ss));  // v_rsq_f32 (1 ulp)
       if (s_ok[r] != 0.f && !(NF_ABL & 16)) {
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
