@@ -77,6 +77,16 @@ __device__ __forceinline__ float wave_sum_dpp_f32(float v) {
   auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
   return (rl(0) + rl(16)) + (rl(32) + rl(48));
 }
+// 64-lane max (exact in any order) by DPP within rows + readlane: no
+// ds_bpermute round trips (wave-uniform result; fmaxf drops NaN)
+__device__ __forceinline__ float wave_max_dpp_f32(float v) {
+  v = fmaxf(v, dpp_f32<kDppQuad1032>(v));
+  v = fmaxf(v, dpp_f32<kDppQuad2301>(v));
+  v = fmaxf(v, dpp_f32<kDppRowHalfMirror>(v));
+  v = fmaxf(v, dpp_f32<kDppRowMirror>(v));
+  auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+  return fmaxf(fmaxf(rl(0), rl(16)), fmaxf(rl(32), rl(48)));
+}
 // Broadcast of lane l's double (l wave-uniform): two v_readlane, no LDS.
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const unsigned long long u = __double_as_longlong(v);

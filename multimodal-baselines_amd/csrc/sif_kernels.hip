@@ -2882,7 +2882,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
         }
       }
       const float cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w != 0.f)));
-      const float sw = wave_sum(w);
+      const float sw = wave_sum_dpp_f32(w);  // (DPP row sums: another order than wave_sum's)
       if (live && lane == 0 && cnt == 0.f && flag_v) atomicOr(flag_v, MMB_FLAG_ZERO_WEIGHTS);
       for (int g0 = GA_MAX; g0 < GA; g0 += GA_MAX) frames(GAc{}, arsrc, voa, a.A, UA, PA, g0, sa, saa)();
       for (int g0 = GV_MAX; g0 < GV; g0 += GV_MAX) frames(GVc{}, vrsrc, vov, a.Vd, UV, PV, g0, sv, svv)();
@@ -2906,7 +2906,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       gather(saa, UA, PA, UA);
       gather(sv, UV, PV, f.kq_a >> 2);
       gather(svv, UV, PV, (f.kq_a >> 2) + UV);
-      const float rsc = row_scale(wave_max(amax4(av)));
+      const float rsc = row_scale(wave_max_dpp_f32(amax4(av)));
       resolve(raw, rid_n, w_n, hs_n);  // the next utterance's
       // x (the a2 row), column bounds, aux; the text term T into LDS
       const float rc = 1.f / cnt;

@@ -870,8 +870,9 @@ def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
     projection from the text cache, hot words from LDS, 32-utterance batches,
     the audio / visual GEMM in-launch) against the two-kernel narrow step
     (utt_narrow_kernel -> HBM s -> mmb_mm2_project_x3) on the same inputs:
-    count and weight sum bit-identical; x to f32 rounding (the fused kernel
-    sums an utterance's hot words first, then its cold words); the PC equal to
+    count identical, weight sum and x to f32 rounding (the fused kernel sums
+    an utterance's hot words first, then its cold words; its weight sum by
+    DPP rows); the PC equal to
     the sklearn-path restatement's on the fused step's own x; the MMB2 rows
     to f32 rounding (another grouping of the same closed form) and both
     within the bar of the CPU oracle.  Partial and single-row batches,
@@ -899,7 +900,9 @@ def test_narrow_fused_matches_two_kernel_step(gpu, N, T, A, Vd, V):
     s2, m2 = b.run()
     torch.cuda.synchronize()
     assert int(a.flag.item()) == int(b.flag.item()) == 0
-    assert torch.equal(a.aux[:2], b.aux[:2])
+    # count exact; the weight sum is a 64-lane f32 sum in another order (DPP rows)
+    assert torch.equal(a.aux[0], b.aux[0])
+    assert torch.allclose(a.aux[1], b.aux[1], rtol=1e-6, atol=0)
     assert M.row_rel_err(a.x.cpu().numpy(), b.x.cpu().numpy()) < 2e-6
     if N >= 300:  # sklearn's direct randomized-SVD branch
         pc_sk = O.compute_pc(a.x.double().cpu().numpy())
