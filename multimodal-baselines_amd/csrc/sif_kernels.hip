@@ -1443,7 +1443,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
       float mx = 0.f;
 #pragma unroll
       for (int c = 0; c < 2; ++c) mx = fmaxf(mx, fmaxf(amax4(sx[c]), amax4(sxx[c])));
-      const float rs = row_scale(wave_max(mx));
+      const float rs = row_scale(wave_max_dpp_f32(mx));
       if (m == 0) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -1652,7 +1652,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
             for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
             if constexpr (TEXT) {
-              cnt = wave_sum((w_c != 0.f) ? 1.f : 0.f);
+              cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w_c != 0.f)));
               sw = wave_sum(w_c);
               // every weight 0: x is 0/0 = NaN (numpy's answer); TruncatedSVD
               // would reject the split -- report it through the flag word
@@ -1801,7 +1801,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
             for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
             if constexpr (TEXT) {
-              cnt = wave_sum((w_c != 0.f) ? 1.f : 0.f);
+              cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w_c != 0.f)));
               sw = wave_sum(w_c);
               // every weight 0: x is 0/0 = NaN (numpy's answer); TruncatedSVD
               // would reject the split -- report it through the flag word

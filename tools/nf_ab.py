@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--workload", choices=["mosi", "synthetic"], default="mosi",
+                    help="synthetic: the headline configs[3] step (T 40, 3 x 300-d, V 400k)")
     args = ap.parse_args()
     mmb_lib.load(os.path.abspath(args.lib))
     import torch
@@ -31,10 +33,15 @@ def main():
     import pipeline as P
     import synth
     dev = torch.device("cuda:0")
-    inp = synth.device_workload(args.n, 20, 3016, D=300, A=76, Vd=48, seed=4000, device=dev)
+    if args.workload == "mosi":
+        T, V, A, Vd = 20, 3016, 76, 48
+        inp = synth.device_workload(args.n, T, V, D=300, A=A, Vd=Vd, seed=4000, device=dev)
+    else:
+        T, V, A, Vd = 40, 400_000, 300, 300
+        inp = synth.device_shard(0, args.n, T, V, D=300, A=A, Vd=Vd, seed=1000, device=dev)
     torch.manual_seed(0)
-    gen = models.AudioVisualGeneratorMultimodal(300, 76, 48, norm=None).to(dev)
-    step = P.FusedStep(inp, gen.networks(), narrow_fused=True)
+    gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(dev)
+    step = P.FusedStep(inp, gen.networks(), narrow_fused=args.workload == "mosi")
     for _ in range(3):
         step.run()
     torch.cuda.synchronize()
@@ -48,11 +55,11 @@ def main():
         step.check()
     except Exception as e:  # timing-only ablations (NF_ABL) compute no valid step
         print(f"# {os.path.basename(args.lib)} check: {type(e).__name__}", flush=True)
-    kn = "mm2_stream_project_narrow"
+    kn = "mm2_stream_project_narrow" if args.workload == "mosi" else "mm2_stream_project"
     kms = sum(a.elapsed_time(b) for tr in traces for a, b in tr.get(kn, ())) / args.steps
     line = f"{os.path.basename(args.lib)} kernel_ms {kms:.4f} step_ms {ms:.4f}"
     if args.check:
-        b = P.FusedStep(inp, gen.networks(), narrow_fused=False)
+        b = P.FusedStep(inp, gen.networks(), narrow_fused=False, stream_project=False)
         b.run(check=True)
         torch.cuda.synchronize()
         dx = ((step.x - b.x).abs().amax(1) / b.x.abs().amax(1).clamp_min(1e-30)).max().item()
