@@ -1653,7 +1653,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
             if constexpr (TEXT) {
               cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w_c != 0.f)));
-              sw = wave_sum(w_c);
+              sw = wave_sum_dpp_f32(w_c);
               // every weight 0: x is 0/0 = NaN (numpy's answer); TruncatedSVD
               // would reject the split -- report it through the flag word
               if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
@@ -1802,7 +1802,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
             for (int c = 0; c < 2; ++c) num[c] = sx[c] = sxx[c] = z4;
             if constexpr (TEXT) {
               cnt = static_cast<float>(__builtin_popcountll(__builtin_amdgcn_ballot_w64(w_c != 0.f)));
-              sw = wave_sum(w_c);
+              sw = wave_sum_dpp_f32(w_c);
               // every weight 0: x is 0/0 = NaN (numpy's answer); TruncatedSVD
               // would reject the split -- report it through the flag word
               if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
