@@ -2615,7 +2615,9 @@ constexpr int kNFCT = kNFLdp / 16;          // 16-column tiles of y and the tota
 constexpr size_t kNFLdsRows = sizeof(float) * (kNFHot * kNFHotRow + kNFRows * kNFLdp) +
                               sizeof(_Float16) * kNFRows * 2 * kNFK + sizeof(float) * 3 * kNFRows;
 static_assert(kNFLdsRows % 16 == 0, "the frame-slot scratch is float4-aligned");
-constexpr size_t kNFLds = kNFLdsRows + 16 * kWave * kNFWaves;  // + 1 KB per wave: frame-slot sums
+// + 1 KB per wave for the frame-slot sums (12 waves: the utterance's own T
+// row, free until T is written, holds them instead)
+constexpr size_t kNFLds = kNFLdsRows + (kNFWaves == 8 ? 16 * kWave * kNFWaves : 0);
 
 struct NarrowFusedArgs {
   StreamArgs s;        // ids, table, V, wtab, audio, visual, N, L, D, A, Vd, num_out, aux_out, flag, cmax_part
@@ -2890,7 +2892,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       // `lane`): each frame sum's P row slots added up through this wave's 1
       // KB of LDS (one write, P reads by the lanes holding that piece; slot 0
       // first, as the shuffle reduction of utt_narrow_kernel); pads 0
-      float4* scr = s_scr + wave * kWave;
+      float4* scr = kNFWaves == 8 ? s_scr + wave * kWave : reinterpret_cast<float4*>(sT + r * kNFLdp);
       float4 av = z4;
       auto gather = [&](const float4& acc, int U, int P, int u0) {
         __builtin_amdgcn_wave_barrier();  // the previous piece's reads are issued
@@ -2906,6 +2908,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       gather(saa, UA, PA, UA);
       gather(sv, UV, PV, f.kq_a >> 2);
       gather(svv, UV, PV, (f.kq_a >> 2) + UV);
+      __builtin_amdgcn_wave_barrier();  // (12 waves: the T row is written below)
       const float rsc = row_scale(wave_max_dpp_f32(amax4(av)));
       resolve(raw, rid_n, w_n, hs_n);  // the next utterance's
       // x (the a2 row), column bounds, aux; the text term T into LDS

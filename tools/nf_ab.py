@@ -63,7 +63,8 @@ def main():
         b.run(check=True)
         torch.cuda.synchronize()
         dx = ((step.x - b.x).abs().amax(1) / b.x.abs().amax(1).clamp_min(1e-30)).max().item()
-        line += f" x_row_rel {dx:.2e}"
+        dm = ((step.mmb2 - b.mmb2).abs().amax(1) / b.mmb2.abs().amax(1).clamp_min(1e-30)).max().item()
+        line += f" x_row_rel {dx:.2e} mmb2_row_rel {dm:.2e}"
     print(line, flush=True)
 
 
