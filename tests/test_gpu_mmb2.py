@@ -517,8 +517,8 @@ def test_gpu2_rejects_combinations_that_are_not_concatenations(gpu, golden):
 def test_full_size_step_sampled_rows_vs_oracle(gpu, T, V, A, Vd):
     """BASELINE configs[3] at full size (1M utterances x 40 x 3 x 300-d, V =
     400k, Zipf ids) and configs[1] at 1M utterances of MOSI shape (T = 20,
-    COVAREP 76, FACET 48, V = 3016: the two-kernel step with the narrow-frame
-    stream kernel): the bench step itself, checked against the oracle where
+    COVAREP 76, FACET 48, V = 3016: the narrow fused kernel with the per-word
+    text projection cache): the bench step itself, checked against the oracle where
     the check is size-independent.  MMB2 rows are per-utterance: 512 sampled
     rows against the oracle's sif2.estimate_embedding_overall_gpu2 on those
     rows (1e-5).  The SIF a2 rows of the sample against the oracle's
