@@ -661,7 +661,7 @@ extern "C" int mmb_layer_norm_backward(const float* dy, const float* x, const fl
   if (n == 0) {  // (empty tensors may hand over null row pointers)
     for (float* p : {dgamma, dbeta}) {
       if (!p) continue;
-      const hipError_t e = hipMemsetAsync(p, 0, sizeof(float) * d, stream);
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(p, static_cast<int64_t>(sizeof(float) * d) / 4, stream));
       if (e != hipSuccess) return static_cast<int>(e);
     }
     return MMB_OK;

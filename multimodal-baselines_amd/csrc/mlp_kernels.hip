@@ -265,18 +265,21 @@ __global__ __launch_bounds__(kTrNT) void mlp_train_mc_kernel(TrainArgs a) {
     }
     __syncthreads();
     if (tid == 0) {
-      __hip_atomic_fetch_add(a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old = __hip_atomic_fetch_add(a.ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned target = static_cast<unsigned>(a.P) * (xc + 1);
+      // exchange xc's arrivals find the counter in [P xc, P (xc + 1)); any
+      // other count is a workspace handed over dirty: abort (as pm_arrive)
       bool ok = false;
-      for (int it = 0; it < (1 << 21); ++it) {
+      const bool counted = old >= target - static_cast<unsigned>(a.P) && old < target;
+      for (int it = 0; counted && it < (1 << 21); ++it) {
+        if (__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         if (__hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
           ok = true;
           break;
         }
-        if (__hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         __builtin_amdgcn_s_sleep(1);
       }
-      if (!ok) {  // ~1 s without the other workgroups (or one of them gave up)
+      if (!ok) {  // ~1 s without the other workgroups, one of them gave up, or a dirty count
         __hip_atomic_store(a.ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.flag) atomicOr(a.flag, MMB_FLAG_SYNC_TIMEOUT);
         s_abort = 1;
@@ -685,6 +688,27 @@ static int launch_train_mc(const TrainArgs& a, size_t lds, hipStream_t stream) {
     if (e != hipSuccess) return static_cast<int>(e);
     attr_set = lds;
   }
+  // the P workgroups wait on each other every mini-batch, so they must be
+  // resident together: check the occupancy the device gives this kernel, and
+  // launch cooperatively where the device supports it (the runtime then
+  // refuses a grid that cannot be co-resident instead of dispatching part of
+  // it behind other work; the bounded waits stay as the last line)
+  int dev = 0, n_cu = 0, per_cu = 0, coop = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
+  if (e == hipSuccess)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&mlp_train_mc_kernel<NTD>), kTrNT, lds);
+  if (e != hipSuccess) return static_cast<int>(e);
+  if (static_cast<int64_t>(per_cu) * n_cu < a.P) return MMB_EINVAL;
+  if (coop) {
+    TrainArgs arg = a;
+    void* args[] = {&arg};
+    e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&mlp_train_mc_kernel<NTD>),
+                                   dim3(a.P), dim3(kTrNT), args, static_cast<unsigned>(lds), stream);
+    return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+  }
   mlp_train_mc_kernel<NTD><<<a.P, kTrNT, lds, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
@@ -809,7 +833,7 @@ extern "C" int mmb_mlp_backward(const float* x, const float* hid, int64_t b, int
     float* outs[4] = {dw1, db1, dw2, db2};
     for (int q = 0; q < 4; ++q) {
       if (!outs[q]) continue;
-      const hipError_t e = hipMemsetAsync(outs[q], 0, nbytes[q], stream);
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(outs[q], static_cast<int64_t>(nbytes[q]) / 4, stream));
       if (e != hipSuccess) return static_cast<int>(e);
     }
     return MMB_OK;

@@ -135,6 +135,14 @@ __host__ __device__ constexpr int x3_swz(int r) { return (0x78 >> (2 * ((r >> 2)
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Zero n 32-bit words with a kernel (probe_kernels.hip).  Used wherever the
+// library must clear a buffer on the caller's stream: a hipMemsetAsync
+// captured into a HIP graph wrote address-like garbage into its destination
+// on every replay after the first (r05, tools/dbg/replay_cause.py:
+// gpurun_out r05a -- the PC solve's control words read [0x14ABxxxx, 0x7BE2]),
+// so no entry point enqueues a memset node.  Returns 0 or a hipError_t.
+int zero_words_async(void* p, int64_t n, hipStream_t stream);
+
 // CUs a launch on `stream` can use: the device's, or the subset a stream made
 // by hipExtStreamCreateWithCUMask is restricted to (sif_kernels.hip).
 int stream_cu_count(hipStream_t stream);

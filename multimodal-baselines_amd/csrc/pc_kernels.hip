@@ -1554,11 +1554,30 @@ __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned
   constexpr int iters = 1 << 20;
 #endif
   for (int it = 0; it < iters; ++it) {
+    // the abort word first: a set word (another workgroup gave up, or a
+    // workspace handed over dirty) ends the wait even where the count is met
+    if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     __builtin_amdgcn_s_sleep(4);
   }
-  // ~0.5-1 s without the other workgroups: give up, release every waiter
+  // ~0.5-1 s without the other workgroups, or an abort seen: give up, release
+  // every waiter, and say so in the flag word whichever way the abort came (a
+  // launch that found the word already set would otherwise leave only a NaN PC)
+  __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (flag) atomicOr(flag, MMB_FLAG_SYNC_TIMEOUT);
+  return false;
+}
+
+// An arrival of round r must find the counter in [T r, T (r + 1)): every
+// workgroup arrives at round r only after seeing T r arrivals, and no
+// workgroup arrives at round r + 1 before all T of round r have.  A count
+// outside that range is a counter this launch did not start from zero (a
+// workspace handed over dirty): abort like a timeout instead of letting the
+// waits pass before the other workgroups' tiles are written.
+__device__ __forceinline__ bool pm_arrive(unsigned* ctr, int T, int r, unsigned* abort_w,
+                                          int32_t* flag) {
+  const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old >= static_cast<unsigned>(T * r) && old < static_cast<unsigned>(T * (r + 1))) return true;
   __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (flag) atomicOr(flag, MMB_FLAG_SYNC_TIMEOUT);
   return false;
@@ -1787,15 +1806,15 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
         // release: the tile stores above are visible at agent scope before
         // the arrival that announces them
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!(last && t != 0)) {
+        if (!pm_arrive(ctr, T, r, abort_w, flag)) {
+          s_abort = 1;
+        } else if (!(last && t != 0)) {
           if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) {
             s_abort = 1;
           } else if (last) {
             // every workgroup has made its last arrival: the counter is free
-            // again, so the next launch finds it at 0 even where the launcher's
-            // memset is not what it reads first (graph replays, r04: the
-            // second replay of a captured step saw the last launch's count)
+            // again, so the next launch (eager or a graph replay) finds it at
+            // 0 with no memset node in front of it
             __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           // acquire: the gather below reads the other workgroups' tiles only
@@ -2199,7 +2218,7 @@ extern "C" int mmb_colmax(const float* x, int64_t n, int d, uint32_t* colmax, in
                           hipStream_t stream) {
   MMB_REQUIRE(x && colmax && n >= 0 && d > 0);
   if (!accumulate) {
-    const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+    const hipError_t e = static_cast<hipError_t>(zero_words_async(colmax, static_cast<int64_t>(sizeof(uint32_t) * d) / 4, stream));
     if (e != hipSuccess) return static_cast<int>(e);
   }
   if (n == 0) return MMB_OK;

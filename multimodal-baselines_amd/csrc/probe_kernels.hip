@@ -8,6 +8,8 @@
 //   probe_copy_kernel: dst = src            (read + write bytes)
 //   probe_read_kernel: sink[block] = f(src) (read bytes; a per-block XOR of
 //                      the words keeps the loads alive)
+#include <algorithm>
+
 #include "mmb_common.h"
 
 namespace mmb {
@@ -83,7 +85,23 @@ int probe_grid(int64_t n4, int blocks) {
   return static_cast<int>(need < blocks ? (need > 0 ? need : 1) : blocks);
 }
 
+__global__ void zero_words_kernel(uint32_t* p, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    p[i] = 0u;
+}
+
 }  // namespace
+
+// (declared in mmb_common.h: the library's graph-safe replacement of
+// hipMemsetAsync)
+int zero_words_async(void* p, int64_t n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const int grid = static_cast<int>(std::min<int64_t>(ceil_div(n, 256), 1024));
+  zero_words_kernel<<<grid, 256, 0, stream>>>(static_cast<uint32_t*>(p), n);
+  return static_cast<int>(hipGetLastError());
+}
+
 }  // namespace mmb
 
 using namespace mmb;

@@ -1252,7 +1252,7 @@ __device__ __forceinline__ void text_piece(const StreamArgs& a, int64_t i, int l
     rid = off < 0 ? -1 : (gather ? static_cast<int>(off / a.D) : lane);
   }
   cnt = wave_sum((w != 0.f) ? 1.f : 0.f);
-  sw = wave_sum(w);
+  sw = wave_sum_dpp_f32(w);  // DPP rows, as the pipelined streamers (bit-identical variants)
   if (lane == 0 && cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -2406,7 +2406,7 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   }
   if (n == 0) {
     if (colmax) {
-      const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(colmax, static_cast<int64_t>(sizeof(uint32_t) * d) / 4, stream));
       if (e != hipSuccess) return static_cast<int>(e);
     }
     return MMB_OK;
@@ -2491,7 +2491,7 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   MMB_REQUIRE(aligned16(audio) && aligned16(visual) && aligned16(num_out) && aligned16(wpieces));
   if (n == 0) {
     if (colmax) {
-      const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(colmax, static_cast<int64_t>(sizeof(uint32_t) * d) / 4, stream));
       if (e != hipSuccess) return static_cast<int>(e);
     }
     return MMB_OK;
@@ -3102,7 +3102,7 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
               aligned16(num_out) && aligned16(mmb2_out) && aligned16(wpieces));
   if (n == 0) {
     if (colmax) {
-      const hipError_t e = hipMemsetAsync(colmax, 0, sizeof(uint32_t) * d, stream);
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(colmax, static_cast<int64_t>(sizeof(uint32_t) * d) / 4, stream));
       if (e != hipSuccess) return static_cast<int>(e);
     }
     return MMB_OK;

@@ -30,9 +30,10 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     return row0, base + (1 if rank < rem else 0)
 
 
-def init(backend: str | None = None):
+def init(backend: str | None = None, force_group: bool = False):
     """Initialise the default process group from the torchrun environment.
-    Returns (rank, world, device)."""
+    Returns (rank, world, device).  A world of one rank gets no group unless
+    `force_group` (tests: RCCL itself exercised on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -43,15 +44,19 @@ def init(backend: str | None = None):
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_group) and not dist.is_initialized():
         kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
     return rank, world, dev
 
 
-def allreduce_sum(group=None):
-    """In-place SUM all-reduce of one tensor (no-op without a process group)."""
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+def allreduce_sum(group=None, force: bool = False):
+    """In-place SUM all-reduce of one tensor.  None (nothing to reduce)
+    without a process group or with one rank, unless `force`: then the
+    collective runs even at world size 1 (tests put RCCL on the step's path)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    if dist.get_world_size(group) == 1 and not force:
         return None
 
     def _ar(t: torch.Tensor):

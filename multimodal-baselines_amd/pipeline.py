@@ -396,13 +396,20 @@ class MMB2Projection:
         """Also keep the text cache of the narrow fused step
         (mmb_mm2_text_cache: P = E Wm_t1 + E^2 Wm_t2 per word, f64 rounded
         once, and the hot-word ranks), rebuilt with every re-merge and when
-        the word or weight table changes."""
-        if getattr(self, "text_cache", None) is None or self.text_src[0] is not table:
+        the word or weight table changes.  The narrow fused kernel reads the
+        token weights from the cache's own copy, so the cache is keyed on BOTH
+        tensors (identity here, storage address + version counter in
+        refresh_if_changed); writes into them that bump neither (raw-pointer
+        writes by other libmmb kernels, `t.data.copy_`) need invalidate()."""
+        src = getattr(self, "text_src", None)
+        if (getattr(self, "text_cache", None) is None or src[0] is not table
+                or src[1] is not wtab32):
             self.enable_pieces()
             V = table.shape[0]
-            nbytes = L.query("mmb_mm2_text_cache_bytes", V, self.d)
-            self.text_cache = torch.empty((nbytes + 15) // 16 * 16, dtype=torch.uint8,
-                                          device=table.device)
+            nbytes = (L.query("mmb_mm2_text_cache_bytes", V, self.d) + 15) // 16 * 16
+            old = getattr(self, "text_cache", None)
+            if old is None or old.numel() != nbytes or old.device != table.device:
+                self.text_cache = torch.empty(nbytes, dtype=torch.uint8, device=table.device)
             self.text_src = (table, wtab32)
             self._build_text_cache()
             self._seen = self._versions()
@@ -784,8 +791,12 @@ class FusedStep:
             t = torch.stack([(flag[0] & b) != 0 for b in bits]).to(torch.int32)
             self.allreduce(t)
             flag = sum((t[i] > 0).to(torch.int32) * b for i, b in enumerate(bits)).reshape(1)
-        if int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT and self.solve_ws is not None:
-            self.solve_ws[:16].zero_()  # an aborted solve leaves its control words set
+        pc = getattr(self, "pc", None)
+        if self.solve_ws is not None and (int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT or (
+                pc is not None and not bool(torch.isfinite(pc).all()))):
+            # an aborted solve leaves its control words set (and a NaN PC):
+            # hand the next launch a zeroed workspace again
+            self.solve_ws[:16].zero_()
         check_flag(flag, self.V, zero_weights=True)
         if getattr(self, "pc", None) is not None:
             check_pc_finite(self.pc)
@@ -979,6 +990,10 @@ class StepGraph:
         caller.wait_stream(side)
         torch.cuda.synchronize(dev)
         for st in self.steps:
+            # the warm-up's verdict first: a flag (or an aborted solve's NaN
+            # PC) raises here instead of being cleared by reset() and leaving
+            # every replay to run on a dirty workspace
+            st.check()
             st.reset()
         self._branches = ([torch.cuda.Stream(device=dev) for _ in self.steps]
                           if concurrent and len(self.steps) > 1 else None)

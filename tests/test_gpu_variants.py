@@ -2,9 +2,10 @@
 
 The product library carries only the default kernels and reads no
 environment variable (`strings libmmb.so` has no MMB_* knob); the variants
-and timing-only ablations live in tools/diag/libmmb_diag.so (`make diag`, on
-request: build() does not make it and .gpurunignore keeps it off the GPU box
-unless a tools session asks for it -- these tests skip without it).  Each group
+and timing-only ablations live in tools/diag/libmmb_diag.so (`make diag`;
+__graft_entry__.build() makes it beside libmmb.so and it travels to the GPU
+box with the tree -- a missing tools build FAILS these tests rather than
+skipping them, so the timeout path is part of every GPU run).  Each group
 of tests/variant_checks.py runs in ONE child process that loads that build
 explicitly; the fused-streamer group also dumps the group-at-a-time
 streamer's outputs, which the product library (this process) must reproduce
@@ -23,12 +24,12 @@ import variant_checks as VC
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DIAG = VC.DIAG_LIB
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(not os.path.exists(DIAG),
-                                 reason="tools build absent (make -C multimodal-baselines_amd/csrc diag)")]
+pytestmark = pytest.mark.gpu
 
 
 def _child(group, tmp_path):
+    assert os.path.exists(DIAG), ("tools build absent: make -C multimodal-baselines_amd/csrc diag "
+                                  "(__graft_entry__.build() makes it)")
     env = {**os.environ, "VARIANT_DUMP": str(tmp_path)}
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "variant_checks.py"),
                         group], env=env, capture_output=True, text=True, timeout=600)
