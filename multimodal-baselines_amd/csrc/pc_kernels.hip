@@ -15,6 +15,9 @@
 //     iterations, then v = Z u with u the top eigenvector of Z^T G Z;
 //   * svd_flip(u_based_decision=False): largest-|.| entry of each component > 0.
 // The removal pass x - (x.pc) pc runs in f64 like the reference (:77-80).
+#include <algorithm>
+#include <vector>
+
 #include "mmb_common.h"
 
 namespace mmb {
@@ -515,6 +518,232 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ Gram i8, range level sums (r05)
+// The same digits and the same 13 digit-pair products as gram_i8_kernel, but
+// each of the five levels l = a + b is summed in its OWN int32 accumulator
+// over the workgroup's whole row range, and the range's f64 partial is formed
+// once at the end:  S = (((L0 2^8 + L1) 2^8 + L2) 2^8 + L3) 2^8 + L4 (exact in
+// f64 up to the last step, which rounds once), G_part = S 2^(e_i + e_j - 44).
+// gram_i8_kernel shifted and combined the levels into three words per 64-row
+// k-step and added them to f64 accumulators: per tile and k-step 8 shifts,
+// 12 conversions and 12 f64 FMAs beside the 13 MFMAs -- with the digit
+// slicing, ~700 vector instructions per wave and chunk against 156 MFMAs, a
+// kernel bound by vector issue (0.76 ms at 1M x 300), not by the matrix pipe
+// (~0.3 ms of MFMA work).  Here the k-step loop issues the MFMAs, their
+// operand reads and the slicing only.
+// Exactness: per 64-row k-step |L0| <= 64 * 64 * 64 = 2^18, |L1| <= 2^20,
+// |L2| <= 2^21, |L3|, |L4| <= 2^21.6, so int32 level sums are exact for 512
+// k-steps: a range holds at most kGlMaxRows = 32768 rows (gram_i8l_plan).
+// Registers: 5 levels x 4 words per 16x16 tile, so a workgroup holds fewer
+// tiles than gram_i8_kernel's pairs: THREE workgroups per row range (on one
+// XCD: the range's x is read from HBM once), each a contiguous run of the
+// row-major triangle (<= 64 tiles, <= 8 per wave), split on the host so that
+// the vector work -- a part slices only the features its tiles touch, from
+// its first tile row on -- and the MFMA work balance (gram_i8l_split).
+constexpr int kGlLev = 5;
+constexpr int64_t kGlMaxRows = 512 * kGiRows;        // int32 level sums exact
+constexpr int kGlMaxParts = 4;
+
+// tile bounds of the parts: part p owns [b[p], b[p + 1]) of the row-major triangle
+struct GlParts {
+  int b[kGlMaxParts + 1];
+};
+
+// Shape of a level-sum kernel: P workgroups per row range, NW waves each, at
+// most MT tiles per wave (P * NW * MT >= 190 tiles at d = 300).
+template <int P, int NW, int MT>
+struct GlShape {
+  static constexpr int kP = P, kNW = NW, kMT = MT, kNT = NW * kWave;
+  static constexpr int kPartMax = NW * MT;
+  static constexpr int kIt = (kGiItems + kNT - 1) / kNT;  // slicing items per thread
+  // item u is sliced after tile slice_at(u): spread over the tile loop
+  static constexpr int slice_at(int u) { return (u * MT) / kIt + MT / kIt - 1; }
+};
+
+// DIAG (timing-only builds, wrong results; MMB_GRAM_DIAG with the level-sum
+// kernel): bit 0 no MFMAs (operands kept live), bit 2 no slicing, bit 3 no x loads
+template <int DIAG, class S>
+__global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restrict__ x,
+                                                         const unsigned* __restrict__ colmax,
+                                                         int64_t N, int D, int nt, int64_t chunk,
+                                                         int xcd_map, GlParts parts,
+                                                         double* __restrict__ part) {
+  constexpr int MT = S::kMT, NT = S::kNT, kIt = S::kIt;
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dig[];  // [2][4][kGiF][64]
+  const int T = nt * (nt + 1) / 2;
+  int range, p;
+  if (xcd_map) {  // the P parts of a range on one XCD (round-robin dispatch: b % 8)
+    const int b = blockIdx.x, s = b >> 3;
+    range = (b & 7) + 8 * (s / S::kP);
+    p = s % S::kP;
+  } else {
+    range = blockIdx.x / S::kP;
+    p = blockIdx.x % S::kP;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int t0 = parts.b[p], t1 = parts.b[p + 1];
+  if (t1 <= t0) return;  // an empty part (tiny d)
+  const int per = (t1 - t0 + S::kNW - 1) / S::kNW;
+  const int q0 = t0 + wave * per;
+  int ti[MT], tj[MT];
+  int ntl = 0;
+#pragma unroll
+  for (int q = 0; q < MT; ++q) {
+    ti[q] = tj[q] = 0;
+    if (q < per && q0 + q < t1) {
+      tri_tile(q0 + q, nt, ti[q], tj[q]);
+      ntl = q + 1;
+    }
+  }
+  i32x4 lev[MT][kGlLev];
+#pragma unroll
+  for (int q = 0; q < MT; ++q)
+#pragma unroll
+    for (int l = 0; l < kGlLev; ++l) lev[q][l] = i32x4{0, 0, 0, 0};
+
+  const int64_t r0 = range * chunk;
+  const int64_t r1 = min(N, r0 + chunk);
+  const int nchunks = static_cast<int>(r1 > r0 ? (r1 - r0 + kGiRows - 1) / kGiRows : 0);
+  // features this part reads: its first tile row on (tj >= ti >= that row)
+  int tr0, tc0;
+  tri_tile(t0, nt, tr0, tc0);
+  const int f_lo = 16 * tr0;
+  const int nf = nt * 16 - f_lo;
+  const int nitems = nf * 4;
+  // item it = (f - f_lo) + nf * kq: feature f, rows 16 kq .. 16 kq + 15 of the
+  // chunk; packed (f | kq << 9 | (e + 256) << 11) with its row offset beside
+  int it_pk[kIt], it_off[kIt];
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int it = tid + NT * u;
+    const int f = it < nitems ? f_lo + it % nf : 0;
+    const int kq = it < nitems ? it / nf : 0;
+    const int e = (it < nitems && f < D) ? gi_exp(colmax[f]) : 0;
+    it_pk[u] = f | (kq << 9) | ((e + 256) << 11);
+    // padding features / missing items read past the record count: 0
+    it_off[u] = (it < nitems && f < D) ? (kq * 16 * D + f) * 4 : 0x7ffffff0;
+  }
+  const int nrec = __builtin_amdgcn_readfirstlane(static_cast<int>((r1 > r0 ? r1 - r0 : 0) * D * 4));
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + r0 * D), 0, nrec, 0x00020000);
+  float xv[kIt][16];
+  auto load = [&](int c) {
+    if constexpr ((DIAG & 8) != 0) {
+#pragma unroll
+      for (int u = 0; u < kIt; ++u)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(xv[u][j]));
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
+#pragma unroll
+      for (int u = 0; u < kIt; ++u)
+        xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
+    }
+  };
+  auto slice_item = [&](int u, unsigned char* buf) {
+    if constexpr ((DIAG & 4) != 0) return;
+    const int it = tid + NT * u;
+    if (it < nitems) {
+      const int f = it_pk[u] & 511, kq = (it_pk[u] >> 9) & 3, e = (it_pk[u] >> 11) - 256;
+      unsigned w[4][kGiDig];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        gi_planes(gi_vbias(xv[u][4 * g + 0], e), gi_vbias(xv[u][4 * g + 1], e),
+                  gi_vbias(xv[u][4 * g + 2], e), gi_vbias(xv[u][4 * g + 3], e), w[g]);
+      const int slot = kq ^ gi_swz(f);
+#pragma unroll
+      for (int a = 0; a < kGiDig; ++a)
+        *reinterpret_cast<uint4*>(buf + ((a * kGiF + f) * 4 + slot) * 16) =
+            make_uint4(w[0][a], w[1][a], w[2][a], w[3][a]);
+    }
+  };
+  constexpr int kBuf = kGiDig * kGiF * kGiRows;
+
+  // double-buffered digits, one barrier per 64-row chunk (as gram_i8_kernel)
+  if (nchunks > 0) {
+    load(0);
+#pragma unroll
+    for (int u = 0; u < kIt; ++u) slice_item(u, s_dig);
+    if (nchunks > 1) load(1);
+  }
+  __syncthreads();
+  const int lf = lane & 15, lsl = lane >> 4;
+  for (int c = 0; c < nchunks; ++c) {
+    const unsigned char* cur = s_dig + (c & 1) * kBuf;
+    unsigned char* nxt = s_dig + ((c + 1) & 1) * kBuf;
+    const bool more = c + 1 < nchunks;
+    i32x4 A[kGiDig];
+#pragma unroll
+    for (int q = 0; q < MT; ++q) {
+      if (q < ntl) {
+        if (q == 0 || ti[q] != ti[q - 1]) {  // the row block changes (wave-uniform)
+          const int fa = ti[q] * 16 + lf;
+#pragma unroll
+          for (int a = 0; a < kGiDig; ++a)
+            A[a] = *reinterpret_cast<const i32x4*>(cur + ((a * kGiF + fa) * 4 + (lsl ^ gi_swz(fa))) * 16);
+        }
+        const int fb = tj[q] * 16 + lf;
+        // B digit by digit: digit b meets A digits a <= 4 - b (levels a + b <= 4)
+#pragma unroll
+        for (int b = 0; b < kGiDig; ++b) {
+          const i32x4 B = *reinterpret_cast<const i32x4*>(cur + ((b * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
+          if constexpr ((DIAG & 1) != 0) {
+            asm volatile("" ::"v"(B));
+          } else {
+#pragma unroll
+            for (int a = 0; a < kGiDig; ++a)
+              if (a + b < kGlLev)
+                lev[q][a + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[a], B, lev[q][a + b], 0, 0, 0);
+          }
+        }
+        if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+          for (int a = 0; a < kGiDig; ++a) asm volatile("" ::"v"(A[a]));
+        }
+      }
+      // the next chunk's slicing spread between the tiles: VALU work beside
+      // the MFMAs in flight
+#pragma unroll
+      for (int u = 0; u < kIt; ++u)
+        if (S::slice_at(u) == q && more) slice_item(u, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c + 2 < nchunks) load(c + 2);
+    __syncthreads();
+  }
+  // the range's partials: S exact to the last step, one rounding, then the
+  // exact power-of-two scale; a non-finite bound gives NaN rows / columns
+  double* pr = part + static_cast<int64_t>(range) * T * 256;
+  const int lc = lane & 15, lr = 4 * (lane >> 4);
+#pragma unroll
+  for (int q = 0; q < MT; ++q) {
+    if (q < ntl) {
+      const int fj = tj[q] * 16 + lc;
+      const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
+      const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int fi = ti[q] * 16 + lr + e;
+        const int ei = fi < D ? gi_exp(colmax[fi]) : 0;
+        const bool bad = (fi < D && !isfinite(__uint_as_float(colmax[fi]))) || !okj;
+        double sum = static_cast<double>(lev[q][0][e]);
+#pragma unroll
+        for (int l = 1; l < kGlLev; ++l) sum = fma(sum, 256.0, static_cast<double>(lev[q][l][e]));
+        pr[static_cast<int64_t>(q0 + q) * 256 + (lr + e) * 16 + lc] =
+            bad ? __builtin_nan("") : ldexp(sum, ei + ej - 44);
+      }
+    }
+  }
+}
+
+// product shape: four workgroups per range (64 ranges: 256 workgroups, one
+// per CU), 8 waves, <= 6 tiles per wave (236 VGPRs; three parts of <= 8
+// tiles per wave need ~290 and spill)
+using GlProduct = GlShape<4, 8, 6>;
+
 // colmax[j] = max_i |x[i, j]| as float bits (atomicMax on the bits of a
 // non-negative float orders like the float); a NaN bound wins (non-finite x
 // then reaches G through mmb_gram_i8).
@@ -623,6 +852,39 @@ __global__ void xt_omega_kernel(const TX* __restrict__ num, const float* __restr
   double acc = 0.0;
   for (int64_t n = 0; n < N; ++n) acc += static_cast<double>(load_x(num, cnt, n, p, D)) * om[n * k + j];
   z0[e] = acc;
+}
+
+// X^T Omega for the transposed branch's small splits (N < d rows, k <= 16):
+// one wave per feature p, lane l summing rows l, l + 64, ... for all k
+// columns (every load of a lane independent), then a fixed-order DPP wave sum
+// per column.  The thread-per-output kernel above walked all N rows as one
+// dependent chain of loads: 59 us for a 229-row split (r04 dataset_splits).
+template <typename TX>
+__global__ __launch_bounds__(256) void xt_omega_wave_kernel(const TX* __restrict__ num,
+                                                            const float* __restrict__ cnt,
+                                                            int64_t N, int D,
+                                                            const double* __restrict__ om, int k,
+                                                            double* __restrict__ z0) {
+  constexpr int kK = 16;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int p = blockIdx.x * (blockDim.x / kWave) + static_cast<int>(threadIdx.x / kWave);
+  if (p >= D) return;
+  double acc[kK];
+#pragma unroll
+  for (int j = 0; j < kK; ++j) acc[j] = 0.0;
+  for (int64_t n = lane; n < N; n += kWave) {
+    const double xv = static_cast<double>(load_x(num, cnt, n, p, D));
+#pragma unroll
+    for (int j = 0; j < kK; ++j)
+      if (j < k) acc[j] = fma(xv, om[n * k + j], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kK; ++j) {
+    if (j < k) {
+      const double s = wave_sum_dpp(acc[j]);
+      if (lane == 0) z0[p * k + j] = s;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ pc_solve
@@ -2171,7 +2433,140 @@ static int gram_i8_diag() {  // timing-only ablations (MMB_GRAM_DIAG), re-read p
   const char* e = getenv("MMB_GRAM_DIAG");
   return e ? atoi(e) : 0;
 }
+static bool gram_i8_v1() {  // the round-4 kernel (per-k-step f64 updates) for A/B runs
+  const char* e = getenv("MMB_GRAM_I8_V1");
+  return e && atoi(e) != 0;
+}
 #endif
+
+// ---- level-sum int8 Gram (gram_i8l_kernel): plan and part split
+struct GramLPlan {
+  int nt, T, R, xcd, P;
+  GlParts parts;
+  int64_t chunk;
+};
+
+static int tri_row_host(int tau, int nt) {
+  int r = 0, rem = tau;
+  while (rem >= nt - r) {
+    rem -= nt - r;
+    ++r;
+  }
+  return r;
+}
+
+// Part bounds of the row-major triangle, P contiguous parts of <= cap tiles,
+// minimising the largest part's modelled cost per 64-row chunk in SIMD
+// cycles: the matrix pipe, 13 MFMAs x 16 cycles per tile over 4 SIMDs,
+// against vector issue, the MFMAs' 8 cycles each plus the slicing of every
+// feature from the part's first tile row on (64 values x ~6.75 vector
+// instructions of 4 cycles, over 64 lanes and 4 SIMDs).  (Dynamic program
+// over the split points: P <= 4, T <= 190.)
+static GlParts gram_i8l_split(int nt, int P, int cap) {
+  const int T = nt * (nt + 1) / 2;
+  auto cost = [&](int t0, int t1) {
+    const int n = t1 - t0;
+    if (n <= 0) return 0.0;
+    const int nf = 16 * (nt - tri_row_host(t0, nt));
+    return std::max(52.0 * n, 26.0 * n + 6.75 * nf);
+  };
+  // best[k][t]: the least max cost of the first t tiles in k parts
+  std::vector<std::vector<double>> best(P + 1, std::vector<double>(T + 1, 1e300));
+  std::vector<std::vector<int>> arg(P + 1, std::vector<int>(T + 1, 0));
+  best[0][0] = 0.0;
+  for (int k = 1; k <= P; ++k)
+    for (int t = 0; t <= T; ++t)
+      for (int s = std::max(0, t - cap); s <= t; ++s) {
+        const double c = std::max(best[k - 1][s], cost(s, t));
+        if (c < best[k][t]) {
+          best[k][t] = c;
+          arg[k][t] = s;
+        }
+      }
+  GlParts g{};
+  g.b[P] = T;
+  for (int k = P; k >= 1; --k) g.b[k - 1] = arg[k][g.b[k]];
+  for (int k = P + 1; k <= kGlMaxParts; ++k) g.b[k] = T;
+  return g;
+}
+
+// R ranges of whole 64-row chunks: as many as keep all P R workgroups
+// resident (P = 3: 80 ranges, 240 workgroups -- ten ranges' parts on each
+// XCD's 32 CUs), at least one k-step each and at most kGlMaxRows rows each
+// (the int32 level sums); a multiple of 8 (the XCD map and
+// gram_tri_reduce_kernel) and <= 128 -- mmb_gram_i8 cuts larger calls into
+// blocks of kGlBlockRows rows.
+constexpr int64_t kGlBlockRows = 128 * kGlMaxRows;
+
+template <class S>
+static GramLPlan gram_i8l_plan(int64_t n, int d) {
+  GramLPlan q;
+  q.nt = static_cast<int>(ceil_div(d, 16));
+  q.T = q.nt * (q.nt + 1) / 2;
+  q.P = S::kP;
+  const int64_t resident = 256 / S::kP / 8 * 8;
+  int64_t R = std::min<int64_t>(resident, std::max<int64_t>(1, n / kGiRows));
+  R = std::max<int64_t>(R, ceil_div(n, kGlMaxRows));
+  if (R >= 8) R = ceil_div(R, 8) * 8;
+  q.R = static_cast<int>(std::min<int64_t>(R, 128));
+  q.xcd = (q.R % 8 == 0) ? 1 : 0;
+  q.chunk = ceil_div(ceil_div(std::max<int64_t>(n, 1), q.R), kGiRows) * kGiRows;
+  q.parts = gram_i8l_split(q.nt, S::kP, S::kPartMax);
+  return q;
+}
+
+template <int DIAG, class S>
+static size_t gram_i8l_lds() {
+  const size_t lds = 2 * kGiDig * kGiF * kGiRows;  // 160 KB: double-buffered digits
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8l_kernel<DIAG, S>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr = true;
+  }
+  return lds;
+}
+
+// One block of <= kGlBlockRows rows: the level-sum kernel, then the range
+// reduction (writing or accumulating into g).
+template <int DIAG, class S>
+static int gram_i8l_block(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
+                          int accumulate, double* part, hipStream_t stream) {
+  const GramLPlan q = gram_i8l_plan<S>(n, d);
+  for (int k = 0; k < q.P; ++k) MMB_REQUIRE(q.parts.b[k + 1] - q.parts.b[k] <= S::kPartMax);
+  MMB_REQUIRE(q.parts.b[q.P] == q.T);
+  // the buffer-descriptor record count and row offsets are 32-bit byte counts of one range
+  MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
+  gram_i8l_kernel<DIAG, S><<<S::kP * q.R, S::kNT, gram_i8l_lds<DIAG, S>(), stream>>>(
+      x, colmax, n, d, q.nt, q.chunk, q.xcd, q.parts, part);
+  MMB_LAUNCH_CHECK();
+  const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
+  if (rc != MMB_OK) return rc;
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+#ifdef MMB_DIAG
+// tools build: the level-sum kernel's shape (MMB_GRAM_I8_SHAPE: 0 the
+// product's 4 parts x 8 waves x 6 tiles, 1 three parts x 8 waves x 8 tiles,
+// 2 four parts x 8 waves x 7 tiles) and its timing-only ablations
+static int gram_i8_shape() {
+  const char* e = getenv("MMB_GRAM_I8_SHAPE");
+  return e ? atoi(e) : 0;
+}
+template <class S>
+static int gram_i8l_block_diag(const float* x, const uint32_t* colmax, int64_t n, int d,
+                               double* g, int accumulate, double* part, hipStream_t stream) {
+  switch (gram_i8_diag()) {
+    case 1: return gram_i8l_block<1, S>(x, colmax, n, d, g, accumulate, part, stream);
+    case 4: return gram_i8l_block<4, S>(x, colmax, n, d, g, accumulate, part, stream);
+    case 12: return gram_i8l_block<12, S>(x, colmax, n, d, g, accumulate, part, stream);
+    case 13: return gram_i8l_block<13, S>(x, colmax, n, d, g, accumulate, part, stream);
+    default: return gram_i8l_block<0, S>(x, colmax, n, d, g, accumulate, part, stream);
+  }
+}
+#endif
+
 }  // namespace mmb
 
 using namespace mmb;
@@ -2183,7 +2578,10 @@ extern "C" size_t mmb_gram_workspace_bytes(int64_t n, int d) {
   const size_t v2 = static_cast<size_t>(q.R) * q.T * 256 * sizeof(double);
   const Gram2Plan qi = gram_i8_plan(n, d);
   const size_t v3 = static_cast<size_t>(qi.R) * qi.T * 256 * sizeof(double);
-  const size_t v23 = v2 > v3 ? v2 : v3;
+  // the level-sum kernel: at most 128 ranges per block (every shape)
+  const GramLPlan ql = gram_i8l_plan<GlShape<2, 8, 12>>(std::min(n, kGlBlockRows), d);
+  const size_t v4 = static_cast<size_t>(ql.R) * ql.T * 256 * sizeof(double);
+  const size_t v23 = std::max(std::max(v2, v3), v4);
   return v1 > v23 ? v1 : v23;
 }
 
@@ -2233,33 +2631,48 @@ extern "C" int mmb_colmax(const float* x, int64_t n, int d, uint32_t* colmax, in
 extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
                            int accumulate, void* ws, hipStream_t stream) {
   MMB_REQUIRE(x && colmax && g && ws && n >= 0 && d > 0 && d <= 304 && d % 4 == 0);
-  const Gram2Plan q = gram_i8_plan(n, d);
-  MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
-  // the kernel's buffer-descriptor record count and row offsets are 32-bit
-  // byte counts of one range (n above ~229M rows at d = 300: split the call)
-  MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
-  // int32 level sums are per 64-row k-step, so any range length is safe
   double* part = static_cast<double*>(ws);
 #ifdef MMB_DIAG
-  switch (gram_i8_diag()) {
-    case 1: launch_gram_i8<1>(x, colmax, n, d, q, part, stream); break;
-    case 2: launch_gram_i8<2>(x, colmax, n, d, q, part, stream); break;
-    case 3: launch_gram_i8<3>(x, colmax, n, d, q, part, stream); break;
-    case 4: launch_gram_i8<4>(x, colmax, n, d, q, part, stream); break;
-    case 12: launch_gram_i8<12>(x, colmax, n, d, q, part, stream); break;
-    case 15: launch_gram_i8<15>(x, colmax, n, d, q, part, stream); break;
-    case 7: launch_gram_i8<7>(x, colmax, n, d, q, part, stream); break;
-    default: launch_gram_i8<0>(x, colmax, n, d, q, part, stream); break;
-  }
-#else
-  launch_gram_i8<0>(x, colmax, n, d, q, part, stream);
-#endif
-  MMB_LAUNCH_CHECK();
-  {
+  if (gram_i8_v1()) {  // the round-4 kernel (tools build only)
+    const Gram2Plan q = gram_i8_plan(n, d);
+    MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
+    MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
+    switch (gram_i8_diag()) {
+      case 1: launch_gram_i8<1>(x, colmax, n, d, q, part, stream); break;
+      case 2: launch_gram_i8<2>(x, colmax, n, d, q, part, stream); break;
+      case 4: launch_gram_i8<4>(x, colmax, n, d, q, part, stream); break;
+      case 12: launch_gram_i8<12>(x, colmax, n, d, q, part, stream); break;
+      case 15: launch_gram_i8<15>(x, colmax, n, d, q, part, stream); break;
+      default: launch_gram_i8<0>(x, colmax, n, d, q, part, stream); break;
+    }
+    MMB_LAUNCH_CHECK();
     const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
     if (rc != MMB_OK) return rc;
+    MMB_LAUNCH_CHECK();
+    return MMB_OK;
   }
-  MMB_LAUNCH_CHECK();
+#endif
+  // blocks of <= kGlBlockRows rows (<= 128 ranges of <= 32768 rows: int32
+  // level sums, at most 128 range partials per reduction); the first block
+  // writes (or accumulates into) g, later ones accumulate
+  int64_t b0 = 0;
+  do {
+    const int64_t nb = std::min(n - b0, kGlBlockRows);
+    const float* xb = x + b0 * d;
+    const int acc = accumulate || b0 > 0;
+#ifdef MMB_DIAG
+    int rc;
+    switch (gram_i8_shape()) {
+      case 1: rc = gram_i8l_block_diag<GlShape<3, 8, 8>>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 2: rc = gram_i8l_block_diag<GlShape<4, 8, 7>>(xb, colmax, nb, d, g, acc, part, stream); break;
+      default: rc = gram_i8l_block_diag<GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
+    }
+#else
+    const int rc = gram_i8l_block<0, GlProduct>(xb, colmax, nb, d, g, acc, part, stream);
+#endif
+    if (rc != MMB_OK) return rc;
+    b0 += nb;
+  } while (b0 < n);
   return MMB_OK;
 }
 
@@ -2289,7 +2702,10 @@ extern "C" int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate,
 extern "C" int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d,
                             const double* omega, int k, double* z0, hipStream_t stream) {
   MMB_REQUIRE(num && omega && z0 && n >= 0 && d > 0 && k > 0);
-  xt_omega_kernel<float><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
+  if (k <= 16)  // (the solver's k = npc + 10 <= 16)
+    xt_omega_wave_kernel<float><<<static_cast<int>(ceil_div(d, 4)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
+  else
+    xt_omega_kernel<float><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -2409,8 +2825,11 @@ extern "C" int mmb_gram_f64(const double* x, int64_t n, int d, double* g, int ac
 extern "C" int mmb_xt_omega_f64(const double* x, int64_t n, int d, const double* omega, int k,
                                 double* z0, hipStream_t stream) {
   MMB_REQUIRE(x && omega && z0 && n >= 0 && d > 0 && k > 0);
-  xt_omega_kernel<double><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(
-      x, nullptr, n, d, omega, k, z0);
+  if (k <= 16)
+    xt_omega_wave_kernel<double><<<static_cast<int>(ceil_div(d, 4)), 256, 0, stream>>>(x, nullptr, n, d, omega, k, z0);
+  else
+    xt_omega_kernel<double><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(
+        x, nullptr, n, d, omega, k, z0);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

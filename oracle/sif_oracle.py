@@ -160,11 +160,15 @@ def pc_from_gram(G, z0, npc=1, transposed=False, n_iter=7):
 
 
 def sliced_gram(X, colmax=None):
-    """CPU restatement of the int8 Gram (csrc/pc_kernels.hip gram_i8_kernel):
-    each value a 30-bit fixed-point integer of its column's power-of-two bound
-    2^e (|x| <= colmax < 2^e), v = rint(x 2^(30-e)), cut into four balanced
-    base-256 digits (top in [-64, 64]); digit-pair products of level a + b <= 4
-    summed exactly, G = 2^(e_i + e_j - 60) sum over those pairs.  Test
+    """CPU restatement of the int8 Gram (csrc/pc_kernels.hip gram_i8l_kernel;
+    r04's gram_i8_kernel had the same digits and pairs): each value a 30-bit
+    fixed-point integer of its column's power-of-two bound 2^e (|x| <= colmax
+    < 2^e), v = rint(x 2^(30-e)), cut into four balanced base-256 digits (top
+    in [-64, 64]); digit-pair products of level a + b <= 4 summed exactly,
+    G = 2^(e_i + e_j - 60) sum over those pairs.  (The device sums each level
+    exactly in int32 over a row range and rounds each range's combination
+    once; here every pair's exact integer sum is rounded once: the two agree
+    to the f64 summation of the range partials, ~1e-16.)  Test
     infrastructure: the reference has no counterpart (its TruncatedSVD works
     on X itself); this pins the device kernel's arithmetic."""
     X = np.asarray(X, np.float32).astype(np.float64)

@@ -424,6 +424,32 @@ def test_gram_i8_vs_sliced_oracle_and_f64(gpu, n, seed, scale):
     assert np.array_equal(G, G.T)
 
 
+def test_gram_i8_blocks_past_int32_range_limit(gpu):
+    """mmb_gram_i8 sums each range's digit-pair levels in int32 (exact for
+    ranges of <= 32768 rows) and cuts calls above 128 such ranges
+    (4,194,304 rows) into blocks whose reductions accumulate into G: a call
+    just past one block (narrow rows, d = 16), and one with accumulate=True
+    on top of a previous G, against the sliced restatement and the exact
+    f64 Gram."""
+    from oracle import sif_oracle as O
+
+    n = 128 * 32768 + 1000
+    g = torch.Generator(device=gpu).manual_seed(11)
+    xt = (torch.randn(n, 16, generator=g, device=gpu) * 0.7 + 0.2).contiguous()
+    xt[: n // 3] *= 3.0
+    cm = P.colmax(xt)
+    G = P.gram_i8(xt, cm)
+    G2 = P.gram_i8(xt[:5000], cm, G.clone(), accumulate=True)
+    x = xt.cpu().numpy()
+    ref = O.sliced_gram(x, cm.cpu().numpy().view(np.float32))
+    exact = x.astype(np.float64).T @ x.astype(np.float64)
+    Gn = G.cpu().numpy()
+    assert np.abs(Gn - ref).max() <= 1e-13 * np.abs(ref).max()
+    assert np.abs(Gn - exact).max() <= 2e-9 * np.abs(exact).max()
+    ref2 = ref + O.sliced_gram(x[:5000], cm.cpu().numpy().view(np.float32))
+    assert np.abs(G2.cpu().numpy() - ref2).max() <= 1e-13 * np.abs(ref2).max()
+
+
 def test_gram_i8_pc_on_golden_splits(gpu, golden):
     """The PC solved from the int8 Gram stays within 1e-9 of the reference's
     TruncatedSVD component on the golden splits (gap-free g3 and npc = 2
