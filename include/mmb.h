@@ -131,7 +131,9 @@ int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n
  * a completed solve leaves them zero -- no memset is enqueued, so the call is
  * safe to capture into a graph and replay.  A workgroup that waits ~1 s for
  * the others gives up and sets MMB_FLAG_SYNC_TIMEOUT in *flag (nullable);
- * pc_out is then NaN and ws must be re-zeroed before the next call.
+ * so does a launch that finds the words dirty (an abort word left set, or an
+ * arrival count outside the round's range); pc_out is then NaN and ws must
+ * be re-zeroed before the next call.
  * replaces: sif_functions.compute_pc /root/reference/sif_functions.py:58-67 */
 size_t mmb_pc_solve_mc_ws_bytes(int d);
 int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
@@ -372,7 +374,10 @@ int mmb_mlp_eval(const float* latents, const float* labels, const int64_t* perm,
  * ws: scratch of mmb_mlp_workspace_bytes(d, h) bytes (16-B aligned), ZEROED
  * by the caller before its first use (a completed launch leaves it zeroed);
  * flag (nullable) gets MMB_FLAG_SYNC_TIMEOUT if the workgroups' exchange
- * stalls (~1 s; the parameters are then invalid and ws must be re-zeroed).  d % 4 == 0, d <= 512, h <= 512,
+ * stalls (~1 s) or finds ws dirty (the parameters are then invalid and ws
+ * must be re-zeroed).  The P = ceil(h / 32) workgroups are launched
+ * cooperatively (co-resident, or the launch fails) after an occupancy check
+ * (MMB_EINVAL when the device cannot hold them at once).  d % 4 == 0, d <= 512, h <= 512,
  * n_out <= 16.
  * replaces: sentiment_model.train_sentiment loop incl. its validation passes
  *   /root/reference/sentiment_model.py:76-127                               */

@@ -2753,9 +2753,17 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
     attr = true;
   }
   // no memset node here: the counter / abort words must be zero when the
-  // caller first hands ws over, and a completed solve leaves them zero (a
-  // captured 16-byte hipMemsetAsync wrote garbage into the abort word on
-  // graph replays, r04)
+  // caller first hands ws over, and a completed solve leaves them zero.  The
+  // r04 launcher enqueued a 16-byte hipMemsetAsync of them instead; captured
+  // into a HIP graph, that node wrote an address-like 64-bit value over BOTH
+  // words on every replay after the first (ctl = [0x14ABxxxx, 0x7BE2]:
+  // tools/dbg/replay_cause.py, r05a).  The garbage count passed every wait at
+  // once, so the workgroups gathered tiles that were not yet written: a wrong
+  // PC (39 of 40 replays of the solve alone) or a NaN one where the Cholesky
+  // of the inconsistent block broke down (the r04e split failure), with no
+  // flag.  Since r05 every arrival checks the count it finds (pm_arrive) and
+  // every wait the abort word first, so a dirty workspace aborts with
+  // MMB_FLAG_SYNC_TIMEOUT and a NaN PC instead
   pc_solve_mc_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
                                                               pc_out, xbuf, ctl, flag);
   MMB_LAUNCH_CHECK();
