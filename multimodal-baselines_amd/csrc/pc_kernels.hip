@@ -127,6 +127,65 @@ __device__ __forceinline__ void tri_tile(int tau, int nt, int& ti, int& tj) {
   tj = r + rem;
 }
 
+// ------------------------------------------------------------------ Gram, small n (r05)
+// Dataset splits (MOSI 229-1284 rows, POM 100-203) take the exact f64 Gram.
+// The row-range kernel below spends its time there on fixed costs: 16 ranges
+// of 80 rows, every workgroup writing 95 tiles of partials that a second
+// launch reduces (37 us per split, r04 dataset_splits).  For n <= 4096 this
+// kernel is tile-parallel instead: one workgroup per 16 x 16 tile of the
+// upper triangle over ALL rows, its 16 waves taking strided 4-row k-steps
+// (fp64 MFMA 16x16x4: f32 x f32 products exact in f64), the 16 partial tiles
+// summed in a fixed order through LDS and written straight into G (and its
+// mirror): one launch, no partials.
+constexpr int kGsNT = 1024;
+constexpr int64_t kGsMaxN = 4096;
+
+__global__ __launch_bounds__(kGsNT) void gram_small_kernel(const float* __restrict__ num,
+                                                           const float* __restrict__ cnt,
+                                                           int64_t N, int D, int nt, int accumulate,
+                                                           double* __restrict__ g) {
+  __shared__ double s_acc[kGsNT / kWave][256];
+  int bi, bj;
+  tri_tile(blockIdx.x, nt, bi, bj);
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  constexpr int NW = kGsNT / kWave;
+  const int ca = 16 * bi + (lane & 15), cb = 16 * bj + (lane & 15), kr = lane >> 4;
+  f64x4 acc = {0, 0, 0, 0};
+  // wave w: k-steps w, w + 16, ... (4 rows each), loads issued ahead in groups
+  constexpr int G = 8;
+  const int64_t nks = (N + 3) / 4;
+  for (int64_t s0 = wave; s0 < nks; s0 += NW * G) {
+    double av[G], bv[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int64_t row = (s0 + NW * u) * 4 + kr;
+      const bool ok = s0 + NW * u < nks && row < N;
+      av[u] = ok ? static_cast<double>(load_x(num, cnt, row, ca, D)) : 0.0;
+      bv[u] = ok ? static_cast<double>(load_x(num, cnt, row, cb, D)) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+  }
+  // C/D layout: col = lane & 15, row = (lane >> 4) + 4 reg
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) s_acc[wave][((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+  __syncthreads();
+  if (threadIdx.x >= 256) return;
+  const int e = threadIdx.x, r = e >> 4, c = e & 15;
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) s += s_acc[w][e];
+  const int p = 16 * bi + r, q = 16 * bj + c;
+  if (p >= D || q >= D) return;
+  const int64_t e1 = static_cast<int64_t>(p) * D + q;
+  g[e1] = accumulate ? g[e1] + s : s;
+  if (bi != bj) {
+    const int64_t e2 = static_cast<int64_t>(q) * D + p;
+    g[e2] = accumulate ? g[e2] + s : s;
+  }
+}
+
+
 __global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict__ num,
                                                          const float* __restrict__ cnt, int64_t N,
                                                          int D, int nt, int R, int64_t chunk,
@@ -403,6 +462,18 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
     }
   };
   // item u of the x values in registers -> digit bytes in LDS buffer `buf`
+  auto load_item = [&](int u, int c) {
+    if constexpr ((DIAG & 8) != 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(xv[u][j]));
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
+      xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
+    }
+  };
   auto slice_item = [&](int u, unsigned char* buf) {
     if constexpr ((DIAG & 4) != 0) return;
     const int it = tid + kGiNT * u;
@@ -543,19 +614,37 @@ __global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict_
 constexpr int kGlLev = 5;
 constexpr int64_t kGlMaxRows = 512 * kGiRows;        // int32 level sums exact
 constexpr int kGlMaxParts = 4;
+constexpr int kGlMaxPartTiles = 64;
 
-// tile bounds of the parts: part p owns [b[p], b[p + 1]) of the row-major triangle
+// One workgroup's share of a range's work: its tiles (ti | tj << 8, grouped
+// by tile row for A reuse) and the features it slices, [f0, f0 + n0) and
+// [f1, f1 + n1) -- every feature its tiles touch (gram_i8l_parts).
+struct GlPart {
+  int n, f0, n0, f1, n1;
+  uint16_t tile[kGlMaxPartTiles];
+};
 struct GlParts {
-  int b[kGlMaxParts + 1];
+  GlPart p[kGlMaxParts];
 };
 
 // Shape of a level-sum kernel: P workgroups per row range, NW waves each, at
-// most MT tiles per wave (P * NW * MT >= 190 tiles at d = 300).
-template <int P, int NW, int MT>
+// most MT tiles per wave (P * NW * MT >= 190 tiles at d = 300); IT slicing
+// items (16 rows of one feature) per thread.
+// SB: the mask of the scheduling barrier between tiles (0: nothing crosses;
+// 0x100: LDS reads may move up into the previous tile); PF: the next tile's
+// first B digit is read during the current tile's MFMAs (4 VGPRs).
+// ST: staggered slicing -- waves 0 .. NW/2-1 slice each item BEFORE their
+// run of tiles, waves NW/2 .. NW-1 (their SIMD partners) AFTER it, so one
+// wave of a SIMD slices while the other issues MFMAs; each item's x for the
+// chunk after next is loaded as soon as it is sliced.
+template <int P, int NW, int MT, int IT, int SB = 0, bool PF = false, bool ST = false>
 struct GlShape {
-  static constexpr int kP = P, kNW = NW, kMT = MT, kNT = NW * kWave;
-  static constexpr int kPartMax = NW * MT;
-  static constexpr int kIt = (kGiItems + kNT - 1) / kNT;  // slicing items per thread
+  static constexpr int kP = P, kNW = NW, kMT = MT, kNT = NW * kWave, kSB = SB;
+  static constexpr bool kPF = PF, kST = ST;
+  // staggered: the slice point of item u (before tile p; p = MT: after the last)
+  static constexpr int slice_before(int u, bool second) { return ((u + (second ? 1 : 0)) * MT) / IT; }
+  static constexpr int kPartMax = NW * MT < kGlMaxPartTiles ? NW * MT : kGlMaxPartTiles;
+  static constexpr int kIt = IT;
   // item u is sliced after tile slice_at(u): spread over the tile loop
   static constexpr int slice_at(int u) { return (u * MT) / kIt + MT / kIt - 1; }
 };
@@ -570,7 +659,6 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
                                                          double* __restrict__ part) {
   constexpr int MT = S::kMT, NT = S::kNT, kIt = S::kIt;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dig[];  // [2][4][kGiF][64]
-  const int T = nt * (nt + 1) / 2;
   int range, p;
   if (xcd_map) {  // the P parts of a range on one XCD (round-robin dispatch: b % 8)
     const int b = blockIdx.x, s = b >> 3;
@@ -580,19 +668,22 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
     range = blockIdx.x / S::kP;
     p = blockIdx.x % S::kP;
   }
+  const GlPart& pt = parts.p[p];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t0 = parts.b[p], t1 = parts.b[p + 1];
-  if (t1 <= t0) return;  // an empty part (tiny d)
-  const int per = (t1 - t0 + S::kNW - 1) / S::kNW;
-  const int q0 = t0 + wave * per;
+  const int npt = pt.n;
+  if (npt <= 0) return;  // an empty part (tiny d)
+  const int per = (npt + S::kNW - 1) / S::kNW;
+  const int q0 = wave * per;
   int ti[MT], tj[MT];
   int ntl = 0;
 #pragma unroll
   for (int q = 0; q < MT; ++q) {
     ti[q] = tj[q] = 0;
-    if (q < per && q0 + q < t1) {
-      tri_tile(q0 + q, nt, ti[q], tj[q]);
+    if (q < per && q0 + q < npt) {
+      const int t = pt.tile[q0 + q];
+      ti[q] = t & 255;
+      tj[q] = t >> 8;
       ntl = q + 1;
     }
   }
@@ -605,19 +696,18 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
   const int64_t r0 = range * chunk;
   const int64_t r1 = min(N, r0 + chunk);
   const int nchunks = static_cast<int>(r1 > r0 ? (r1 - r0 + kGiRows - 1) / kGiRows : 0);
-  // features this part reads: its first tile row on (tj >= ti >= that row)
-  int tr0, tc0;
-  tri_tile(t0, nt, tr0, tc0);
-  const int f_lo = 16 * tr0;
-  const int nf = nt * 16 - f_lo;
+  // the features this part slices: two ranges (every feature its tiles touch)
+  const int f0 = pt.f0, n0 = pt.n0, f1 = pt.f1;
+  const int nf = n0 + pt.n1;
   const int nitems = nf * 4;
-  // item it = (f - f_lo) + nf * kq: feature f, rows 16 kq .. 16 kq + 15 of the
-  // chunk; packed (f | kq << 9 | (e + 256) << 11) with its row offset beside
+  // item it = k + nf * kq: the k-th sliced feature f, rows 16 kq .. 16 kq + 15
+  // of the chunk; packed (f | kq << 9 | (e + 256) << 11) with its row offset
   int it_pk[kIt], it_off[kIt];
 #pragma unroll
   for (int u = 0; u < kIt; ++u) {
     const int it = tid + NT * u;
-    const int f = it < nitems ? f_lo + it % nf : 0;
+    const int k = it < nitems ? it % nf : 0;
+    const int f = it < nitems ? (k < n0 ? f0 + k : f1 + k - n0) : 0;
     const int kq = it < nitems ? it / nf : 0;
     const int e = (it < nitems && f < D) ? gi_exp(colmax[f]) : 0;
     it_pk[u] = f | (kq << 9) | ((e + 256) << 11);
@@ -641,6 +731,18 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
 #pragma unroll
       for (int u = 0; u < kIt; ++u)
         xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
+    }
+  };
+  auto load_item = [&](int u, int c) {
+    if constexpr ((DIAG & 8) != 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(xv[u][j]));
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
+      xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
     }
   };
   auto slice_item = [&](int u, unsigned char* buf) {
@@ -676,8 +778,29 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
     unsigned char* nxt = s_dig + ((c + 1) & 1) * kBuf;
     const bool more = c + 1 < nchunks;
     i32x4 A[kGiDig];
+    auto ld_b = [&](const unsigned char* buf, int fb, int b) {
+      return *reinterpret_cast<const i32x4*>(buf + ((b * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
+    };
+    i32x4 Bn0 = {0, 0, 0, 0};
+    if constexpr (S::kPF) {
+      if (ntl > 0) Bn0 = ld_b(cur, tj[0] * 16 + lf, 0);
+    }
+    const bool second = wave >= S::kNW / 2;
+    // staggered slicing: the items whose slice point is before tile p
+    auto slice_point = [&](int p) {
+      if constexpr (S::kST) {
+#pragma unroll
+        for (int u = 0; u < kIt; ++u) {
+          if (S::slice_before(u, second) == p && more) {
+            slice_item(u, nxt);
+            if (c + 2 < nchunks) load_item(u, c + 2);
+          }
+        }
+      }
+    };
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
+      slice_point(q);
       if (q < ntl) {
         if (q == 0 || ti[q] != ti[q - 1]) {  // the row block changes (wave-uniform)
           const int fa = ti[q] * 16 + lf;
@@ -686,10 +809,17 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
             A[a] = *reinterpret_cast<const i32x4*>(cur + ((a * kGiF + fa) * 4 + (lsl ^ gi_swz(fa))) * 16);
         }
         const int fb = tj[q] * 16 + lf;
+        i32x4 Bd[kGiDig];
+#pragma unroll
+        for (int b = 0; b < kGiDig; ++b)
+          Bd[b] = (S::kPF && b == 0) ? Bn0 : ld_b(cur, fb, b);
+        if constexpr (S::kPF) {
+          if (q + 1 < ntl) Bn0 = ld_b(cur, tj[q + 1] * 16 + lf, 0);
+        }
         // B digit by digit: digit b meets A digits a <= 4 - b (levels a + b <= 4)
 #pragma unroll
         for (int b = 0; b < kGiDig; ++b) {
-          const i32x4 B = *reinterpret_cast<const i32x4*>(cur + ((b * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
+          const i32x4 B = Bd[b];
           if constexpr ((DIAG & 1) != 0) {
             asm volatile("" ::"v"(B));
           } else {
@@ -706,21 +836,26 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
       }
       // the next chunk's slicing spread between the tiles: VALU work beside
       // the MFMAs in flight
+      if constexpr (!S::kST) {
 #pragma unroll
-      for (int u = 0; u < kIt; ++u)
-        if (S::slice_at(u) == q && more) slice_item(u, nxt);
-      __builtin_amdgcn_sched_barrier(0);
+        for (int u = 0; u < kIt; ++u)
+          if (S::slice_at(u) == q && more) slice_item(u, nxt);
+      }
+      __builtin_amdgcn_sched_barrier(S::kSB);
     }
-    if (c + 2 < nchunks) load(c + 2);
+    slice_point(MT);
+    if (!S::kST && c + 2 < nchunks) load(c + 2);
     __syncthreads();
   }
   // the range's partials: S exact to the last step, one rounding, then the
   // exact power-of-two scale; a non-finite bound gives NaN rows / columns
+  const int T = nt * (nt + 1) / 2;
   double* pr = part + static_cast<int64_t>(range) * T * 256;
   const int lc = lane & 15, lr = 4 * (lane >> 4);
 #pragma unroll
   for (int q = 0; q < MT; ++q) {
     if (q < ntl) {
+      const int tau = ti[q] * nt - ti[q] * (ti[q] - 1) / 2 + (tj[q] - ti[q]);  // row-major triangle
       const int fj = tj[q] * 16 + lc;
       const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
       const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
@@ -732,17 +867,16 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
         double sum = static_cast<double>(lev[q][0][e]);
 #pragma unroll
         for (int l = 1; l < kGlLev; ++l) sum = fma(sum, 256.0, static_cast<double>(lev[q][l][e]));
-        pr[static_cast<int64_t>(q0 + q) * 256 + (lr + e) * 16 + lc] =
+        pr[static_cast<int64_t>(tau) * 256 + (lr + e) * 16 + lc] =
             bad ? __builtin_nan("") : ldexp(sum, ei + ej - 44);
       }
     }
   }
 }
 
-// product shape: four workgroups per range (64 ranges: 256 workgroups, one
-// per CU), 8 waves, <= 6 tiles per wave (236 VGPRs; three parts of <= 8
-// tiles per wave need ~290 and spill)
-using GlProduct = GlShape<4, 8, 6>;
+// product shape: three workgroups per range (80 ranges), 8 waves, <= 8 tiles
+// per wave, each slicing two of three feature groups (<= 2 items per thread)
+using GlProduct = GlShape<3, 8, 8, 2>;
 
 // colmax[j] = max_i |x[i, j]| as float bits (atomicMax on the bits of a
 // non-negative float orders like the float); a NaN bound wins (non-finite x
@@ -2439,7 +2573,7 @@ static bool gram_i8_v1() {  // the round-4 kernel (per-k-step f64 updates) for A
 }
 #endif
 
-// ---- level-sum int8 Gram (gram_i8l_kernel): plan and part split
+// ---- level-sum int8 Gram (gram_i8l_kernel): plan and parts
 struct GramLPlan {
   int nt, T, R, xcd, P;
   GlParts parts;
@@ -2455,14 +2589,85 @@ static int tri_row_host(int tau, int nt) {
   return r;
 }
 
-// Part bounds of the row-major triangle, P contiguous parts of <= cap tiles,
-// minimising the largest part's modelled cost per 64-row chunk in SIMD
-// cycles: the matrix pipe, 13 MFMAs x 16 cycles per tile over 4 SIMDs,
-// against vector issue, the MFMAs' 8 cycles each plus the slicing of every
-// feature from the part's first tile row on (64 values x ~6.75 vector
-// instructions of 4 cycles, over 64 lanes and 4 SIMDs).  (Dynamic program
-// over the split points: P <= 4, T <= 190.)
-static GlParts gram_i8l_split(int nt, int P, int cap) {
+static void gl_set_features(GlPart& g, int f0, int n0, int f1, int n1) {
+  g.f0 = f0;
+  g.n0 = n0;
+  g.f1 = f1;
+  g.n1 = n1;
+}
+
+// Three feature groups G0 | G1 | G2 of tile rows (nt split as evenly as it
+// goes, the larger groups last) and three parts, one per pair of groups:
+// {G0, G1}, {G0, G2}, {G1, G2}.  Each off-diagonal block Gi x Gj goes to part
+// {Gi, Gj}; each diagonal block Gg x Gg is cut between the two parts holding
+// Gg (row-major: the first x_g tiles to the first of them), the three cuts
+// chosen to minimise the largest part (exhaustively: <= 29^3 cases, once per
+// nt).  So every part slices two thirds of the features (the three together
+// twice x, like a pair of workgroups) while holding a third of the tiles --
+// where contiguous runs of the triangle made the first part slice every
+// feature.
+static GlParts gl_parts_groups3(int nt) {
+  GlParts g{};
+  const int c = nt / 3 + (nt % 3 > 1 ? 1 : 0), b = nt / 3 + (nt % 3 > 0 ? 1 : 0), a = nt - b - c;
+  const int lo[3] = {0, a, a + b}, hi[3] = {a, a + b, nt};
+  const int pg[3][2] = {{0, 1}, {0, 2}, {1, 2}};  // part -> its two groups
+  const int dpart[3][2] = {{0, 1}, {0, 2}, {1, 2}};  // group -> the two parts holding it
+  auto sz = [&](int k) { return hi[k] - lo[k]; };
+  const int off[3] = {sz(0) * sz(1), sz(0) * sz(2), sz(1) * sz(2)};  // blocks 01, 02, 12
+  int dg[3];
+  for (int k = 0; k < 3; ++k) dg[k] = sz(k) * (sz(k) + 1) / 2;
+  int bx[3] = {dg[0], dg[1], dg[2]}, best = 1 << 30;
+  for (int x0 = 0; x0 <= dg[0]; ++x0)
+    for (int x1 = 0; x1 <= dg[1]; ++x1)
+      for (int x2 = 0; x2 <= dg[2]; ++x2) {
+        int load[3] = {off[0], off[1], off[2]};
+        const int xs[3] = {x0, x1, x2};
+        for (int k = 0; k < 3; ++k) {
+          load[dpart[k][0]] += xs[k];
+          load[dpart[k][1]] += dg[k] - xs[k];
+        }
+        const int m = std::max(load[0], std::max(load[1], load[2]));
+        if (m < best) {
+          best = m;
+          bx[0] = x0;
+          bx[1] = x1;
+          bx[2] = x2;
+        }
+      }
+  auto group_of = [&](int r) { return r < hi[0] ? 0 : (r < hi[1] ? 1 : 2); };
+  std::vector<std::pair<int, int>> lists[3];
+  int seen[3] = {0, 0, 0};  // diagonal tiles handed out per group
+  for (int ti = 0; ti < nt; ++ti) {
+    for (int tj = ti; tj < nt; ++tj) {
+      const int gi = group_of(ti), gj = group_of(tj);
+      int q;
+      if (gi != gj) {
+        q = gi == 0 ? (gj == 1 ? 0 : 1) : 2;
+      } else {
+        q = seen[gi] < bx[gi] ? dpart[gi][0] : dpart[gi][1];
+        ++seen[gi];
+      }
+      lists[q].push_back({ti, tj});
+    }
+  }
+  for (int k = 0; k < 3; ++k) {
+    std::sort(lists[k].begin(), lists[k].end());
+    g.p[k].n = static_cast<int>(lists[k].size());
+    for (int i = 0; i < g.p[k].n && i < kGlMaxPartTiles; ++i)
+      g.p[k].tile[i] = static_cast<uint16_t>(lists[k][i].first | (lists[k][i].second << 8));
+    const int g0 = pg[k][0], g1 = pg[k][1];
+    gl_set_features(g.p[k], 16 * lo[g0], 16 * sz(g0), 16 * lo[g1], 16 * sz(g1));
+  }
+  return g;
+}
+
+// P contiguous runs of the row-major triangle, <= cap tiles each, minimising
+// the largest part's modelled cost per 64-row chunk in SIMD cycles: the
+// matrix pipe (13 MFMAs x 16 cycles per tile over 4 SIMDs) against vector
+// issue (the MFMAs' 8 cycles each plus the slicing of every feature from the
+// part's first tile row on: 64 values x ~6.75 vector instructions of 4
+// cycles over 64 lanes and 4 SIMDs).  Dynamic program over the split points.
+static GlParts gl_parts_runs(int nt, int P, int cap) {
   const int T = nt * (nt + 1) / 2;
   auto cost = [&](int t0, int t1) {
     const int n = t1 - t0;
@@ -2470,7 +2675,6 @@ static GlParts gram_i8l_split(int nt, int P, int cap) {
     const int nf = 16 * (nt - tri_row_host(t0, nt));
     return std::max(52.0 * n, 26.0 * n + 6.75 * nf);
   };
-  // best[k][t]: the least max cost of the first t tiles in k parts
   std::vector<std::vector<double>> best(P + 1, std::vector<double>(T + 1, 1e300));
   std::vector<std::vector<int>> arg(P + 1, std::vector<int>(T + 1, 0));
   best[0][0] = 0.0;
@@ -2483,10 +2687,22 @@ static GlParts gram_i8l_split(int nt, int P, int cap) {
           arg[k][t] = s;
         }
       }
+  int bnd[kGlMaxParts + 1];
+  bnd[P] = T;
+  for (int k = P; k >= 1; --k) bnd[k - 1] = arg[k][bnd[k]];
   GlParts g{};
-  g.b[P] = T;
-  for (int k = P; k >= 1; --k) g.b[k - 1] = arg[k][g.b[k]];
-  for (int k = P + 1; k <= kGlMaxParts; ++k) g.b[k] = T;
+  for (int k = 0; k < P; ++k) {
+    g.p[k].n = bnd[k + 1] - bnd[k];
+    int r0 = nt;
+    for (int t = bnd[k]; t < bnd[k + 1] && t - bnd[k] < kGlMaxPartTiles; ++t) {
+      const int ti = tri_row_host(t, nt);
+      int rem = t;
+      for (int r = 0; r < ti; ++r) rem -= nt - r;
+      g.p[k].tile[t - bnd[k]] = static_cast<uint16_t>(ti | ((ti + rem) << 8));
+      r0 = std::min(r0, ti);
+    }
+    gl_set_features(g.p[k], 16 * r0, 16 * (nt - r0), 0, 0);
+  }
   return g;
 }
 
@@ -2495,23 +2711,35 @@ static GlParts gram_i8l_split(int nt, int P, int cap) {
 // XCD's 32 CUs), at least one k-step each and at most kGlMaxRows rows each
 // (the int32 level sums); a multiple of 8 (the XCD map and
 // gram_tri_reduce_kernel) and <= 128 -- mmb_gram_i8 cuts larger calls into
-// blocks of kGlBlockRows rows.
+// blocks of kGlBlockRows rows.  The parts depend on nt and the shape only:
+// built once per (shape, nt) and cached (the dynamic program costs ~0.1 ms
+// of host time, more than a small split's whole Gram).
 constexpr int64_t kGlBlockRows = 128 * kGlMaxRows;
 
-template <class S>
+static int gram_i8l_ranges(int64_t n, int P) {
+  const int64_t resident = 256 / P / 8 * 8;
+  int64_t R = std::min<int64_t>(resident, std::max<int64_t>(1, n / kGiRows));
+  R = std::max<int64_t>(R, ceil_div(n, kGlMaxRows));
+  if (R >= 8) R = ceil_div(R, 8) * 8;
+  return static_cast<int>(std::min<int64_t>(R, 128));
+}
+
+template <class S, bool GROUPS>
 static GramLPlan gram_i8l_plan(int64_t n, int d) {
   GramLPlan q;
   q.nt = static_cast<int>(ceil_div(d, 16));
   q.T = q.nt * (q.nt + 1) / 2;
   q.P = S::kP;
-  const int64_t resident = 256 / S::kP / 8 * 8;
-  int64_t R = std::min<int64_t>(resident, std::max<int64_t>(1, n / kGiRows));
-  R = std::max<int64_t>(R, ceil_div(n, kGlMaxRows));
-  if (R >= 8) R = ceil_div(R, 8) * 8;
-  q.R = static_cast<int>(std::min<int64_t>(R, 128));
+  q.R = gram_i8l_ranges(n, S::kP);
   q.xcd = (q.R % 8 == 0) ? 1 : 0;
   q.chunk = ceil_div(ceil_div(std::max<int64_t>(n, 1), q.R), kGiRows) * kGiRows;
-  q.parts = gram_i8l_split(q.nt, S::kP, S::kPartMax);
+  static GlParts cache[kGiF / 16 + 1];
+  static bool have[kGiF / 16 + 1] = {};
+  if (!have[q.nt]) {
+    cache[q.nt] = GROUPS ? gl_parts_groups3(q.nt) : gl_parts_runs(q.nt, S::kP, S::kPartMax);
+    have[q.nt] = true;
+  }
+  q.parts = cache[q.nt];
   return q;
 }
 
@@ -2529,12 +2757,17 @@ static size_t gram_i8l_lds() {
 
 // One block of <= kGlBlockRows rows: the level-sum kernel, then the range
 // reduction (writing or accumulating into g).
-template <int DIAG, class S>
+template <int DIAG, class S, bool GROUPS>
 static int gram_i8l_block(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
                           int accumulate, double* part, hipStream_t stream) {
-  const GramLPlan q = gram_i8l_plan<S>(n, d);
-  for (int k = 0; k < q.P; ++k) MMB_REQUIRE(q.parts.b[k + 1] - q.parts.b[k] <= S::kPartMax);
-  MMB_REQUIRE(q.parts.b[q.P] == q.T);
+  const GramLPlan q = gram_i8l_plan<S, GROUPS>(n, d);
+  int tiles = 0;
+  for (int k = 0; k < q.P; ++k) {  // every tile once, within the shape's tiles and items
+    MMB_REQUIRE(q.parts.p[k].n <= S::kPartMax);
+    MMB_REQUIRE((q.parts.p[k].n0 + q.parts.p[k].n1) * 4 <= S::kIt * S::kNT);
+    tiles += q.parts.p[k].n;
+  }
+  MMB_REQUIRE(tiles == q.T);
   // the buffer-descriptor record count and row offsets are 32-bit byte counts of one range
   MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
   gram_i8l_kernel<DIAG, S><<<S::kP * q.R, S::kNT, gram_i8l_lds<DIAG, S>(), stream>>>(
@@ -2548,21 +2781,24 @@ static int gram_i8l_block(const float* x, const uint32_t* colmax, int64_t n, int
 
 #ifdef MMB_DIAG
 // tools build: the level-sum kernel's shape (MMB_GRAM_I8_SHAPE: 0 the
-// product's 4 parts x 8 waves x 6 tiles, 1 three parts x 8 waves x 8 tiles,
-// 2 four parts x 8 waves x 7 tiles) and its timing-only ablations
+// product's three feature-group parts x 8 waves x 8 tiles, 1 four triangle
+// runs x 8 waves x 6 tiles, 2 three triangle runs x 8 waves x 8 tiles, 3 the
+// product with LDS reads free to cross tiles, 4 the product with the next
+// tile's first B digit prefetched, 5 the product with staggered slicing) and
+// its timing-only ablations
 static int gram_i8_shape() {
   const char* e = getenv("MMB_GRAM_I8_SHAPE");
   return e ? atoi(e) : 0;
 }
-template <class S>
+template <class S, bool GROUPS>
 static int gram_i8l_block_diag(const float* x, const uint32_t* colmax, int64_t n, int d,
                                double* g, int accumulate, double* part, hipStream_t stream) {
   switch (gram_i8_diag()) {
-    case 1: return gram_i8l_block<1, S>(x, colmax, n, d, g, accumulate, part, stream);
-    case 4: return gram_i8l_block<4, S>(x, colmax, n, d, g, accumulate, part, stream);
-    case 12: return gram_i8l_block<12, S>(x, colmax, n, d, g, accumulate, part, stream);
-    case 13: return gram_i8l_block<13, S>(x, colmax, n, d, g, accumulate, part, stream);
-    default: return gram_i8l_block<0, S>(x, colmax, n, d, g, accumulate, part, stream);
+    case 1: return gram_i8l_block<1, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
+    case 4: return gram_i8l_block<4, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
+    case 12: return gram_i8l_block<12, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
+    case 13: return gram_i8l_block<13, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
+    default: return gram_i8l_block<0, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
   }
 }
 #endif
@@ -2579,8 +2815,9 @@ extern "C" size_t mmb_gram_workspace_bytes(int64_t n, int d) {
   const Gram2Plan qi = gram_i8_plan(n, d);
   const size_t v3 = static_cast<size_t>(qi.R) * qi.T * 256 * sizeof(double);
   // the level-sum kernel: at most 128 ranges per block (every shape)
-  const GramLPlan ql = gram_i8l_plan<GlShape<2, 8, 12>>(std::min(n, kGlBlockRows), d);
-  const size_t v4 = static_cast<size_t>(ql.R) * ql.T * 256 * sizeof(double);
+  const int64_t ntl = ceil_div(d, 16);
+  const size_t v4 = static_cast<size_t>(gram_i8l_ranges(std::min(n, kGlBlockRows), 2)) *
+                    (ntl * (ntl + 1) / 2) * 256 * sizeof(double);  // every shape's ranges bound
   const size_t v23 = std::max(std::max(v2, v3), v4);
   return v1 > v23 ? v1 : v23;
 }
@@ -2590,6 +2827,12 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
   MMB_REQUIRE(num && g && ws && n >= 0 && d > 0);
   double* part = static_cast<double*>(ws);
   const int64_t total = static_cast<int64_t>(d) * d;
+  if (n <= kGsMaxN && d <= 320) {  // small splits: tile-parallel, one launch, no partials
+    const int nt = static_cast<int>(ceil_div(d, 16));
+    gram_small_kernel<<<nt * (nt + 1) / 2, kGsNT, 0, stream>>>(num, cnt, n, d, nt, accumulate, g);
+    MMB_LAUNCH_CHECK();
+    return MMB_OK;
+  }
   if (gram2_ok(num, d)) {
     const Gram2Plan q = gram2_plan(n, d);
     const size_t lds = gram2_lds();
@@ -2663,12 +2906,15 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
 #ifdef MMB_DIAG
     int rc;
     switch (gram_i8_shape()) {
-      case 1: rc = gram_i8l_block_diag<GlShape<3, 8, 8>>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 2: rc = gram_i8l_block_diag<GlShape<4, 8, 7>>(xb, colmax, nb, d, g, acc, part, stream); break;
-      default: rc = gram_i8l_block_diag<GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 1: rc = gram_i8l_block_diag<GlShape<4, 8, 6, 3>, false>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 2: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 3>, false>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 3: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0x100>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 4: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 5: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, false, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      default: rc = gram_i8l_block_diag<GlProduct, true>(xb, colmax, nb, d, g, acc, part, stream); break;
     }
 #else
-    const int rc = gram_i8l_block<0, GlProduct>(xb, colmax, nb, d, g, acc, part, stream);
+    const int rc = gram_i8l_block<0, GlProduct, true>(xb, colmax, nb, d, g, acc, part, stream);
 #endif
     if (rc != MMB_OK) return rc;
     b0 += nb;

@@ -68,7 +68,11 @@ def check_flag(flag: torch.Tensor, V: int, zero_weights: bool = False):
     ValueError for an utterance whose weights are all 0 -- its a2 row is
     0/0 = NaN (sif_functions.py:55) and the reference's TruncatedSVD rejects
     the split (sklearn check_array: "Input X contains NaN")."""
-    f = int(flag.item())
+    check_flag_bits(int(flag.item()), V, zero_weights)
+
+
+def check_flag_bits(f: int, V: int, zero_weights: bool = False):
+    """check_flag on flag bits already read back."""
     if f & L.MMB_FLAG_SYNC_TIMEOUT:
         raise RuntimeError("a bounded in-kernel hand-over timed out (mmb_mm2_stream_project's "
                            "streaming / projecting waves, or mmb_pc_solve_mc's workgroups); "
@@ -79,6 +83,10 @@ def check_flag(flag: torch.Tensor, V: int, zero_weights: bool = False):
         raise ValueError("Input X contains NaN: an utterance whose SIF weights are all 0 has a "
                          "0/0 weighted average (sif_functions.py:55), which the reference's "
                          "TruncatedSVD rejects (sif_functions.py:65-67)")
+
+
+# status word of a checked step: the flag bits | PC_NONFINITE (FusedStep.status)
+PC_NONFINITE = 1 << 16
 
 
 # ------------------------------------------------------------------ a1
@@ -791,15 +799,30 @@ class FusedStep:
             t = torch.stack([(flag[0] & b) != 0 for b in bits]).to(torch.int32)
             self.allreduce(t)
             flag = sum((t[i] > 0).to(torch.int32) * b for i, b in enumerate(bits)).reshape(1)
+        self.raise_status(int(self.status(flag).item()))  # the one device sync
+
+    def status(self, flag=None, out=None) -> torch.Tensor:
+        """[1] int32 on the device: the flag bits | PC_NONFINITE when the last
+        step's PC is not finite -- what check() reads back, formed without a
+        sync (StepGraph captures it into the graph)."""
+        flag = self.flag if flag is None else flag
         pc = getattr(self, "pc", None)
-        if self.solve_ws is not None and (int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT or (
-                pc is not None and not bool(torch.isfinite(pc).all()))):
+        if pc is None:
+            return torch.add(flag, 0, out=out)
+        nonfinite = (~torch.isfinite(pc)).any().to(torch.int32)
+        return torch.add(flag, nonfinite * PC_NONFINITE, out=out)
+
+    def raise_status(self, v: int):
+        """check()'s verdict on a status word read back (status())."""
+        if self.solve_ws is not None and v & (L.MMB_FLAG_SYNC_TIMEOUT | PC_NONFINITE):
             # an aborted solve leaves its control words set (and a NaN PC):
             # hand the next launch a zeroed workspace again
             self.solve_ws[:16].zero_()
-        check_flag(flag, self.V, zero_weights=True)
-        if getattr(self, "pc", None) is not None:
-            check_pc_finite(self.pc)
+        check_flag_bits(v & (PC_NONFINITE - 1), self.V, zero_weights=True)
+        if v & PC_NONFINITE:
+            raise ValueError("Input X contains NaN or infinity: the split's Gram is not finite "
+                             "(an all-zero-weight utterance on some rank, or non-finite inputs), "
+                             "which the reference's TruncatedSVD rejects (sif_functions.py:65-67)")
 
     def reset(self):
         self.flag.zero_()
@@ -997,6 +1020,10 @@ class StepGraph:
             st.reset()
         self._branches = ([torch.cuda.Stream(device=dev) for _ in self.steps]
                           if concurrent and len(self.steps) > 1 else None)
+        # every step's status word (FusedStep.status) is formed inside the
+        # graph, so a checked replay reads ONE small tensor back (one sync for
+        # all steps; check() per step took up to four)
+        self._status = torch.zeros(len(self.steps), dtype=torch.int32, device=dev)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             cap = torch.cuda.current_stream(dev)
@@ -1010,12 +1037,19 @@ class StepGraph:
                         self.outs.append(st._run(None))
                 for br in self._branches:
                     cap.wait_stream(br)
+            for i, st in enumerate(self.steps):
+                if st.allreduce is None:
+                    st.status(out=self._status[i:i + 1])
 
     def run(self, check: bool = False):
         for st in self.steps:
             st.proj.refresh_if_changed()
         self.graph.replay()
         if check:
-            for st in self.steps:
-                st.check()
+            words = self._status.tolist()  # the one sync
+            for st, v in zip(self.steps, words):
+                if st.allreduce is not None:
+                    st.check()  # (its flag bits cross ranks: check()'s all-reduce)
+                else:
+                    st.raise_status(v)
         return self.outs if len(self.steps) > 1 else self.outs[0]
