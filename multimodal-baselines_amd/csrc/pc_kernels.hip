@@ -339,7 +339,13 @@ constexpr int kGiDig = 4;       // base-256 digits per value
 constexpr int kGiMaxTiles = 12; // tiles per wave (<= 96 per workgroup: d <= 304)
 constexpr int kGiItems = kGiF / 16 * 16 * 4;  // (feature, 16-row slot) items per chunk
 
-__host__ __device__ constexpr int gi_swz(int f) { return (0x78 >> (2 * ((f >> 2) & 3))) & 3; }
+// 16-byte slot swizzle of a feature's 64-byte digit row: slot kq of feature
+// f sits at kq ^ gi_swz(f).  (f >> 1) & 3 keeps the MFMA operand reads
+// (ds_read_b128 lane groups: features 16 t + (l & 15) at slot l >> 4)
+// conflict-free AND the slicing writes (ds_write_b128 groups of 8 lanes = 8
+// consecutive features at one slot) -- the r04 swizzle over f >> 2 left the
+// writes 2-way (checked exhaustively, r05).
+__host__ __device__ constexpr int gi_swz(int f) { return (f >> 1) & 3; }
 
 using i32x4 = __attribute__((ext_vector_type(4))) int;
 
@@ -875,8 +881,11 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
 }
 
 // product shape: three workgroups per range (80 ranges), 8 waves, <= 8 tiles
-// per wave, each slicing two of three feature groups (<= 2 items per thread)
-using GlProduct = GlShape<3, 8, 8, 2>;
+// per wave, each slicing two of three feature groups (<= 2 items per
+// thread), staggered slicing between SIMD partners (r05, tools/gram_ab.py at
+// 1M x 300: 0.62-0.63 ms vs 0.65-0.66 unstaggered, 0.77-0.80 for r04's
+// kernel; 125k: 0.095 vs 0.099 / 0.122)
+using GlProduct = GlShape<3, 8, 8, 2, 0, false, true>;
 
 // colmax[j] = max_i |x[i, j]| as float bits (atomicMax on the bits of a
 // non-negative float orders like the float); a NaN bound wins (non-finite x
@@ -2784,8 +2793,8 @@ static int gram_i8l_block(const float* x, const uint32_t* colmax, int64_t n, int
 // product's three feature-group parts x 8 waves x 8 tiles, 1 four triangle
 // runs x 8 waves x 6 tiles, 2 three triangle runs x 8 waves x 8 tiles, 3 the
 // product with LDS reads free to cross tiles, 4 the product with the next
-// tile's first B digit prefetched, 5 the product with staggered slicing) and
-// its timing-only ablations
+// tile's first B digit prefetched, 5 the product without the staggered
+// slicing) and its timing-only ablations
 static int gram_i8_shape() {
   const char* e = getenv("MMB_GRAM_I8_SHAPE");
   return e ? atoi(e) : 0;
@@ -2908,9 +2917,9 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
     switch (gram_i8_shape()) {
       case 1: rc = gram_i8l_block_diag<GlShape<4, 8, 6, 3>, false>(xb, colmax, nb, d, g, acc, part, stream); break;
       case 2: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 3>, false>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 3: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0x100>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 4: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 5: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, false, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 3: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0x100, false, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 4: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, true, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 5: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
       default: rc = gram_i8l_block_diag<GlProduct, true>(xb, colmax, nb, d, g, acc, part, stream); break;
     }
 #else

@@ -6,10 +6,10 @@
 x = the a2 rows of a bench-shaped FusedStep (1M x 300, Zipf ids), so the
 column bounds are the step's own.  Per size: the round-4 kernel
 (MMB_GRAM_I8_V1=1: per-k-step f64 updates), the level-sum kernel in each
-shape (MMB_GRAM_I8_SHAPE 0 = product: three feature-group parts; 1: four
-triangle runs; 2: three triangle runs, spilling; 3: the product with LDS reads
-free to cross tiles; 4: with the next tile's first B digit prefetched; 5:
-staggered slicing between SIMD partners) and
+shape (MMB_GRAM_I8_SHAPE 0 = product: three feature-group parts, slicing
+staggered between SIMD partners; 1: four triangle runs; 2: three triangle
+runs, spilling; 3: the product with LDS reads free to cross tiles; 4: with
+the next tile's first B digit prefetched; 5: unstaggered) and
 the product shape's
 timing-only ablations (MMB_GRAM_DIAG 1 no MFMAs, 4 no slicing, 12 no slicing
 and no x loads, 13 only barriers / LDS / epilogue), alternated over rounds;
@@ -34,12 +34,12 @@ import synth  # noqa: E402
 
 VARIANTS = {
     "v1_r04": {"MMB_GRAM_I8_V1": "1"},
-    "levels_groups3": {},
+    "levels_groups3_stagger": {},
     "levels_runs4x6": {"MMB_GRAM_I8_SHAPE": "1"},
     "levels_runs3x8": {"MMB_GRAM_I8_SHAPE": "2"},
     "levels_groups3_sb": {"MMB_GRAM_I8_SHAPE": "3"},
     "levels_groups3_pf": {"MMB_GRAM_I8_SHAPE": "4"},
-    "levels_groups3_stagger": {"MMB_GRAM_I8_SHAPE": "5"},
+    "levels_groups3_plain": {"MMB_GRAM_I8_SHAPE": "5"},
     "abl_no_mfma": {"MMB_GRAM_DIAG": "1"},
     "abl_no_slice": {"MMB_GRAM_DIAG": "4"},
     "abl_no_slice_no_load": {"MMB_GRAM_DIAG": "12"},
