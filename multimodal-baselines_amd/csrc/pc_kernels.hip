@@ -1463,11 +1463,13 @@ struct P16Lds {
   double* part;  // [16 waves][256]
 };
 
-// M (k x k, compact) = X^T Y over the Dp rows of two [Dp][16] blocks.
+// M (k x k, compact) = X^T Y over the Dp rows of two [Dp][16] blocks (NW
+// waves: every thread of the workgroup).
+template <int NW = kP16NT / kWave>
 __device__ __forceinline__ void p16_gram(const double* X, const double* Y, int Dp, int k, double* part, double* M) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   f64x4 acc = {0, 0, 0, 0};
-  for (int p = 4 * wave; p < Dp; p += 4 * (kP16NT / kWave)) {
+  for (int p = 4 * wave; p < Dp; p += 4 * NW) {
     const int o = (p + (lane >> 4)) * kP16W + (lane & 15);
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(X[o], Y[o], acc, 0, 0, 0);
   }
@@ -1478,7 +1480,7 @@ __device__ __forceinline__ void p16_gram(const double* X, const double* Y, int D
     const int i = tid >> 4, j = tid & 15;
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < kP16NT / kWave; ++w) s += part[w * 256 + tid];
+    for (int w = 0; w < NW; ++w) s += part[w * 256 + tid];
     if (i < k && j < k) M[i * k + j] = s;
   }
   __syncthreads();
@@ -1748,21 +1750,22 @@ struct P16Small {
 // finder: W = Z^T G Z, H = (GZ)^T (GZ), the k x k generalised eigenproblem
 // H y = s^2 W y (Cholesky of W, A = L^-1 H L^-T), v = GZ L^-T u, svd_flip
 // (extmath.py:537-566); the transposed branch takes A = Q^T G Q, v = Q u.
+template <int NW = kP16NT / kWave>
 __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int D, int Dp, int k,
                                          int npc, int transposed, double* part, const P16Small& sm,
                                          double* __restrict__ pc_out, const double* Hpre = nullptr) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   if (transposed) {
-    p16_gram(Z, GZ, Dp, k, part, sm.A);  // Q^T G Q
+    p16_gram<NW>(Z, GZ, Dp, k, part, sm.A);  // Q^T G Q
     symmetrize(sm.A, k);
     __syncthreads();
   } else {
-    p16_gram(Z, GZ, Dp, k, part, sm.W);   // W = Z^T G Z
+    p16_gram<NW>(Z, GZ, Dp, k, part, sm.W);   // W = Z^T G Z
     if (Hpre) {                           // H = (GZ)^T (GZ), summed by the caller
       if (threadIdx.x < k * k) sm.T[threadIdx.x] = Hpre[threadIdx.x];
       __syncthreads();
     } else {
-      p16_gram(GZ, GZ, Dp, k, part, sm.T);
+      p16_gram<NW>(GZ, GZ, Dp, k, part, sm.T);
     }
     symmetrize(sm.W, k);
     symmetrize(sm.T, k);
@@ -1848,7 +1851,7 @@ __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int 
     __syncthreads();
     double tot = 0.0, bb = -1.0;
     int bi = 0x7fffffff;
-    for (int w = 0; w < kP16NT / kWave; ++w) {
+    for (int w = 0; w < NW; ++w) {
       tot += sm.rd[w];
       if (sm.rv[w] > bb || (sm.rv[w] == bb && sm.ri[w] < bi)) {
         bb = sm.rv[w];
@@ -1989,10 +1992,11 @@ __device__ __forceinline__ bool pm_arrive(unsigned* ctr, int T, int r, unsigned*
 }
 
 // Out [Dp][16] = In [Dp][16] M^T for a 16 x 16 M (row-major, zero past k):
-// the 16-row tiles over the waves, 4 MFMA k-steps each.  In != Out.
+// the 16-row tiles over the NW waves, 4 MFMA k-steps each.  In != Out.
+template <int NW = kP16NT / kWave>
 __device__ __forceinline__ void p16_rmul(const double* In, const double* M, double* Out, int Dp) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  for (int t = wave; t < Dp / 16; t += kP16NT / kWave) {
+  for (int t = wave; t < Dp / 16; t += NW) {
     f64x4 acc = {0, 0, 0, 0};
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
@@ -2031,12 +2035,17 @@ __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* 
   PC_WMARK(34);
 }
 
-__global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,
-                                                               const double* __restrict__ z0, int k,
-                                                               int npc, int n_iter, int transposed,
-                                                               double* __restrict__ pc_out,
-                                                               double* xbuf, unsigned* ctl,
-                                                               int32_t* flag) {
+#ifdef MMB_DIAG
+// The r03-r04 round (tools build, MMB_PC_SOLVE_V1=1 for A/B runs): the
+// Cholesky of W_r on wave 15 beside the partials of G_t B_r, then the
+// exchange of Y_t = G_t B_r M_r^T and P_t = Y_t^T Y_t -- the factor (~5.5 us
+// of a ~11 us round) and the exchange (~4.5 us) in sequence.
+__global__ __launch_bounds__(kP16NT) void pc_solve_mc_v1_kernel(const double* __restrict__ G, int D,
+                                                                  const double* __restrict__ z0, int k,
+                                                                  int npc, int n_iter, int transposed,
+                                                                  double* __restrict__ pc_out,
+                                                                  double* xbuf, unsigned* ctl,
+                                                                  int32_t* flag) {
   extern __shared__ __attribute__((aligned(16))) double p16_lds[];
   const int Dp = (D + 15) / 16 * 16;
   const int T = Dp / 16;
@@ -2284,6 +2293,374 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_kernel(const double* __res
   PC_MARK(40);
   p16_tail(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT);
 }
+#endif  // MMB_DIAG
+
+// Since r05 an implicit round exchanges the RAW product H_t = G_t B_r, which
+// needs no factor of W_r, so the equilibrated Cholesky of W_r (the last wave) runs
+// beside the whole exchange -- partials, publish, the wait for the other
+// workgroups and the gather of H = G B_r -- instead of before it.  After the
+// join every workgroup forms B_{r+1} = H M_r^T (the tiles Y_t of r04, the
+// same MFMAs on the same operands) and W_{r+1} = B_{r+1}^T B_{r+1} from its
+// own copy of the rows (per-wave partial Grams summed in a fixed wave order:
+// identical in all workgroups), so the exchange carries 16 x 16 per tile
+// instead of 16 x 32.  The partial waves synchronise among themselves through
+// an LDS arrival counter while the last wave factors (s_barrier would wait
+// for it).  A round whose factor fails (a pivot <= 0) drops H and runs a
+// second exchange of G_t Z for the MGS^2-orthonormalised block; the round
+// entering the tail is the r04 round (the factor beside the partials,
+// explicit CholeskyQR2 rows for the transposed branch).  Exchange x
+// (counting the extra ones) arrives at T x .. T (x + 1) - 1 and uses tile
+// buffer x & 1.
+//
+// 8 waves, not r04's 16: at 1024 threads a wave has 128 VGPRs, and with the
+// factor's 16-entry rows, the G fragments and the gather's loads in one
+// kernel the compiler spilled ~70 VGPRs -- the G fragments reloaded from
+// scratch before every MFMA, the gather's addresses spilled and reloaded
+// around every load (probe: the round's non-factor work 2x slower than its
+// operations).  At 512 threads there are 256.
+constexpr int kPnNT = 512;
+constexpr int kPnNW = kPnNT / kWave;                   // 8
+constexpr int kPnPw = kPnNW - 1;                       // waves holding G (the last one factors)
+constexpr int kPnKs = (kP16MaxD / 4 + kPnPw - 1) / kPnPw;  // k-steps of G per wave (12)
+constexpr int kPnGu = (kPmMaxT * 256 + kPnPw * kWave - 1) / (kPnPw * kWave);  // gather loads per thread (12)
+
+__global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,
+                                                               const double* __restrict__ z0, int k,
+                                                               int npc, int n_iter, int transposed,
+                                                               double* __restrict__ pc_out,
+                                                               double* xbuf, unsigned* ctl,
+                                                               int32_t* flag) {
+  extern __shared__ __attribute__((aligned(16))) double p16_lds[];
+  const int Dp = (D + 15) / 16 * 16;
+  int T = Dp / 16;
+  double* sZ = p16_lds;          // H = G B_r (implicit rounds); the explicit block Z
+  double* sY = sZ + Dp * kP16W;  // the raw block B_r (z0, then G Z_{r-1}); G Z for the tail
+  double* part = sY + Dp * kP16W;  // max(16 x 256, Dp x 16)
+  P16_SMALL_DECL
+  __shared__ double sHt[256], sYt[256], sM[256], sM2[256], sd[kMaxK];
+  __shared__ int s_abort;
+  __shared__ unsigned s_bar;
+  int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int t = blockIdx.x;
+  unsigned* ctr = ctl;
+  unsigned* abort_w = ctl + 1;
+
+  // this workgroup's 16 rows of G as MFMA A fragments on waves 0-6 (G
+  // symmetric: row p of the tile = column p, 16 consecutive doubles per k-row:
+  // coalesced); wave 7 is free for the k x k factor that overlaps the rest
+  double ga[kPnKs];
+  {
+    const int p = t * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < kPnKs; ++j) {
+      const int q = 4 * (wave + kPnPw * j) + (lane >> 4);
+      ga[j] = (wave < kPnPw && p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
+    }
+  }
+  // waves 0-6: their partial products of this tile of G with a [Dp][16] block
+  auto tile_partials = [&](const double* B) {
+    if (wave < kPnPw) {
+      f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < kPnKs; ++j) {
+        const int q = 4 * (wave + kPnPw * j) + (lane >> 4);
+        if (4 * (wave + kPnPw * j) < Dp)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], B[q * kP16W + (lane & 15)], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+    }
+  };
+  // ... summed over the waves in a fixed order (threads 0-255; the caller
+  // synchronises before and after)
+  auto tile_sum = [&](double* out) {
+    if (tid < 256) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < kPnPw; ++w) s += part[w * 256 + tid];
+      out[tid] = s;
+    }
+  };
+  auto tile_product = [&](const double* B, double* out) {
+    tile_partials(B);
+    __syncthreads();
+    tile_sum(out);
+    __syncthreads();
+  };
+  // the barrier of waves 0-6 while wave 7 factors: every wave adds one
+  // arrival to an LDS counter after its LDS writes, then polls for the
+  // phase's 7 arrivals (the counter only grows within a launch)
+  unsigned bar_target = 0;
+  auto bar_pw = [&]() {
+    bar_target += kPnPw;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) {
+      __hip_atomic_fetch_add(&s_bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      while (__hip_atomic_load(&s_bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < bar_target)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+  // MGS^2 of the k columns of a [Dp][16] block on wave 0 (extreme
+  // ill-conditioning: a Cholesky pivot <= 0), in place
+  auto mgs = [&](double* B) {
+    if (wave == 0) {
+      for (int e = lane; e < D * k; e += kWave) part[e] = B[(e / k) * kP16W + e % k];
+      wave_lds_sync();
+      orth_wave(part, D, k, lane);
+      for (int e = lane; e < D * k; e += kWave) B[(e / k) * kP16W + e % k] = part[e];
+    }
+    __syncthreads();
+  };
+  // wave 0: publishes this workgroup's 16 x 16 tile for exchange x with
+  // write-through 8-byte stores, drains them and adds one arrival; then waits
+  // for all T (not after the final exchange, except workgroup 0, which then
+  // returns the counter to zero: every workgroup has made its last arrival,
+  // so the next launch -- eager or a graph replay -- finds it at 0 with no
+  // memset node in front of it).  A failed arrival or wait sets s_abort.
+  auto publish = [&](const double* tile, int x, bool final_x) {
+    double* xb = xbuf + static_cast<int64_t>(x & 1) * T * 256;
+    wave_lds_sync();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = lane + kWave * u;
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(xb + t * 256 + e),
+                         __builtin_bit_cast(unsigned long long, tile[e]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      // release: the tile stores above are visible at agent scope before
+      // the arrival that announces them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (!pm_arrive(ctr, T, x, abort_w, flag)) {
+        s_abort = 1;
+      } else if (!(final_x && t != 0)) {
+        if (!pm_wait(ctr, static_cast<unsigned>(T * (x + 1)), abort_w, flag)) {
+          s_abort = 1;
+        } else if (final_x) {
+          __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // acquire: the gather reads the other workgroups' tiles only after
+        // their arrivals were observed (the barrier that follows releases the
+        // other waves of this workgroup)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+    }
+  };
+  // every tile of exchange x into the rows of dst by the first nthr threads
+  // (element f = tid + nthr u of the T x 256 published doubles), all of a
+  // thread's loads (sc1, 8 B) issued before any is used (a load-then-store
+  // loop waited ~1.5 us per load)
+  auto gather = [&](double* dst, int x, int nthr) {
+    if (tid < nthr) {
+      const double* xb = xbuf + static_cast<int64_t>(x & 1) * T * 256;
+      double v[kPnGu];
+#pragma unroll
+      for (int u = 0; u < kPnGu; ++u) {
+        const int f = tid + nthr * u;
+        v[u] = f < T * 256 ? __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(xb + f),
+                                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                           : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kPnGu; ++u) {
+        const int f = tid + nthr * u;
+        if (f < T * 256) dst[((f >> 8) * 16 + ((f >> 4) & 15)) * kP16W + (f & 15)] = v[u];
+      }
+    }
+  };
+  // no caller may go on with a stale PC: an aborted solve leaves NaN in
+  // pc_out (every aborting workgroup writes the same NaNs; workgroup 0
+  // cannot complete the tail once any workgroup has left).  After a barrier.
+  auto aborted = [&]() -> bool {
+    if (!s_abort) return false;
+    for (int e = tid; e < npc * D; e += kPnNT) pc_out[e] = __builtin_nan("");
+    return true;
+  };
+
+  for (int e = tid; e < Dp * kP16W; e += kPnNT) {
+    const int p = e / kP16W, j = e % kP16W;
+    sY[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
+    sZ[e] = 0.0;
+  }
+  if (tid == 0) {
+    s_abort = 0;
+    s_bar = 0;
+  }
+  __syncthreads();
+  PC_MARK(0);
+  p16_gram<kPnNW>(sY, sY, Dp, k, part, sW);  // W_0 = B_0^T B_0 (every workgroup: identical)
+  PC_MARK(1);
+
+  int x = 0;  // the exchange
+  const int T0 = T, k0 = k;
+  for (int r = 0; r < n_iter; ++r) {
+    {
+      // the round's LDS addresses, bounds and per-lane indices are rebuilt
+      // from an opaque zero every round: left loop-invariant, the compiler
+      // hoisted all of them out of the loop (hundreds of values held across
+      // the kernel) and spilled the G fragments and the gather's addresses
+      int zo = 0;
+      asm volatile("" : "+s"(zo));
+      sZ = p16_lds + zo;
+      sY = sZ + Dp * kP16W;
+      part = sY + Dp * kP16W;
+      T = T0 + zo;
+      k = k0 + zo;
+      tid = static_cast<int>(threadIdx.x) + zo;
+      lane = tid & (kWave - 1);
+    }
+    if (wave == kPnPw) {
+      p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);  // M_r, beside the exchange
+    } else {
+      tile_partials(sY);
+      bar_pw();
+      tile_sum(sHt);  // H_t = G_t B_r
+      bar_pw();
+      if (wave == 0) {
+        publish(sHt, x, false);
+        PC_WMARK(2 + 3 * r);
+      }
+      bar_pw();
+      gather(sZ, x, kPnPw * kWave);  // H = G B_r
+      if (wave == 0) PC_WMARK(3 + 3 * r);
+    }
+    ++x;
+    __syncthreads();  // the join: M_r, s_fail and H
+    PC_MARK(44 + 2 * r);
+    if (aborted()) return;
+    if (s_fail) {
+      // the equilibrated rows of B_r orthonormalised by MGS^2 (H is dropped),
+      // then a second exchange of G_t Z
+      for (int e = tid; e < Dp * kP16W; e += kPnNT) {
+        const int p = e / kP16W, j = e % kP16W;
+        sZ[e] = (p < D && j < k) ? sY[e] * sd[j] : 0.0;
+      }
+      __syncthreads();
+      mgs(sZ);
+      tile_product(sZ, sHt);
+      if (wave == 0) publish(sHt, x, false);
+      __syncthreads();
+      if (aborted()) return;
+      gather(sY, x, kPnNT);  // B_{r+1} = G Z
+      ++x;
+      __syncthreads();
+      p16_gram<kPnNW>(sY, sY, Dp, k, part, sW);  // W_{r+1}
+    } else {
+      // B_{r+1} = H M_r^T tile by tile (all 8 waves), each wave's tiles' Grams
+      // accumulated in its MFMA registers; W_{r+1} = their fixed-order sum
+      f64x4 pa = {0, 0, 0, 0};
+      for (int tt = wave; tt < T; tt += kPnNW) {
+        f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const int m = 4 * st + (lane >> 4);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sZ[(tt * 16 + (lane & 15)) * kP16W + m],
+                                                     sM[(lane & 15) * kP16W + m], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) sY[(tt * 16 + (lane >> 4) + 4 * reg) * kP16W + (lane & 15)] = acc[reg];
+        wave_lds_sync();
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const double y = sY[(tt * 16 + 4 * st + (lane >> 4)) * kP16W + (lane & 15)];
+          pa = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, pa, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = pa[reg];
+      if (wave == 0) PC_WMARK(35);
+      __syncthreads();
+      if (wave == 0) PC_WMARK(36);
+      if (tid < 256) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kPnNW; ++w) s += part[w * 256 + tid];
+        const int i = tid >> 4, j = tid & 15;
+        if (i < k && j < k) sW[i * k + j] = s;
+      }
+      __syncthreads();
+    }
+    PC_MARK(45 + 2 * r);
+  }
+
+  // the round entering the tail (r04's): the factor of W beside the partials
+  // of G_t B, then the block Z of the tail.  The direct branch's tail is a
+  // generalised eigenproblem on span(Z), invariant to the basis, so its block
+  // stays implicit (Y_t = H_t M^T; workgroup 0 forms Z's rows); a failed
+  // pivot (MGS^2) or the transposed branch (an orthonormal Q: CholeskyQR2)
+  // forms explicit rows
+  if (wave == kPnPw) {
+    p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);
+  } else {
+    tile_partials(sY);
+  }
+  __syncthreads();
+  PC_MARK(44 + 2 * n_iter);
+  const bool explicit_z = transposed || s_fail;
+  if (!explicit_z && t == 0) p16_rmul<kPnNW>(sY, sM, sZ, Dp);  // Z = B M^T
+  if (explicit_z) {
+    if (s_fail) {  // the equilibrated rows, orthonormalised by MGS^2
+      for (int e = tid; e < Dp * kP16W; e += kPnNT) {
+        const int p = e / kP16W, j = e % kP16W;
+        sZ[e] = (p < D && j < k) ? sY[e] * sd[j] : 0.0;
+      }
+      __syncthreads();
+      mgs(sZ);
+    } else {
+      p16_rmul<kPnNW>(sY, sM, sZ, Dp);  // Z1 = B M1^T
+      __syncthreads();
+      p16_gram<kPnNW>(sZ, sZ, Dp, k, part, sW);  // second CholeskyQR pass on the rows
+      if (wave == 0) {
+        if (lane == 0) s_fail = 0;
+        wave_lds_sync();
+        p16_chol(sW, sL, sLi, k, lane, &s_fail);
+        for (int e = lane; e < 256; e += kWave) {
+          const int j = e / kP16W, m = e % kP16W;
+          sM2[e] = (j < k && m <= j) ? sLi[j * k + m] : 0.0;
+        }
+      }
+      __syncthreads();
+      if (s_fail) {
+        mgs(sZ);
+      } else {
+        p16_rmul<kPnNW>(sZ, sM2, sY, Dp);  // Z = Z1 L2^-T (sY free: B is no longer needed)
+        __syncthreads();
+        for (int e = tid; e < Dp * kP16W; e += kPnNT) sZ[e] = sY[e];
+        __syncthreads();
+      }
+    }
+    tile_product(sZ, sYt);  // Y_t = G_t Z
+  } else {
+    tile_sum(sHt);  // H_t = G_t B (its partials formed beside the Cholesky)
+    __syncthreads();
+    if (wave == 0) {  // Y_t = H_t M^T
+      f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int m = 4 * st + (lane >> 4);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sHt[(lane & 15) * 16 + m], sM[(lane & 15) * 16 + m],
+                                                   acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) sYt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+    }
+  }
+  if (wave == 0) publish(sYt, x, true);
+  if (t != 0) return;  // the tail runs on workgroup 0 only
+  __syncthreads();
+  PC_MARK(45 + 2 * n_iter);
+  if (aborted()) return;
+  gather(sY, x, kPnNT);  // G Z
+  __syncthreads();
+  p16_gram<kPnNW>(sY, sY, Dp, k, part, sW);  // (G Z)^T (G Z)
+  for (int e = tid; e < k * k; e += kPnNT) sT[e] = sW[e];
+  __syncthreads();
+  PC_MARK(40);
+  p16_tail<kPnNW>(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT);
+}
 
 inline size_t p16_lds_bytes(int d) {
   const size_t dp = (d + 15) / 16 * 16;
@@ -2381,7 +2758,10 @@ __global__ __launch_bounds__(256) void pc_remove_kernel(const TX* __restrict__ n
 // dependent load -> dot -> sum -> store chain per wave; the PC's lane values
 // stay in registers.  Arithmetic (f64 fma order, shuffle-tree wave sum, f32
 // rounding) is pc_remove_kernel<4, 2>'s: bit-identical.
-template <int R>
+// NT (tools build, MMB_PC_REMOVE_NT=1): x read and the rows written
+// non-temporally -- an A/B of whether the removal's 2 x N x D x 4 bytes evict
+// the word rows the next step's fused kernel would find in L2 / MALL
+template <int R, bool NT = false>
 __global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict__ num,
                                                          const float* __restrict__ cnt, int64_t N,
                                                          int D, const double* __restrict__ pc,
@@ -2404,8 +2784,17 @@ __global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict
     for (int r = 0; r < R; ++r) {
       const int64_t row = min(base + r, N - 1);
       const float* src = num + row * D;
-      v[r][0] = lane < U ? *reinterpret_cast<const float4*>(src + 4 * lane) : make_float4(0.f, 0.f, 0.f, 0.f);
-      v[r][1] = h1 ? *reinterpret_cast<const float4*>(src + 4 * (lane + kWave)) : make_float4(0.f, 0.f, 0.f, 0.f);
+      auto ld = [](const float* q) {
+        if constexpr (NT) {
+          using f4 = float __attribute__((ext_vector_type(4)));
+          const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4*>(q));
+          return make_float4(t.x, t.y, t.z, t.w);
+        } else {
+          return *reinterpret_cast<const float4*>(q);
+        }
+      };
+      v[r][0] = lane < U ? ld(src + 4 * lane) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[r][1] = h1 ? ld(src + 4 * (lane + kWave)) : make_float4(0.f, 0.f, 0.f, 0.f);
       sc[r] = cnt ? cnt[row] : 1.f;
     }
     double x[R][2][4], d[R];
@@ -2445,7 +2834,12 @@ __global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict
           q.y = static_cast<float>(x[r][m][1] - fma(d[r], p[m][1], 0.0));
           q.z = static_cast<float>(x[r][m][2] - fma(d[r], p[m][2], 0.0));
           q.w = static_cast<float>(x[r][m][3] - fma(d[r], p[m][3], 0.0));
-          *reinterpret_cast<float4*>(dst + 4 * (lane + kWave * m)) = q;
+          if constexpr (NT) {
+            using f4 = float __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(f4{q.x, q.y, q.z, q.w}, reinterpret_cast<f4*>(dst + 4 * (lane + kWave * m)));
+          } else {
+            *reinterpret_cast<float4*>(dst + 4 * (lane + kWave * m)) = q;
+          }
         }
       }
     }
@@ -3019,7 +3413,18 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
   // flag.  Since r05 every arrival checks the count it finds (pm_arrive) and
   // every wait the abort word first, so a dirty workspace aborts with
   // MMB_FLAG_SYNC_TIMEOUT and a NaN PC instead
-  pc_solve_mc_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
+#ifdef MMB_DIAG
+  if (const char* e = getenv("MMB_PC_SOLVE_V1"); e && atoi(e) != 0) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve_mc_v1_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(p16_lds_bytes(kP16MaxD)));
+    pc_solve_mc_v1_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
+                                                                   pc_out, xbuf, ctl, flag);
+    MMB_LAUNCH_CHECK();
+    return MMB_OK;
+  }
+#endif
+  pc_solve_mc_kernel<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
                                                               pc_out, xbuf, ctl, flag);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
@@ -3040,7 +3445,10 @@ extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int 
     const int64_t waves = ceil_div(n, rr);
     const int grid = static_cast<int>(std::min<int64_t>(ceil_div(waves, 4), 256 * 8));
 #ifdef MMB_DIAG
-    if (rr == 2) {
+    const char* nte = getenv("MMB_PC_REMOVE_NT");
+    if (nte && atoi(nte) != 0 && rr == 4) {
+      pc_remove1_kernel<4, true><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
+    } else if (rr == 2) {
       pc_remove1_kernel<2><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
     } else if (rr == 8) {
       pc_remove1_kernel<8><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);

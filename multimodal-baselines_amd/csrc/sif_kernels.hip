@@ -130,33 +130,41 @@ __device__ __forceinline__ void stage_token(const StreamArgs& a, int64_t i, int 
 // (flagged) are dropped: they contribute nothing (sif_functions.py:8-15).
 constexpr int kStageIters = (kTokChunk + kNT - 1) / kNT;
 
-template <bool MM2, int VT, int VA, int VV>
-__global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
+// FU: frame rows (and TU: text rows) per thread in flight -- 4 / 4 when the
+// grid fills the chip (occupancy hides the latency); for a few hundred long
+// rows (dataset splits: one workgroup per CU at most, so one workgroup's
+// loads in flight set the time; POM's 100-row valid split spent 0.18 ms in 68
+// rounds of 4 frame loads per thread) NT = 1024 threads with 8 / 4.  NT
+// changes the f32 order of the row sums (RT = NT / CT row slots).
+template <bool MM2, int VT, int VA, int VV, int FU = 4, int TU = 4, int NT = kNT>
+__global__ __launch_bounds__(NT) void utt_stream_kernel(StreamArgs a) {
+  constexpr int kRF = NT * 4;  // one accumulator image: R*F <= NT*VEC
+  constexpr int kSI = (kTokChunk + NT - 1) / NT;
   __shared__ int64_t s_off[kTokChunk];
   __shared__ float s_w[kTokChunk];
-  __shared__ float s_red[(MM2 ? 4 : 1) * kRedFloats];
-  __shared__ float s_cnt[kNT / kWave], s_sw[kNT / kWave];
-  __shared__ float s_c0[kNT / kWave], s_w0[kNT / kWave];
-  __shared__ int s_keep[kStageIters][kNT / kWave];
+  __shared__ float s_red[(MM2 ? 4 : 1) * kRF];
+  __shared__ float s_cnt[NT / kWave], s_sw[NT / kWave];
+  __shared__ float s_c0[NT / kWave], s_w0[NT / kWave];
+  __shared__ int s_keep[kSI][NT / kWave];
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), wave = tid / kWave;
   // text lane map: CT column units of VT floats, RT row slots
   const int CT = a.D / VT;
-  const int RT = kNT / CT;
+  const int RT = NT / CT;
   const int rT = tid / CT, cT = tid - (tid / CT) * CT;
   const bool actT = rT < RT;
   // audio / visual lane maps
-  const int CA = MM2 ? a.A / VA : 1, RA = kNT / CA;
+  const int CA = MM2 ? a.A / VA : 1, RA = NT / CA;
   const int rA = tid / CA, cA = tid - rA * CA;
-  const int CV = MM2 ? a.Vd / VV : 1, RV = kNT / CV;
+  const int CV = MM2 ? a.Vd / VV : 1, RV = NT / CV;
   const int rV = tid / CV, cV = tid - rV * CV;
   const float* tsrc = a.ids ? a.table : a.text_dense;
   const float* esrc = a.ids ? a.table : a.emb_dense;
   const bool split_emb = MM2 && (esrc != tsrc);
 
   const bool gather = a.ids != nullptr;
-  float cmx0 = 0.f, cmx1 = 0.f;  // running max |x| of columns tid, tid + kNT (MMB2)
+  float cmx0 = 0.f, cmx1 = 0.f;  // running max |x| of columns tid, tid + NT (MMB2)
   for (int64_t i = blockIdx.x; i < a.N; i += gridDim.x) {
     float num[VT], sx[VT], sxx[VT];
 #pragma unroll
@@ -165,13 +173,13 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
 
     for (int t0 = 0; t0 < a.L; t0 += kTokChunk) {
       const int tl = min(kTokChunk, a.L - t0);
-      int64_t off_k[kStageIters];
-      float w_k[kStageIters];
-      int rank_k[kStageIters];
-      bool keep_k[kStageIters];
+      int64_t off_k[kSI];
+      float w_k[kSI];
+      int rank_k[kSI];
+      bool keep_k[kSI];
 #pragma unroll
-      for (int k = 0; k < kStageIters; ++k) {
-        const int t = tid + k * kNT;
+      for (int k = 0; k < kSI; ++k) {
+        const int t = tid + k * NT;
         int64_t off = -1;
         float w = 0.f;
         if (t < tl) {
@@ -194,8 +202,8 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       __syncthreads();
       int nkeep = 0;
 #pragma unroll
-      for (int k = 0; k < kStageIters; ++k) {
-        for (int v = 0; v < kNT / kWave; ++v) {
+      for (int k = 0; k < kSI; ++k) {
+        for (int v = 0; v < NT / kWave; ++v) {
           if (keep_k[k] && v == wave) s_off[nkeep + rank_k[k]] = off_k[k];
           if (keep_k[k] && v == wave) s_w[nkeep + rank_k[k]] = w_k[k];
           nkeep += s_keep[k][v];
@@ -207,7 +215,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         // 0 and contributes nothing, so the unrolled iterations keep their
         // loads in flight together (a `continue` per token would wait on
         // each load right after its branch)
-#pragma unroll 4
+#pragma unroll TU
         for (int t = rT; t < nkeep; t += RT) {
           const float w = s_w[t];
           const int64_t off = s_off[t];
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
     if constexpr (MM2) {
       if (rA < RA) {
         const float* base = a.audio + (i * a.L) * a.A + cA * VA;
-#pragma unroll 4
+#pragma unroll FU
         for (int t = rA; t < a.L; t += RA) {
           float v[VA];
           ldv_nt<VA>(base + static_cast<int64_t>(t) * a.A, v);
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       }
       if (rV < RV) {
         const float* base = a.visual + (i * a.L) * a.Vd + cV * VV;
-#pragma unroll 4
+#pragma unroll FU
         for (int t = rV; t < a.L; t += RV) {
           float v[VV];
           ldv_nt<VV>(base + static_cast<int64_t>(t) * a.Vd, v);
@@ -292,22 +300,22 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         const int f = rT * a.D + cT * VT + e;
         s_red[f] = num[e];
         if constexpr (MM2) {
-          s_red[kRedFloats + f] = sx[e];
-          s_red[2 * kRedFloats + f] = sxx[e];
+          s_red[kRF + f] = sx[e];
+          s_red[2 * kRF + f] = sxx[e];
         }
       }
     }
     __syncthreads();
     float cnt = 0.f, sw = 0.f, c0 = 0.f, w0 = 0.f;
 #pragma unroll
-    for (int w = 0; w < kNT / kWave; ++w) {
+    for (int w = 0; w < NT / kWave; ++w) {
       cnt += s_cnt[w];
       sw += s_sw[w];
       c0 += s_c0[w];
       w0 += s_w0[w];
     }
     float smax = 0.f;  // max |sum| of this thread's part of the row (MMB2)
-    for (int f = tid; f < a.D; f += kNT) {
+    for (int f = tid; f < a.D; f += NT) {
       float n_ = 0.f;
       for (int r = 0; r < RT; ++r) n_ += s_red[r * a.D + f];
       // row 0 once for its c0 tokens (gather mode; c0 = 0 otherwise)
@@ -316,14 +324,14 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
       if constexpr (MM2) {
         float x1 = 0.f, x2 = 0.f;
         for (int r = 0; r < RT; ++r) {
-          x1 += s_red[kRedFloats + r * a.D + f];
-          x2 += s_red[2 * kRedFloats + r * a.D + f];
+          x1 += s_red[kRF + r * a.D + f];
+          x2 += s_red[2 * kRF + r * a.D + f];
         }
         x1 = fmaf(c0, e0, x1);
         x2 = fmaf(c0 * e0, e0, x2);
         const float xf = n_ / cnt;
         a.num_out[i * a.D + f] = xf;  // x = the a2 row (sif_functions.py:55)
-        if (f < kNT) cmx0 = bmax(cmx0, fabsf(xf)); else cmx1 = bmax(cmx1, fabsf(xf));
+        if (f < NT) cmx0 = bmax(cmx0, fabsf(xf)); else cmx1 = bmax(cmx1, fabsf(xf));
         a.s_out[i * a.Kp + f] = x1;
         a.s_out[i * a.Kp + a.D + f] = x2;
         smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
@@ -349,47 +357,47 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
         for (int e = 0; e < VA; ++e) {
           const int f = rA * a.A + cA * VA + e;
           s_red[f] = sa[e];
-          s_red[kRedFloats + f] = saa[e];
+          s_red[kRF + f] = saa[e];
         }
       }
       if (rV < RV) {
 #pragma unroll
         for (int e = 0; e < VV; ++e) {
           const int f = rV * a.Vd + cV * VV + e;
-          s_red[2 * kRedFloats + f] = sv[e];
-          s_red[3 * kRedFloats + f] = svv[e];
+          s_red[2 * kRF + f] = sv[e];
+          s_red[3 * kRF + f] = svv[e];
         }
       }
       __syncthreads();
       float* srow = a.s_out + i * a.Kp + 2 * a.D;
-      for (int f = tid; f < a.A; f += kNT) {
+      for (int f = tid; f < a.A; f += NT) {
         float x1 = 0.f, x2 = 0.f;
         for (int r = 0; r < RA; ++r) {
           x1 += s_red[r * a.A + f];
-          x2 += s_red[kRedFloats + r * a.A + f];
+          x2 += s_red[kRF + r * a.A + f];
         }
         srow[f] = x1;
         srow[a.A + f] = x2;
         smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
       }
-      for (int f = tid; f < a.Vd; f += kNT) {
+      for (int f = tid; f < a.Vd; f += NT) {
         float x1 = 0.f, x2 = 0.f;
         for (int r = 0; r < RV; ++r) {
-          x1 += s_red[2 * kRedFloats + r * a.Vd + f];
-          x2 += s_red[3 * kRedFloats + r * a.Vd + f];
+          x1 += s_red[2 * kRF + r * a.Vd + f];
+          x2 += s_red[3 * kRF + r * a.Vd + f];
         }
         srow[2 * a.A + f] = x1;
         srow[2 * a.A + a.Vd + f] = x2;
         smax = fmaxf(smax, fmaxf(fabsf(x1), fabsf(x2)));
       }
       const int k = 2 * (a.D + a.A + a.Vd);
-      for (int f = k + tid; f < a.Kp; f += kNT) a.s_out[i * a.Kp + f] = 0.f;
+      for (int f = k + tid; f < a.Kp; f += NT) a.s_out[i * a.Kp + f] = 0.f;
       smax = wave_max(smax);
       if (lane == 0) s_cnt[wave] = smax;
       __syncthreads();
       if (tid == 0) {
         float m = 0.f;
-        for (int w = 0; w < kNT / kWave; ++w) m = fmaxf(m, s_cnt[w]);
+        for (int w = 0; w < NT / kWave; ++w) m = fmaxf(m, s_cnt[w]);
         a.aux_out[2 * a.N + i] = row_scale(m);
       }
     }
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(kNT) void utt_stream_kernel(StreamArgs a) {
   if (MM2 && a.cmax_part) {  // this workgroup's column bounds (mmb_gram_i8)
     float* pr = a.cmax_part + static_cast<int64_t>(blockIdx.x) * a.D;
     if (tid < a.D) pr[tid] = cmx0;
-    if (tid + kNT < a.D) pr[tid + kNT] = cmx1;
+    if (tid + NT < a.D) pr[tid + NT] = cmx1;
   }
 }
 
@@ -2284,7 +2292,26 @@ static int launch_stream(const StreamArgs& a, hipStream_t stream, int* parts = n
   int grid = stream_grid(a.N, 6, stream);
   if (a.cmax_part && grid > kCmaxRows) grid = kCmaxRows;
   if (parts) *parts = grid;
-  utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
+  if (MM2 && a.N <= stream_cu_count(stream)) {
+    // a few long rows (POM's splits: 100 / 203 rows of 1089 / 1357 tokens):
+    // 16 frame / 8 text rows in flight per group instead of 4 / 4 (r05
+    // tools/splits_ab.py, gpurun_out r05m: stream 0.180 -> 0.148 ms and
+    // 0.217 -> 0.188 ms, the same sums bit for bit; 1024 threads x 4 / 4:
+    // 0.157 / 0.193 ms)
+#ifdef MMB_DIAG
+    const char* e = getenv("MMB_STREAM_SMALL");  // 0: as large N, 1: 320 x 16 / 8, 2: 1024 x 4 / 4
+    const int v = e ? atoi(e) : 1;
+    if (v == 0) {
+      utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
+    } else if (v == 2) {
+      utt_stream_kernel<MM2, VT, VA, VV, 4, 4, 1024><<<grid, 1024, 0, stream>>>(a);
+    } else
+#endif
+    {
+      utt_stream_kernel<MM2, VT, VA, VV, 16, 8><<<grid, kNT, 0, stream>>>(a);
+    }
+  } else
+    utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

@@ -36,6 +36,13 @@ for step in "$@"; do
       timeout -k 10 300 python3 -u bench.py --only-main --no-cpu-baseline --steps 10 --warmup 3 \
         > "$OUT/main.json" 2> "$OUT/main.err" || exit $?
       ;;
+    pcprobe)  # phase marks of the multi-workgroup PC solve, r05 round and (V1) r04 round
+      timeout -k 10 60 tools/pc_probe/pc_probe_mc > "$OUT/pc_probe.txt" 2>&1 || exit $?
+      MMB_PC_SOLVE_V1=1 timeout -k 10 60 tools/pc_probe/pc_probe_mc_diag > "$OUT/pc_probe_v1.txt" 2>&1 || exit $?
+      ;;
+    splits)  # the dataset splits as one graph (tools/splits_ab.py)
+      timeout -k 10 300 python3 -u tools/splits_ab.py > "$OUT/splits_ab.txt" 2>&1 || exit $?
+      ;;
     *)
       echo "unknown step $step" >&2
       exit 2

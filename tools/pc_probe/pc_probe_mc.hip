@@ -1,7 +1,8 @@
 // Phase timing of pc_solve_mc_kernel (wall_clock64 marks of workgroup 0,
 // MMB_PC_PROBE build) and its PC against the one-workgroup solve.
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMMB_PC_PROBE -I../../include \
-//     pc_probe_mc.hip ../../multimodal-baselines_amd/csrc/host_rng.cpp -o pc_probe_mc
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMMB_PC_PROBE -DMMB_DIAG -I../../include \
+//     pc_probe_mc.hip ../../multimodal-baselines_amd/csrc/host_rng.cpp \
+//     ../../multimodal-baselines_amd/csrc/probe_kernels.hip -o pc_probe_mc
 #include "../../multimodal-baselines_amd/csrc/pc_kernels.hip"
 
 #include <algorithm>
@@ -50,15 +51,18 @@ int main() {
     (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(mmb::g_pc_probe), sizeof(t));
     auto us = [&](int i, int j) { return (double)(t[j] - t[i]) * 1e3 / rate; };
     printf("rep %d rc %d: kernel+memset %.1f us | gram0 %.1f", rep, rc, ms * 1e3, us(0, 1));
+    // r05 rounds: wave 0's partials + publish + wait, its gather, the join
+    // (wave 15's factor), then B_{r+1} = H M^T and W_{r+1}
     int prev = 1;
-    for (int r = 0; r <= 7; ++r) {
-      printf(" | r%d chol %.1f prod %.1f pub+wait %.1f gather %.1f", r, us(prev, 44 + 2 * r),
-             us(44 + 2 * r, 45 + 2 * r), us(45 + 2 * r, 2 + 3 * r), us(3 + 3 * r, 4 + 3 * r));
-      prev = 4 + 3 * r;
+    for (int r = 0; r < 7; ++r) {
+      printf(" | r%d pub+wait %.1f gather %.1f join %.1f rmul+W %.1f", r, us(prev, 2 + 3 * r),
+             us(2 + 3 * r, 3 + 3 * r), us(3 + 3 * r, 44 + 2 * r), us(44 + 2 * r, 45 + 2 * r));
+      prev = 45 + 2 * r;
     }
-    printf(" | tail-rr %.1f eig %.1f out %.1f", us(40, 41), us(41, 42), us(42, 43));
-    printf(" | last eq-chol: equilibrate %.2f factor %.2f substitute %.2f store %.2f\n", us(30, 31),
-           us(31, 32), us(32, 33), us(33, 34));
+    printf(" | last: chol %.1f Y+pub+wait %.1f", us(prev, 44 + 14), us(44 + 14, 45 + 14));
+    printf(" | tail gram+rr %.1f eig %.1f out %.1f", us(45 + 14, 41), us(41, 42), us(42, 43));
+    printf(" | last eq-chol %.2f (factor %.2f substitute %.2f)", us(30, 34), us(31, 32), us(32, 33));
+    printf(" | r6 rmul+W: tiles %.2f barrier %.2f sum %.2f\n", us(44 + 12, 35), us(35, 36), us(36, 45 + 12));
   }
   int32_t hflag = 0;
   (void)hipMemcpy(&hflag, flag, 4, hipMemcpyDeviceToHost);
