@@ -1033,15 +1033,27 @@ __global__ __launch_bounds__(256) void xt_omega_wave_kernel(const TX* __restrict
 // ------------------------------------------------------------------ pc_solve
 #ifdef MMB_PC_PROBE  // phase timestamps for tools/pc_probe.hip (never in libmmb)
 __device__ unsigned long long g_pc_probe[64];
-#define PC_MARK(i)                                                         \
-  do {                                                                     \
-    __syncthreads();                                                       \
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
+// The marks go to LDS and are copied out at the end of the kernel
+// (PC_PROBE_FLUSH): a global store per mark put its completion wait into the
+// next barrier's phase (r05: ~4 us of a round's update phase was the mark).
+__device__ __forceinline__ unsigned long long* pc_probe_lds() {
+  __shared__ unsigned long long s[64];
+  return s;
+}
+#define PC_MARK(i)                                                               \
+  do {                                                                           \
+    __syncthreads();                                                             \
+    if (threadIdx.x == 0 && blockIdx.x == 0) pc_probe_lds()[i] = wall_clock64(); \
   } while (0)
 // one wave's own mark (no barrier): lane 0 of the calling wave, workgroup 0
-#define PC_WMARK(i)                                                               \
-  do {                                                                            \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_pc_probe[i] = wall_clock64(); \
+#define PC_WMARK(i)                                                                     \
+  do {                                                                                  \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) pc_probe_lds()[i] = wall_clock64(); \
+  } while (0)
+#define PC_PROBE_FLUSH()                                                                    \
+  do {                                                                                      \
+    __syncthreads();                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x < 64) g_pc_probe[threadIdx.x] = pc_probe_lds()[threadIdx.x]; \
   } while (0)
 #else
 #define PC_MARK(i) \
@@ -1049,6 +1061,9 @@ __device__ unsigned long long g_pc_probe[64];
   } while (0)
 #define PC_WMARK(i) \
   do {              \
+  } while (0)
+#define PC_PROBE_FLUSH() \
+  do {                   \
   } while (0)
 #endif
 constexpr int kMaxD = 512;
@@ -1486,6 +1501,34 @@ __device__ __forceinline__ void p16_gram(const double* X, const double* Y, int D
   __syncthreads();
 }
 
+// M1 = X1^T Y1 and M2 = X2^T Y2 (k x k, compact) in one pass over the Dp rows
+// (the two sums as p16_gram's, one barrier pair instead of two).
+template <int NW>
+__device__ __forceinline__ void p16_gram2(const double* X1, const double* Y1, double* M1, const double* X2,
+                                          const double* Y2, double* M2, int Dp, int k, double* part) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  f64x4 a1 = {0, 0, 0, 0}, a2 = {0, 0, 0, 0};
+  for (int p = 4 * wave; p < Dp; p += 4 * NW) {
+    const int o = (p + (lane >> 4)) * kP16W + (lane & 15);
+    a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(X1[o], Y1[o], a1, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(X2[o], Y2[o], a2, 0, 0, 0);
+  }
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = a1[reg];
+    part[(NW + wave) * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = a2[reg];
+  }
+  __syncthreads();
+  if (tid < 512) {
+    const int e = tid & 255, i = e >> 4, j = e & 15, h = tid >> 8;
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += part[(h * NW + w) * 256 + e];
+    if (i < k && j < k) (h ? M2 : M1)[i * k + j] = s;
+  }
+  __syncthreads();
+}
+
 // GZ = G Z (G symmetric [D][D] in global memory / L2).  16 k-steps of loads
 // are issued before their MFMAs (one L2 latency per batch, not per step);
 // two accumulators alternate so consecutive MFMAs are independent.  (32-step
@@ -1555,14 +1598,14 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
 // of L^{-1}.  *fail is set if a pivot is not positive (the pivot is then
 // replaced by 1).
 __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, double* sLi, int k,
-                                              int lane, int* fail, double (&x)[kMaxK]) {
+                                              int lane, int* fail, double (&x)[kMaxK], int mark = 31) {
   // L's columns and the reciprocal pivots go to LDS as they are produced
   // (sLi's storage holds the pivots until the inverse overwrites it): at
   // 1024 threads a wave has 128 VGPRs, and the arrays of L and 1 / L_jj held
   // in registers spilled to scratch, one reload per substitution step
   double* rl = sLi;
   bool bad = false;
-  PC_WMARK(31);
+  PC_WMARK(mark);
 #pragma unroll
   for (int j = 0; j < kMaxK; ++j) {
     if (j < k) {
@@ -1579,7 +1622,7 @@ __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, do
   }
   if (bad && lane == 0) *fail = 1;
   wave_lds_sync();
-  PC_WMARK(32);
+  PC_WMARK(mark + 1);
   // column c = lane of Linv: forward substitution, L entries and the
   // reciprocal pivots read as LDS broadcasts
 #pragma unroll
@@ -1592,7 +1635,7 @@ __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, do
       x[i] = s * rl[kMaxK * kMaxK - kMaxK + i];
     }
   }
-  PC_WMARK(33);
+  PC_WMARK(mark + 2);
   wave_lds_sync();  // every lane has read the pivots before sLi is written
   if (lane < k) {
 #pragma unroll
@@ -1753,14 +1796,15 @@ struct P16Small {
 template <int NW = kP16NT / kWave>
 __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int D, int Dp, int k,
                                          int npc, int transposed, double* part, const P16Small& sm,
-                                         double* __restrict__ pc_out, const double* Hpre = nullptr) {
+                                         double* __restrict__ pc_out, const double* Hpre = nullptr,
+                                         bool wpre = false) {
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   if (transposed) {
     p16_gram<NW>(Z, GZ, Dp, k, part, sm.A);  // Q^T G Q
     symmetrize(sm.A, k);
     __syncthreads();
   } else {
-    p16_gram<NW>(Z, GZ, Dp, k, part, sm.W);   // W = Z^T G Z
+    if (!wpre) p16_gram<NW>(Z, GZ, Dp, k, part, sm.W);  // W = Z^T G Z (wpre: the caller's, in sm.W)
     if (Hpre) {                           // H = (GZ)^T (GZ), summed by the caller
       if (threadIdx.x < k * k) sm.T[threadIdx.x] = Hpre[threadIdx.x];
       __syncthreads();
@@ -1772,18 +1816,28 @@ __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int 
     __syncthreads();
     if (wave == 0) {
       p16_chol(sm.W, sm.L, sm.Li, k, lane, sm.fail);  // a failed pivot is clamped (W is SPD here)
-      for (int e = lane; e < k * k; e += kWave) {  // Linv H
-        const int i = e / k, j = e % k;
-        double s = 0.0;
-        for (int m = 0; m < k; ++m) s += sm.Li[i * k + m] * sm.T[m * k + j];
-        sm.V[e] = s;
+      // A = Linv H Linv^T on the matrix pipe (r05; two k^3 LDS loops before):
+      // U^T = H Linv^T lands in the accumulator layout that is the B operand
+      // of A = Linv U^T (k-step st = U^T's rows 4 st .. 4 st + 3), zero padded
+      // past k
+      const int r = lane & 15, g = lane >> 4;
+      f64x4 ut = {0, 0, 0, 0}, av = {0, 0, 0, 0};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int m = 4 * st + g;
+        const bool in = r < k && m < k;
+        ut = __builtin_amdgcn_mfma_f64_16x16x4f64(in ? sm.T[r * k + m] : 0.0, in ? sm.Li[r * k + m] : 0.0, ut, 0, 0,
+                                                  0);
       }
-      wave_lds_sync();
-      for (int e = lane; e < k * k; e += kWave) {  // (Linv H) Linv^T
-        const int i = e / k, j = e % k;
-        double s = 0.0;
-        for (int m = 0; m < k; ++m) s += sm.V[i * k + m] * sm.Li[j * k + m];
-        sm.A[e] = s;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int m = 4 * st + g;
+        av = __builtin_amdgcn_mfma_f64_16x16x4f64((r < k && m < k) ? sm.Li[r * k + m] : 0.0, ut[st], av, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int i = g + 4 * reg;
+        if (i < k && r < k) sm.A[i * k + r] = av[reg];
       }
       wave_lds_sync();
       for (int e = lane; e < k * k; e += kWave) {
@@ -1822,12 +1876,17 @@ __device__ __forceinline__ void p16_tail(const double* Z, const double* GZ, int 
       }
       __syncthreads();
     }
+    // v = row tid of Z u (transposed) or GZ y; each thread starts its row at
+    // column tid mod k: rows are 128 B apart, so lanes reading one column
+    // fell on 2 bank pairs (8-way conflicts)
     double v = 0.0;
     if (tid < D) {
-      if (transposed) {
-        for (int j = 0; j < k; ++j) v += Z[tid * kP16W + j] * u[j];
-      } else {
-        for (int j = 0; j < k; ++j) v += GZ[tid * kP16W + j] * sm.y[j];
+      const double* row = (transposed ? Z : GZ) + tid * kP16W;
+      const double* c = transposed ? u : sm.y;
+      int j = tid % k;
+      for (int q = 0; q < k; ++q) {
+        v += row[j] * c[j];
+        j = j + 1 == k ? 0 : j + 1;
       }
     }
     // norm and first argmax |v|
@@ -1916,6 +1975,7 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
   __syncthreads();
   PC_MARK(40);
   p16_tail(Z, GZ, D, Dp, k, npc, transposed, part, sm, pc_out);
+  PC_PROBE_FLUSH();
 }
 
 // ------------------------------------------------------------------ pc_solve, multi-workgroup (r03)
@@ -1991,9 +2051,10 @@ __device__ __forceinline__ bool pm_arrive(unsigned* ctr, int T, int r, unsigned*
   return false;
 }
 
-// Out [Dp][16] = In [Dp][16] M^T for a 16 x 16 M (row-major, zero past k):
-// the 16-row tiles over the NW waves, 4 MFMA k-steps each.  In != Out.
-template <int NW = kP16NT / kWave>
+// Out [Dp][16] = In [Dp][16] M^T for a 16 x 16 M (row-major, zero past k;
+// MT: M holds M^T, whose reads are conflict-free): the 16-row tiles over the
+// NW waves, 4 MFMA k-steps each.  In != Out.
+template <int NW = kP16NT / kWave, bool MT = false>
 __device__ __forceinline__ void p16_rmul(const double* In, const double* M, double* Out, int Dp) {
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   for (int t = wave; t < Dp / 16; t += NW) {
@@ -2002,7 +2063,8 @@ __device__ __forceinline__ void p16_rmul(const double* In, const double* M, doub
     for (int st = 0; st < 4; ++st) {
       const int m = 4 * st + (lane >> 4);
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(In[(t * 16 + (lane & 15)) * kP16W + m],
-                                                 M[(lane & 15) * kP16W + m], acc, 0, 0, 0);
+                                                 MT ? M[m * kP16W + (lane & 15)] : M[(lane & 15) * kP16W + m],
+                                                 acc, 0, 0, 0);
     }
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) Out[(t * 16 + (lane >> 4) + 4 * reg) * kP16W + (lane & 15)] = acc[reg];
@@ -2014,9 +2076,11 @@ __device__ __forceinline__ void p16_rmul(const double* In, const double* M, doub
 // M = L^-1 diag(d) (16 x 16, zero past k) is the right factor that
 // orthonormalises the block: Z = B M^T (one CholeskyQR pass after
 // equilibration, from the Gram alone).  d[] = the scales.  All in registers
-// (lane i = row i); *fail as p16_chol.
+// (lane i = row i); *fail as p16_chol.  Mt (optional) receives M^T, the
+// layout whose MFMA B-operand reads are conflict-free (M's own reads
+// M[j][m] for lanes j = 0..15 fall 16 doubles apart: 8-way LDS conflicts).
 __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* Li, double* M,
-                                            double* d, int k, int lane, int* fail) {
+                                            double* d, int k, int lane, int* fail, double* Mt = nullptr) {
   double w[kMaxK], x[kMaxK];
   PC_WMARK(30);
 #pragma unroll
@@ -2026,10 +2090,14 @@ __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* 
   for (int m = 0; m < kMaxK; ++m) w[m] *= di * readlane_f64(di, m);
   if (lane < kMaxK) d[lane] = lane < k ? di : 0.0;
   if (lane == 0) *fail = 0;
-  p16_chol_regs(w, L, Li, k, lane, fail, x);
+  p16_chol_regs(w, L, Li, k, lane, fail, x, 37);  // probe marks 37-39
   if (lane < kP16W) {  // lane c: column c of L^-1 diag(d)
 #pragma unroll
-    for (int i = 0; i < kP16W; ++i) M[i * kP16W + lane] = (lane < k && i < k) ? x[i] * di : 0.0;
+    for (int i = 0; i < kP16W; ++i) {
+      const double v = (lane < k && i < k) ? x[i] * di : 0.0;
+      M[i * kP16W + lane] = v;
+      if (Mt) Mt[lane * kP16W + i] = v;
+    }
   }
   wave_lds_sync();
   PC_WMARK(34);
@@ -2292,6 +2360,7 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_v1_kernel(const double* __
   __syncthreads();
   PC_MARK(40);
   p16_tail(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT);
+  PC_PROBE_FLUSH();
 }
 #endif  // MMB_DIAG
 
@@ -2324,6 +2393,9 @@ constexpr int kPnPw = kPnNW - 1;                       // waves holding G (the l
 constexpr int kPnKs = (kP16MaxD / 4 + kPnPw - 1) / kPnPw;  // k-steps of G per wave (12)
 constexpr int kPnGu = (kPmMaxT * 256 + kPnPw * kWave - 1) / (kPnPw * kWave);  // gather loads per thread (12)
 
+// ABL (tools build only, timing ablations, results invalid): 1 skips the
+// round's B_{r+1} / W_{r+1} update, 2 skips the round's factor
+template <int ABL = 0>
 __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,
                                                                const double* __restrict__ z0, int k,
                                                                int npc, int n_iter, int transposed,
@@ -2373,13 +2445,13 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
     }
   };
   // ... summed over the waves in a fixed order (threads 0-255; the caller
-  // synchronises before and after)
-  auto tile_sum = [&](double* out) {
+  // synchronises before and after); tr: the tile's transpose
+  auto tile_sum = [&](double* out, bool tr = false) {
     if (tid < 256) {
       double s = 0.0;
 #pragma unroll
       for (int w = 0; w < kPnPw; ++w) s += part[w * 256 + tid];
-      out[tid] = s;
+      out[tr ? (tid & 15) * 16 + (tid >> 4) : tid] = s;
     }
   };
   auto tile_product = [&](const double* B, double* out) {
@@ -2449,10 +2521,12 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       }
     }
   };
-  // every tile of exchange x into the rows of dst by the first nthr threads
-  // (element f = tid + nthr u of the T x 256 published doubles), all of a
-  // thread's loads (sc1, 8 B) issued before any is used (a load-then-store
-  // loop waited ~1.5 us per load)
+  // every tile of exchange x into dst by the first nthr threads (element f =
+  // tid + nthr u of the T x 256 published doubles, copied to dst[f]: a
+  // row-major tile lands as rows t*16.. of a [Dp][16] block, a transposed one
+  // as a [T][16][16] stack of transposed tiles), all of a thread's loads (sc1,
+  // 8 B) issued before any is used (a load-then-store loop waited ~1.5 us per
+  // load)
   auto gather = [&](double* dst, int x, int nthr) {
     if (tid < nthr) {
       const double* xb = xbuf + static_cast<int64_t>(x & 1) * T * 256;
@@ -2467,7 +2541,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
 #pragma unroll
       for (int u = 0; u < kPnGu; ++u) {
         const int f = tid + nthr * u;
-        if (f < T * 256) dst[((f >> 8) * 16 + ((f >> 4) & 15)) * kP16W + (f & 15)] = v[u];
+        if (f < T * 256) dst[f] = v[u];
       }
     }
   };
@@ -2513,18 +2587,18 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       lane = tid & (kWave - 1);
     }
     if (wave == kPnPw) {
-      p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);  // M_r, beside the exchange
+      if (!(ABL & 2)) p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);  // M_r, beside the exchange
     } else {
       tile_partials(sY);
       bar_pw();
-      tile_sum(sHt);  // H_t = G_t B_r
+      tile_sum(sHt, true);  // H_t^T, H_t = G_t B_r
       bar_pw();
       if (wave == 0) {
         publish(sHt, x, false);
         PC_WMARK(2 + 3 * r);
       }
       bar_pw();
-      gather(sZ, x, kPnPw * kWave);  // H = G B_r
+      gather(sZ, x, kPnPw * kWave);  // H = G B_r as T transposed tiles
       if (wave == 0) PC_WMARK(3 + 3 * r);
     }
     ++x;
@@ -2548,26 +2622,29 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       ++x;
       __syncthreads();
       p16_gram<kPnNW>(sY, sY, Dp, k, part, sW);  // W_{r+1}
-    } else {
+    } else if (!(ABL & 1)) {
       // B_{r+1} = H M_r^T tile by tile (all 8 waves), each wave's tiles' Grams
-      // accumulated in its MFMA registers; W_{r+1} = their fixed-order sum
+      // accumulated in its MFMA registers; W_{r+1} = their fixed-order sum.
+      // Both operands are read from transposed copies (H's tiles as
+      // gathered, M^T from the factor): lane (i, k) reads element 16 k + i,
+      // conflict-free, where the rows' own layout put the 16 i of a read 128 B
+      // apart (8-way bank conflicts: the update took ~5 us a round, r05
+      // tools/pc_probe/rmul_bench.hip).  The tile's Gram Y^T Y takes its
+      // operands straight from the accumulator: its k-step st is Y's rows
+      // 4 st .. 4 st + 3, which is acc[st] in both operand layouts.
       f64x4 pa = {0, 0, 0, 0};
       for (int tt = wave; tt < T; tt += kPnNW) {
         f64x4 acc = {0, 0, 0, 0};
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
           const int m = 4 * st + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sZ[(tt * 16 + (lane & 15)) * kP16W + m],
-                                                     sM[(lane & 15) * kP16W + m], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sZ[tt * 256 + m * 16 + (lane & 15)],
+                                                     sM2[m * kP16W + (lane & 15)], acc, 0, 0, 0);
         }
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) sY[(tt * 16 + (lane >> 4) + 4 * reg) * kP16W + (lane & 15)] = acc[reg];
-        wave_lds_sync();
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          const double y = sY[(tt * 16 + 4 * st + (lane >> 4)) * kP16W + (lane & 15)];
-          pa = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, pa, 0, 0, 0);
-        }
+        for (int st = 0; st < 4; ++st) pa = __builtin_amdgcn_mfma_f64_16x16x4f64(acc[st], acc[st], pa, 0, 0, 0);
       }
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = pa[reg];
@@ -2593,14 +2670,13 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   // pivot (MGS^2) or the transposed branch (an orthonormal Q: CholeskyQR2)
   // forms explicit rows
   if (wave == kPnPw) {
-    p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);
+    p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);
   } else {
     tile_partials(sY);
   }
   __syncthreads();
   PC_MARK(44 + 2 * n_iter);
   const bool explicit_z = transposed || s_fail;
-  if (!explicit_z && t == 0) p16_rmul<kPnNW>(sY, sM, sZ, Dp);  // Z = B M^T
   if (explicit_z) {
     if (s_fail) {  // the equilibrated rows, orthonormalised by MGS^2
       for (int e = tid; e < Dp * kP16W; e += kPnNT) {
@@ -2634,14 +2710,14 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
     }
     tile_product(sZ, sYt);  // Y_t = G_t Z
   } else {
-    tile_sum(sHt);  // H_t = G_t B (its partials formed beside the Cholesky)
+    tile_sum(sHt, true);  // H_t^T, H_t = G_t B (its partials formed beside the Cholesky)
     __syncthreads();
-    if (wave == 0) {  // Y_t = H_t M^T
+    if (wave == 0) {  // Y_t = H_t M^T from the transposes (conflict-free reads)
       f64x4 acc = {0, 0, 0, 0};
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         const int m = 4 * st + (lane >> 4);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sHt[(lane & 15) * 16 + m], sM[(lane & 15) * 16 + m],
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sHt[m * 16 + (lane & 15)], sM2[m * 16 + (lane & 15)],
                                                    acc, 0, 0, 0);
       }
 #pragma unroll
@@ -2650,16 +2726,23 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   }
   if (wave == 0) publish(sYt, x, true);
   if (t != 0) return;  // the tail runs on workgroup 0 only
+  // workgroup 0 forms Z = B M^T for the tail while wave 0 waits for the
+  // other workgroups' tiles (before r05 the product preceded its publish,
+  // and every workgroup waited for it).  (Keeping B's tiles transposed for
+  // conflict-free A reads here cost the round's update more than it saved:
+  // the transposed stores are the conflicted pattern, r05x.)
+  if (!explicit_z) p16_rmul<kPnNW, true>(sY, sM2, sZ, Dp);
   __syncthreads();
   PC_MARK(45 + 2 * n_iter);
   if (aborted()) return;
   gather(sY, x, kPnNT);  // G Z
   __syncthreads();
-  p16_gram<kPnNW>(sY, sY, Dp, k, part, sW);  // (G Z)^T (G Z)
-  for (int e = tid; e < k * k; e += kPnNT) sT[e] = sW[e];
-  __syncthreads();
+  // the direct branch's two Grams in one pass: H = (G Z)^T (G Z), W = Z^T G Z
+  // (the transposed branch forms its own Q^T G Q in the tail)
+  if (!transposed) p16_gram2<kPnNW>(sY, sY, sT, sZ, sY, sW, Dp, k, part);
   PC_MARK(40);
-  p16_tail<kPnNW>(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT);
+  p16_tail<kPnNW>(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT, !transposed);
+  PC_PROBE_FLUSH();
 }
 
 inline size_t p16_lds_bytes(int d) {
@@ -3396,7 +3479,7 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
   double* xbuf = reinterpret_cast<double*>(static_cast<char*>(ws) + 16);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve_mc_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve_mc_kernel<0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(p16_lds_bytes(kP16MaxD)));
     attr = true;
@@ -3420,6 +3503,17 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
                               static_cast<int>(p16_lds_bytes(kP16MaxD)));
     pc_solve_mc_v1_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
                                                                    pc_out, xbuf, ctl, flag);
+    MMB_LAUNCH_CHECK();
+    return MMB_OK;
+  }
+#endif
+#ifdef MMB_DIAG
+  if (const char* e = getenv("MMB_PC_ABL"); e && atoi(e) != 0) {
+    const int abl = atoi(e);
+    auto kern = abl == 1 ? pc_solve_mc_kernel<1> : abl == 2 ? pc_solve_mc_kernel<2> : pc_solve_mc_kernel<3>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(p16_lds_bytes(kP16MaxD)));
+    kern<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out, xbuf, ctl, flag);
     MMB_LAUNCH_CHECK();
     return MMB_OK;
   }

@@ -6,7 +6,10 @@ against the r04 round (MMB_PC_SOLVE_V1=1: Cholesky, then the exchange,
 Gram (d = 300, k = 11, 7 power iterations), alternated over rounds; and the
 two PCs against each other.
 
-    python tools/pc_ab.py [--reps 200] [--rounds 5]
+    python tools/pc_ab.py [--reps 200] [--rounds 5] [--iters 7] [--ablations]
+
+(several --iters: the per-round cost is the slope over n_iter; --ablations
+adds the r05 kernel without the round's update / factor / both, timing only)
 """
 import argparse
 import json
@@ -27,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, nargs="+", default=[7])
+    ap.add_argument("--ablations", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(1)
@@ -36,32 +41,38 @@ def main():
     z0 = torch.randn(d, k, generator=g, dtype=torch.float64).to(dev)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     pc = torch.empty((1, d), dtype=torch.float64, device=dev)
-    out = {"new": [], "v1": []}
+    out = {}
     pcs = {}
 
-    def run(name):
-        if name == "v1":
-            os.environ["MMB_PC_SOLVE_V1"] = "1"
-        else:
-            os.environ.pop("MMB_PC_SOLVE_V1", None)
-        P.pc_solve(G, z0, 1, False, out=pc, flag=flag)
+    variants = {"new": {}, "v1": {"MMB_PC_SOLVE_V1": "1"}}
+    if args.ablations:  # timing only: the round without its update (1), factor (2), both (3)
+        variants.update({f"abl{a}": {"MMB_PC_ABL": str(a)} for a in (1, 2, 3)})
+
+    def run(name, it):
+        for key in ("MMB_PC_SOLVE_V1", "MMB_PC_ABL"):
+            os.environ.pop(key, None)
+        os.environ.update(variants[name])
+        P.pc_solve(G, z0, 1, False, n_iter=it, out=pc, flag=flag)
         torch.cuda.synchronize()
-        pcs[name] = pc.clone()
+        pcs[(name, it)] = pc.clone()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(args.reps):
-            P.pc_solve(G, z0, 1, False, out=pc, flag=flag)
+            P.pc_solve(G, z0, 1, False, n_iter=it, out=pc, flag=flag)
         b.record()
         torch.cuda.synchronize()
-        out[name].append(round(a.elapsed_time(b) * 1e3 / args.reps, 2))
+        out.setdefault(f"{name}_iter{it}", []).append(round(a.elapsed_time(b) * 1e3 / args.reps, 2))
 
     for _ in range(args.rounds):
-        for name in ("new", "v1"):
-            run(name)
-    os.environ.pop("MMB_PC_SOLVE_V1", None)
+        for it in args.iters:
+            for name in variants:
+                run(name, it)
+    for key in ("MMB_PC_SOLVE_V1", "MMB_PC_ABL"):
+        os.environ.pop(key, None)
     res = {"us_per_solve": out, "us_min": {k_: min(v) for k_, v in out.items()},
            "flag": int(flag.item()),
-           "pc_maxdiff_new_vs_v1": float((pcs["new"] - pcs["v1"]).abs().max())}
+           "pc_maxdiff_new_vs_v1": {str(it): float((pcs[("new", it)] - pcs[("v1", it)]).abs().max())
+                                    for it in args.iters}}
     print(json.dumps(res), flush=True)
 
 

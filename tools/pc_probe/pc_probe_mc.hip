@@ -60,8 +60,11 @@ int main() {
       prev = 45 + 2 * r;
     }
     printf(" | last: chol %.1f Y+pub+wait %.1f", us(prev, 44 + 14), us(44 + 14, 45 + 14));
-    printf(" | tail gram+rr %.1f eig %.1f out %.1f", us(45 + 14, 41), us(41, 42), us(42, 43));
-    printf(" | last eq-chol %.2f (factor %.2f substitute %.2f)", us(30, 34), us(31, 32), us(32, 33));
+    printf(" | tail gather+grams %.1f rr %.1f eig %.1f out %.1f", us(45 + 14, 40), us(40, 41), us(41, 42),
+           us(42, 43));
+    printf(" | last eq-chol %.2f (equilibrate %.2f factor %.2f substitute %.2f store %.2f)", us(30, 34),
+           us(30, 37), us(37, 38), us(38, 39), us(39, 34));
+    printf(" | tail chol: factor %.2f substitute %.2f", us(31, 32), us(32, 33));
     printf(" | r6 rmul+W: tiles %.2f barrier %.2f sum %.2f\n", us(44 + 12, 35), us(35, 36), us(36, 45 + 12));
   }
   int32_t hflag = 0;
