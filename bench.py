@@ -195,7 +195,11 @@ def load_traffic(name, utts_per_launch, tokens, phase="mm2_stream"):
 
 def run_workload(P, inp, gen, steps, warmup, allreduce=None, world=1, rank=0):
     """FusedStep over `inp`: warmup, then `steps` timed steps bracketed by
-    barrier + synchronize.  Returns (step, elapsed_s, per-step traces)."""
+    barrier + synchronize, then the same number of steps again with HIP
+    events around each phase (the per-phase times and the kernels' launch
+    durations; r05: the events are no longer inside the timed region, where
+    their ~12 markers per step added to the stream).  Returns (step,
+    elapsed_s, per-step traces)."""
     import torch
     import torch.distributed as dist
 
@@ -204,18 +208,22 @@ def run_workload(P, inp, gen, steps, warmup, allreduce=None, world=1, rank=0):
     for _ in range(warmup):
         step.run()
     torch.cuda.synchronize()
-    traces = [dict() for _ in range(steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        step.run(trace=traces[k])
+    for _ in range(steps):
+        step.run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     step.check()  # ids in range, no all-zero-weight utterance (one sync, after timing)
+    traces = [dict() for _ in range(steps)]
+    for k in range(steps):
+        step.run(trace=traces[k])
+    torch.cuda.synchronize()
+    step.check()
     return step, elapsed, traces
 
 
@@ -1128,15 +1136,17 @@ def main():
         step.run()
     torch.cuda.synchronize()
 
-    # timed region: K steps, barrier + sync on both sides.  HIP events are
-    # recorded on the stream each phase is launched on (FusedStep.run trace).
-    traces = [dict() for _ in range(args.steps)]
+    # timed region: K steps, barrier + sync on both sides.  Then K more steps
+    # with HIP events recorded on the stream each phase is launched on
+    # (FusedStep.run trace) for phase_ms and the kernels' launch durations --
+    # outside the timed region (r05: ~12 event markers per step had been
+    # inside it)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step.run(trace=traces[k])
+    for _ in range(args.steps):
+        step.run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1146,6 +1156,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     step.check()  # ids in range, no all-zero-weight utterance, finite PC (every rank)
+    traces = [dict() for _ in range(args.steps)]
+    for k in range(args.steps):
+        step.run(trace=traces[k])
+    torch.cuda.synchronize()
+    step.check()
     if args.dump_rows:
         dump_rows(args.dump_rows, rank, row0, step)
 
