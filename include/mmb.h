@@ -250,7 +250,9 @@ int mmb_mm2_split_pieces(const float* wm, int d, int a, int vd, int ldw, void* i
  * rows as float bits, the input of mmb_gram_i8 -- a by-product of the stream
  * kernel (per-wave running maxima into colmax_ws, then one fixed-order reduce
  * launch) instead of a second pass over x.  colmax_ws: scratch of
- * mmb_mm2_colmax_ws_bytes(d) bytes.                                          */
+ * mmb_mm2_colmax_ws_bytes(d) bytes (its last 16 bytes: the batch counter of
+ * mmb_mm2_stream_project's dynamic batch order, zeroed by that call itself;
+ * one launch at a time per workspace).                                      */
 size_t mmb_mm2_colmax_ws_bytes(int d);
 
 /* Padded width (row stride) of the per-utterance sums: roundup(2(d+a+vd), 32). */

@@ -1179,9 +1179,10 @@ constexpr int kFTiles = 5;              // 16-column tiles per projector (ldw = 
 constexpr int kFLdw = 320;
 constexpr int kFThreads = 512;
 // ring [SL slots] | irs [SL] | counters [8] | cnt, tw [2][48] each | tot [2][48] | ssq [2][4][48]
+// | the dynamic schedule's batch and tag slots [8] each
 __host__ __device__ constexpr size_t fused_lds_bytes(int sl) {
   return static_cast<size_t>(sl) * kGSlot * sizeof(_Float16) + sl * 4 + 8 * 4 + 2 * 2 * kGR * 4 +
-         2 * kGR * 4 + 2 * 4 * kGR * 4;
+         2 * kGR * 4 + 2 * 4 * kGR * 4 + 2 * 8 * 4;
 }
 static_assert(fused_lds_bytes(kGSlots) <= 160 * 1024, "fused ring exceeds LDS");
 static_assert((kGSlot * 2) % 256 == 0 && (kGPlane * 2) % 256 == 0,
@@ -1196,6 +1197,8 @@ struct FusedArgs {
   int64_t nb;              // batches = ceil(N / 48)
   int kq[3];               // padded piece widths (multiples of 32)
   int balanced;            // rows past the last full round split evenly over the workgroups
+  unsigned* sched;         // the launch's batch counter, zero at launch (nullable: static order)
+  int64_t big, nu;         // dynamic order: units [0, big) are 48-row batches, the rest 12 rows
 };
 
 #ifdef MMB_DIAG
@@ -1397,12 +1400,17 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   float* s_tw = s_cnt + 2 * kGR;                        // [2][48]
   float* s_tot = s_tw + 2 * kGR;                        // [2][48]
   float* s_ssq = s_tot + 2 * kGR;                       // [2][4][48]
+  int* s_bat = reinterpret_cast<int*>(s_ssq + 2 * 4 * kGR);  // [8] global batch of local batch j (slot j & 7)
+  int* s_tag = s_bat + 8;                                // [8] j + 1 once slot j & 7 holds batch j
   int* fill = ctr;
   int* consumed = ctr + 4;
   int* pbar = ctr + 5;
   int* abort_flag = ctr + 6;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
-  if (tid < 8) ctr[tid] = 0;
+  if (tid < 8) {
+    ctr[tid] = 0;
+    s_tag[tid] = 0;
+  }
   if (tid == 0) FUSED_PROBE(0);
   __syncthreads();
   const int64_t N = a.N;
@@ -1415,7 +1423,28 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
   // workgroups instead of being whole batches of a few of them (a CU with
   // one batch more than another runs ~0.28 ms longer).
   const int64_t full = N / (static_cast<int64_t>(kGR) * G);  // full rounds
+  // Dynamic schedule (r05; the pipelined streamer with a counter): local
+  // batch j is whatever global batch the streamers' wave 0 drew from the
+  // launch's counter for it (one batch ahead of its own use), so a CU that
+  // streams faster takes more batches.  The static round robin left the
+  // workgroups' finishing times 0.3-0.7 ms apart at 1M rows (the even XCDs
+  // slower; tools/fused_balance.py, gpurun_out r05ab).  Neighbouring CUs
+  // still draw neighbouring batches.
+  const bool dyn = PIPE == 2 && f.sched != nullptr;
   auto batch = [&](int64_t j, int64_t& row0, int64_t& rend) -> bool {
+    if (dyn) {
+      int64_t u = blockIdx.x + j * G;  // local batches 0 and 1: the round robin's units
+      if (j >= 2) {
+        if (!fused_wait(&s_tag[j & 7], static_cast<int>(j) + 1, abort_flag, a.flag)) return false;
+        u = s_bat[j & 7];
+      }
+      if (u >= f.nu) return false;
+      // the last round's worth of rows in quarter batches: the end of the
+      // kernel waits for one 12-row unit, not one 48-row batch (~0.3 ms)
+      row0 = u < f.big ? u * kGR : f.big * kGR + (u - f.big) * (kGR / 4);
+      rend = min<int64_t>(N, row0 + (u < f.big ? kGR : kGR / 4));
+      return true;
+    }
     if (f.balanced && j >= full) {
       if (j > full) return false;
       const int64_t t0 = full * kGR * G, tail = N - t0, b = blockIdx.x;
@@ -1870,23 +1899,65 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
           pre = false;
         }
       };
+      // Local batches 0 and 1 are the round robin's units (every workgroup
+      // drawing at once at the start queued 512 atomics on one word); from 2
+      // on, streamer wave 0 draws local batch j + 2's unit at the top of batch
+      // j and publishes it after the batch's text piece, so the atomic's
+      // return is not waited for where it is issued; the other waves need it
+      // at the top of batch j + 1, the projectors later still
+      unsigned drawn = 0;
+      auto draw_issue = [&]() {
+        if (dyn && uw == 0 && lane == 0)
+          drawn = __hip_atomic_fetch_add(f.sched, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      };
+      auto draw_commit = [&](int64_t j) {  // publishes local batch j + 2
+        if (dyn && uw == 0 && lane == 0) {
+          const unsigned b = 2u * G + drawn;
+          s_bat[(j + 2) & 7] = static_cast<int>(b < 0x7fffffffu ? b : 0x7fffffffu);
+          __hip_atomic_store(&s_tag[(j + 2) & 7], static_cast<int>(j) + 3, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      };
       auto rows_of = [&](int64_t jb, int64_t& i0) -> int {
         int64_t row0, rend;
         if (!batch(jb, row0, rend)) {
           i0 = 0;
-          return 0;
+          return dyn ? -1 : 0;  // (dynamic: -1 = no batch, 0 = a batch without this wave's rows)
         }
         i0 = row0 + uw;
         return i0 < rend ? static_cast<int>(min<int64_t>(kGR / 4, (rend - i0 + 3) / 4)) : 0;
       };
+      // dynamic order: every wave counts kGR / 4 fill increments per piece,
+      // its rows' and the rest as padding after them, so the projectors'
+      // targets stay kGR per piece whatever the unit's rows (a 12-row unit
+      // followed by more units would otherwise leave the next targets short)
+      auto pad = [&](int64_t j, int m, int nrows) {
+        if (dyn && nrows < kGR / 4 && lane == 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(&fill[(3 * static_cast<int>(j) + m) & 3], kGR / 4 - nrows, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      };
       if constexpr (PIPE == 2) {
         int64_t i0, ni0;
         int nrows = rows_of(0, i0);
-        for (int64_t j = 0; nrows > 0; ++j) {
+        for (int64_t j = 0; nrows > 0 || (dyn && nrows == 0); ++j) {
+          draw_issue();
           const int nnr = rows_of(j + 1, ni0);
-          piece2(std::integral_constant<int, 0>{}, j, i0, nrows, ni0, nnr);
-          piece2(std::integral_constant<int, 1>{}, j, i0, nrows, ni0, nnr);
-          piece2(std::integral_constant<int, 2>{}, j, i0, nrows, ni0, nnr);
+          if (nrows > 0) {
+            const int nn = nnr > 0 ? nnr : 0;
+            piece2(std::integral_constant<int, 0>{}, j, i0, nrows, ni0, nn);
+            draw_commit(j);
+            pad(j, 0, nrows);
+            piece2(std::integral_constant<int, 1>{}, j, i0, nrows, ni0, nn);
+            pad(j, 1, nrows);
+            piece2(std::integral_constant<int, 2>{}, j, i0, nrows, ni0, nn);
+            pad(j, 2, nrows);
+          } else {  // a unit without rows for this wave (its last < 4 rows)
+            pre = false;
+            draw_commit(j);
+            for (int m = 0; m < 3; ++m) pad(j, m, 0);
+          }
           i0 = ni0;
           nrows = nnr;
         }
@@ -1952,7 +2023,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll 1
     for (int m = 0; m < 3; ++m) {
       const int p = 3 * static_cast<int>(j) + m;
-      fused_wait(&fill[p & 3], kGR * (p >> 2) + nvalid, abort_flag, a.flag);
+      fused_wait(&fill[p & 3], kGR * (p >> 2) + (dyn ? kGR : nvalid), abort_flag, a.flag);
       if constexpr ((DIAG & 1) != 0) {
         fused_signal(consumed);
         continue;
@@ -2149,9 +2220,13 @@ static bool fused_pipe_ok(const FusedArgs& f, int un) {
   return (f.s.L + un - 1) / un >= 3 && (f.s.ids == nullptr || f.s.V * f.s.D * 4 < (int64_t{1} << 31));
 }
 
+static int fused_grid(int64_t nb, hipStream_t stream) {
+  return static_cast<int>(std::min<int64_t>(nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
+}
+
 #ifndef MMB_DIAG
 static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
-  const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
+  const int grid = fused_grid(f.nb, stream);
   if (parts) *parts = grid * 4;
   if (fused_pipe_ok(f, 8)) {
     launch_fused_v<0, 8, 2>(f, grid, stream);
@@ -2183,7 +2258,7 @@ static int fused_slots() {  // ring slots: 62 (default) or 60 (in-process A/B)
 }
 
 static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
-  const int grid = static_cast<int>(std::min<int64_t>(f.nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
+  const int grid = fused_grid(f.nb, stream);
   if (parts) *parts = grid * 4;
   const int dg = fused_diag(), un = fused_unr();
   const bool pipe = fused_pipe() != 0 && fused_pipe_ok(f, un);
@@ -2412,8 +2487,10 @@ __global__ __launch_bounds__(256) void split_rows_kernel(float* __restrict__ s,
   }
 }
 
+// the column-bound partials [kCmaxRows][d], then (mmb_mm2_stream_project)
+// the fused kernel's batch counter (16 bytes)
 extern "C" size_t mmb_mm2_colmax_ws_bytes(int d) {
-  return static_cast<size_t>(kCmaxRows) * (d > 0 ? d : 0) * sizeof(float);
+  return static_cast<size_t>(kCmaxRows) * (d > 0 ? d : 0) * sizeof(float) + 16;
 }
 
 extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
@@ -2542,12 +2619,35 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   f.out = mmb2_out;
   f.nb = ceil_div(n, kGR);
   f.balanced = 1;  // balanced tail: 22.35 -> 22.26 ms (r02s)
+  // the dynamic batch schedule's counter, past the column-bound partials
+  // (zeroed here by a kernel: no memset node in a captured step)
+  f.sched = colmax ? reinterpret_cast<unsigned*>(static_cast<char*>(colmax_ws) +
+                                                 static_cast<size_t>(kCmaxRows) * d * sizeof(float))
+                   : nullptr;
 #ifdef MMB_DIAG
-  {  // in-process A/B switch
+  {  // in-process A/B switches
     const char* e = getenv("MMB_FUSED_BALANCED");
     f.balanced = e ? atoi(e) : 1;
+    const char* dn = getenv("MMB_FUSED_DYN");
+    if (dn && atoi(dn) == 0) f.sched = nullptr;
   }
 #endif
+  {
+    // the dynamic order from 16 rounds of batches on (fewer: the static round
+    // robin, whose finishing times spread little there); its units: 48-row
+    // batches, then the last ~G batches' rows as 12-row units.  Same-process
+    // A/B (tools/fused_dyn_ab.py, r05af/ag, fused kernel ms static ->
+    // dynamic): 1M 22.63 -> 22.38, 500k 11.41 -> 11.28, 250k 5.98 -> 5.96;
+    // 125k (10 rounds) 2.98 -> 3.06, so it stays static
+    const int64_t G = fused_grid(f.nb, stream);
+    if (f.nb < 16 * G) f.sched = nullptr;
+    if (f.sched) {
+      f.big = std::max<int64_t>(0, n - kGR * G) / kGR;
+      f.nu = f.big + ceil_div(n - f.big * kGR, kGR / 4);
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(f.sched, 1, stream));
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+  }
   int parts = 0;
   const int rc = launch_fused(f, stream, &parts);
   if (rc != MMB_OK || !colmax) return rc;

@@ -114,7 +114,7 @@ def fused_outputs(inp, proj, n, t, a, vd, dense=False):
     d = 300
     flag = torch.zeros(1, dtype=torch.int32, device=inp["audio"].device)
     colmax = torch.empty(d, dtype=torch.int32, device=flag.device)
-    ws = torch.empty((8192, d), dtype=torch.float32, device=flag.device)
+    ws = torch.empty(L.query("mmb_mm2_colmax_ws_bytes", d), dtype=torch.uint8, device=flag.device)
     kw = dict(ids32=inp["ids"], table=inp["table"], wtab32=inp["wtab"])
     if dense:
         ids = inp["ids"].long()
