@@ -157,6 +157,29 @@ def check_fused_streamer(dev):
     print(f"fused streamer: {len(FUSED_CASES)} shapes x 5 streamer / tail variants bit-identical")
 
 
+def check_fused_order(dev):
+    """The fused kernel's dynamic batch order (from 16 rounds of batches on:
+    streamers draw 48-row batches from a per-launch counter, the last round
+    in 12-row units) against the static round robin (MMB_FUSED_DYN=0): x,
+    aux, MMB2 rows, column bounds and the flag bit-identical -- N = 200,018
+    rows (4,168 batches >= 16 x 256) leaves a last unit of 2 rows, so two
+    streamer waves see a unit without rows of their own and only pad its
+    fill counts; the same launch twice (the counter re-zeroed per launch)."""
+    names = ["x", "aux", "mmb2", "colmax", "flag"]
+    N, T, A, Vd = 200_018, 24, 64, 64
+    assert (N + 47) // 48 >= 16 * min(256, L.cu_count(dev)), "too few rows for the dynamic order"
+    inp, proj = fused_case(dev, N, T, A, Vd, False)
+    with knobs(MMB_FUSED_DYN=0):
+        ref = fused_outputs(inp, proj, N, T, A, Vd)
+    for rep in range(2):
+        with knobs(MMB_FUSED_DYN=1):
+            got = fused_outputs(inp, proj, N, T, A, Vd)
+        for nm, r, g in zip(names, ref, got):
+            assert torch.equal(torch.nan_to_num(r, nan=7.0), torch.nan_to_num(g, nan=7.0)), (nm, rep)
+    assert int(ref[4].item()) == 0
+    print("fused order: dynamic batch order bit-identical to the round robin (2 launches)")
+
+
 def check_remove_rows(dev):
     """pc_remove1_kernel (one PC, R = 2 / 4 / 8 rows per wave in flight, the
     PC in registers) against pc_remove_kernel (MMB_PC_REMOVE_R=0):
@@ -256,6 +279,7 @@ def check_timeouts(dev):
 
 
 GROUPS = {"projection": check_projection, "fused_streamer": check_fused_streamer,
+          "fused_order": check_fused_order,
           "remove_rows": check_remove_rows, "gram": check_gram_schedules,
           "timeouts": check_timeouts}
 
