@@ -32,13 +32,30 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, nargs="+", default=[7])
     ap.add_argument("--ablations", action="store_true")
+    ap.add_argument("--step-g", type=int, default=0,
+                    help="solve the Gram (and Omega) of a bench-shaped FusedStep of this many rows "
+                         "instead of the synthetic 4096 x 300 one")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(1)
     n, d, k = 4096, 300, 11
-    x = 0.4 * torch.randn(n, d, generator=g, dtype=torch.float64) + 0.3 * torch.randn(d, generator=g, dtype=torch.float64)
-    G = (x.T @ x).to(dev)
-    z0 = torch.randn(d, k, generator=g, dtype=torch.float64).to(dev)
+    if args.step_g:
+        import models
+        import synth
+        inp = synth.device_shard(0, args.step_g, 40, 400_000, seed=1000, device=dev)
+        torch.manual_seed(0)
+        gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(dev)
+        st = P.FusedStep(inp, gen.networks())
+        st.run(check=True)
+        G = st.G.clone()
+        z0 = P.omega(d, k, dev).clone()
+        ev = torch.linalg.eigvalsh(G.cpu())
+        print(json.dumps({"step_rows": args.step_g, "eig_top12": [float(v) for v in ev.flip(0)[:12]]}), flush=True)
+        del st, inp
+    else:
+        x = 0.4 * torch.randn(n, d, generator=g, dtype=torch.float64) + 0.3 * torch.randn(d, generator=g, dtype=torch.float64)
+        G = (x.T @ x).to(dev)
+        z0 = torch.randn(d, k, generator=g, dtype=torch.float64).to(dev)
     flag = torch.zeros(1, dtype=torch.int32, device=dev)
     pc = torch.empty((1, d), dtype=torch.float64, device=dev)
     out = {}
