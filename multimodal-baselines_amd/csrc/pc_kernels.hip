@@ -2079,22 +2079,32 @@ __device__ __forceinline__ void p16_rmul(const double* In, const double* M, doub
 // (lane i = row i); *fail as p16_chol.  Mt (optional) receives M^T, the
 // layout whose MFMA B-operand reads are conflict-free (M's own reads
 // M[j][m] for lanes j = 0..15 fall 16 doubles apart: 8-way LDS conflicts).
+// EQ = false (r05, pc_solve_mc_kernel): no equilibration -- M = L^-1 of W
+// itself.  Cholesky's backward error is invariant to diagonal scaling (the
+// factor of D W D is D times W's, to rounding), so scaling W first changes
+// neither which blocks factor nor the span Z keeps; it only put ~1 us of
+// broadcasts and scalings on the round's critical path.  d is then not
+// written (the MGS^2 fallback forms its scales from W).
+template <bool EQ = true>
 __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* Li, double* M,
                                             double* d, int k, int lane, int* fail, double* Mt = nullptr) {
   double w[kMaxK], x[kMaxK];
   PC_WMARK(30);
 #pragma unroll
   for (int m = 0; m < kMaxK; ++m) w[m] = (lane < k && m < k) ? W[lane * k + m] : 0.0;
-  const double di = rsqrt_f64(lane < k ? W[lane * k + lane] : 1.0);
+  double di = 1.0;
+  if constexpr (EQ) {
+    di = rsqrt_f64(lane < k ? W[lane * k + lane] : 1.0);
 #pragma unroll
-  for (int m = 0; m < kMaxK; ++m) w[m] *= di * readlane_f64(di, m);
-  if (lane < kMaxK) d[lane] = lane < k ? di : 0.0;
+    for (int m = 0; m < kMaxK; ++m) w[m] *= di * readlane_f64(di, m);
+    if (lane < kMaxK) d[lane] = lane < k ? di : 0.0;
+  }
   if (lane == 0) *fail = 0;
   p16_chol_regs(w, L, Li, k, lane, fail, x, 37);  // probe marks 37-39
   if (lane < kP16W) {  // lane c: column c of L^-1 diag(d)
 #pragma unroll
     for (int i = 0; i < kP16W; ++i) {
-      const double v = (lane < k && i < k) ? x[i] * di : 0.0;
+      const double v = (lane < k && i < k) ? (EQ ? x[i] * di : x[i]) : 0.0;
       M[i * kP16W + lane] = v;
       if (Mt) Mt[lane * kP16W + i] = v;
     }
@@ -2587,7 +2597,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       lane = tid & (kWave - 1);
     }
     if (wave == kPnPw) {
-      if (!(ABL & 2)) p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);  // M_r, beside the exchange
+      if (!(ABL & 2)) p16_eq_chol<false>(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);  // M_r, beside the exchange
     } else {
       tile_partials(sY);
       bar_pw();
@@ -2610,7 +2620,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       // then a second exchange of G_t Z
       for (int e = tid; e < Dp * kP16W; e += kPnNT) {
         const int p = e / kP16W, j = e % kP16W;
-        sZ[e] = (p < D && j < k) ? sY[e] * sd[j] : 0.0;
+        sZ[e] = (p < D && j < k) ? sY[e] * rsqrt_f64(sW[j * k + j]) : 0.0;  // the equilibrated rows
       }
       __syncthreads();
       mgs(sZ);
@@ -2670,7 +2680,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   // pivot (MGS^2) or the transposed branch (an orthonormal Q: CholeskyQR2)
   // forms explicit rows
   if (wave == kPnPw) {
-    p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);
+    p16_eq_chol<false>(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);
   } else {
     tile_partials(sY);
   }
@@ -2681,7 +2691,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
     if (s_fail) {  // the equilibrated rows, orthonormalised by MGS^2
       for (int e = tid; e < Dp * kP16W; e += kPnNT) {
         const int p = e / kP16W, j = e % kP16W;
-        sZ[e] = (p < D && j < k) ? sY[e] * sd[j] : 0.0;
+        sZ[e] = (p < D && j < k) ? sY[e] * rsqrt_f64(sW[j * k + j]) : 0.0;  // the equilibrated rows
       }
       __syncthreads();
       mgs(sZ);

@@ -66,7 +66,9 @@ def main(src, tag, workloads):
                       f"algorithmic per launch ({stream / alg:.3f}x)" if stream else "no stream kernel",
                   f"every libmmb kernel of the step: {step_total / 1e9:.3f} GB"
                   + (f" vs the path's {path / 1e9:.3f} GB ({step_total / path:.3f}x)" if path else ""), ""]
-        tj = {"tag": tag, "workload": wl, "utts_per_launch": U, "tokens": cfg["tokens"],
+        sha_f = os.path.join(src, "tree_sha.txt")  # tools/gpu_r05_final.sh: "tree: <sha>"
+        sha = open(sha_f).read().split()[-1] if os.path.exists(sha_f) else None
+        tj = {"tag": tag, "tree_sha": sha, "workload": wl, "utts_per_launch": U, "tokens": cfg["tokens"],
               "mm2_stream_hbm_bytes_per_launch": stream, "phase": phase,
               "algorithmic_bytes_per_launch": alg, "step_hbm_bytes": step_total,
               "path_bytes_per_step": path, "per_kernel_hbm_bytes_per_launch": traffic}
