@@ -2005,8 +2005,10 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
 // the caller first hands ws over; workgroup 0 returns the counter to zero
 // once every workgroup has made its last arrival, so a launch -- eager or a
 // graph replay -- leaves ws ready for the next one).
+#ifdef MMB_DIAG  // the r04 kernel's (pc_solve_mc_v1_kernel) wave split
 constexpr int kPmPw = 15;  // waves holding G (wave 15 runs the Cholesky meanwhile)
 constexpr int kPmKs = 6;   // k-steps of G per wave: ceil(kP16MaxD / 4 / kPmPw)
+#endif
 constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
 
 #ifdef MMB_DIAG
