@@ -183,15 +183,19 @@ def _perturb(inp, i):
     inp["table"][: inp["table"].shape[0] // 2].mul_(f)
 
 
-@pytest.mark.parametrize("mosi", [True, False], ids=["narrow_fused", "stream_project"])
-def test_graph_replay_int8_gram_on_changing_inputs(gpu, mosi):
+@pytest.mark.parametrize("mosi,n", [(True, 1 << 15), (False, 40_000), (False, 200_018)],
+                         ids=["narrow_fused", "stream_project", "stream_project_dynamic_order"])
+def test_graph_replay_int8_gram_on_changing_inputs(gpu, mosi, n):
     """>= 32,768 rows (GRAM_I8_MIN_ROWS): the captured step runs the stream
     kernel's column-bound partials, their reduction and the int8 Gram.  Each
     replay follows new inputs (rescaled frames and table rows, re-ordered ids)
     and equals an eager step on the same inputs bit for bit: SIF rows, MMB2
     rows, PC, column bounds -- a stale bound, hand-over word or text cache
-    would show."""
-    n = 1 << 15 if mosi else 40_000
+    would show.  At 200,018 rows (>= 16 rounds of 48-row batches) the fused
+    kernel runs in its dynamic batch order: the batch counter is re-zeroed by a
+    kernel node on every replay."""
+    if n > 100_000:
+        assert (n + 47) // 48 >= 16 * min(256, L.cu_count(gpu))
     inp, gen = _bench_like_step(gpu, n, mosi=mosi, seed=93)
     st = P.FusedStep(inp, gen.networks())
     assert st.gram_i8 and (st.narrow_fused if mosi else st.stream_project)
