@@ -924,15 +924,15 @@ __global__ __launch_bounds__(256) void gram_tri_reduce_kernel(const double* __re
   const int64_t e = static_cast<int64_t>(blockIdx.x) * kRedEl + el;
   double s = 0.0;
   if (e < total) {
-    if (R >= 8) {  // R is a multiple of 8 here (gram2_plan / gram_i8_plan)
+    if (R >= 8) {  // thread group u sums ranges u, u + 8, .. (< R)
       double v[kRedMaxPer];
-      const int per = R / 8;
+      const int per = (R + 7) / 8;
 #pragma unroll
       for (int j = 0; j < kRedMaxPer; ++j)
-        v[j] = j < per ? part[static_cast<int64_t>(u + 8 * j) * total + e] : 0.0;
+        v[j] = (j < per && u + 8 * j < R) ? part[static_cast<int64_t>(u + 8 * j) * total + e] : 0.0;
 #pragma unroll
       for (int j = 0; j < kRedMaxPer; ++j)
-        if (j < per) s += v[j];
+        if (j < per && u + 8 * j < R) s += v[j];
     } else if (u == 0) {
       for (int r = 0; r < R; ++r) s += part[static_cast<int64_t>(r) * total + e];
     }
@@ -957,9 +957,9 @@ __global__ __launch_bounds__(256) void gram_tri_reduce_kernel(const double* __re
 
 static int launch_tri_reduce(const double* part, int d, int nt, int R, int accumulate, double* g,
                              hipStream_t stream) {
-  // the kernel sums ranges u + 8 j (j < R / 8, at most kRedMaxPer per thread)
-  // for R >= 8: a plan outside that would silently drop ranges
-  MMB_REQUIRE(R >= 1 && (R < 8 || (R % 8 == 0 && R <= 8 * kRedMaxPer)));
+  // the kernel sums ranges u + 8 j < R (at most kRedMaxPer per thread) for
+  // R >= 8: a plan outside that would silently drop ranges
+  MMB_REQUIRE(R >= 1 && R <= 8 * kRedMaxPer);
   const int64_t total = static_cast<int64_t>(nt) * (nt + 1) / 2 * 256;
   gram_tri_reduce_kernel<<<static_cast<int>(ceil_div(total, kRedEl)), 256, 0, stream>>>(
       part, d, nt, R, accumulate, g);
@@ -3229,6 +3229,10 @@ static GramLPlan gram_i8l_plan(int64_t n, int d) {
   q.T = q.nt * (q.nt + 1) / 2;
   q.P = S::kP;
   q.R = gram_i8l_ranges(n, S::kP);
+#ifdef MMB_DIAG
+  if (const char* e = getenv("MMB_GRAM_RANGES"); e && atoi(e) > 0)  // A/B: ranges (<= 128)
+    q.R = std::max<int>(q.R, std::min(atoi(e), 128));
+#endif
   q.xcd = (q.R % 8 == 0) ? 1 : 0;
   q.chunk = ceil_div(ceil_div(std::max<int64_t>(n, 1), q.R), kGiRows) * kGiRows;
   static GlParts cache[kGiF / 16 + 1];

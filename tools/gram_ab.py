@@ -12,7 +12,9 @@ runs, spilling; 3: the product with LDS reads free to cross tiles; 4: with
 the next tile's first B digit prefetched; 5: unstaggered) and
 the product shape's
 timing-only ablations (MMB_GRAM_DIAG 1 no MFMAs, 4 no slicing, 12 no slicing
-and no x loads, 13 only barriers / LDS / epilogue), alternated over rounds;
+and no x loads, 13 only barriers / LDS / epilogue), and 84 / 85 row ranges
+(252 / 255 workgroups, the parts of a range then on different XCDs;
+MMB_GRAM_RANGES) instead of 80, alternated over rounds;
 HIP events around `reps` back-to-back calls (kernel + range reduction).
 Also each variant's max |G - G_f64| / max |G_f64| against the exact f64 Gram.
 """
@@ -44,11 +46,14 @@ VARIANTS = {
     "abl_no_slice": {"MMB_GRAM_DIAG": "4"},
     "abl_no_slice_no_load": {"MMB_GRAM_DIAG": "12"},
     "abl_skeleton": {"MMB_GRAM_DIAG": "13"},
+    "ranges84": {"MMB_GRAM_RANGES": "84"},
+    "ranges85": {"MMB_GRAM_RANGES": "85"},
 }
 
 
 def with_env(kv, fn):
-    old = {k: os.environ.get(k) for k in ("MMB_GRAM_I8_V1", "MMB_GRAM_I8_SHAPE", "MMB_GRAM_DIAG")}
+    old = {k: os.environ.get(k) for k in ("MMB_GRAM_I8_V1", "MMB_GRAM_I8_SHAPE", "MMB_GRAM_DIAG",
+                                          "MMB_GRAM_RANGES")}
     for k in old:
         os.environ.pop(k, None)
     os.environ.update(kv)
