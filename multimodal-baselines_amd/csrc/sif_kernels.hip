@@ -2744,7 +2744,7 @@ constexpr size_t kNFLdsRows = sizeof(float) * (kNFHot * kNFHotRow + kNFRows * kN
 static_assert(kNFLdsRows % 16 == 0, "the frame-slot scratch is float4-aligned");
 // + 1 KB per wave for the frame-slot sums (12 waves: the utterance's own T
 // row, free until T is written, holds them instead)
-constexpr size_t kNFLds = kNFLdsRows + (kNFWaves == 8 ? 16 * kWave * kNFWaves : 0);
+constexpr size_t kNFLds = kNFLdsRows + (kNFWaves == 8 ? 16 * kWave * kNFWaves : 0) + 16;  // + team counters
 
 struct NarrowFusedArgs {
   StreamArgs s;        // ids, table, V, wtab, audio, visual, N, L, D, A, Vd, num_out, aux_out, flag, cmax_part
@@ -2759,12 +2759,18 @@ struct NarrowFusedArgs {
   int cb_av;                 // first audio chunk of the image (kq(D) / 32)
   int kq_a, kq_v;            // K rows of the audio / visual pieces (multiples of 32)
   int rpw;                   // utterances per wave and batch (4; 1 or 2 for small N)
-  int64_t nb;                // batches of 8 rpw rows
+  int64_t nb;                // batches of 8 rpw rows (teams: of 4 rpw rows)
+  int team_lag;              // teams: team 1 starts after team 0's first stream phase
 };
 
-template <int UNR, int HU, int GA_MAX, int GV_MAX>
+// TM (teams): the workgroup's two halves (waves 0-3 and 4-7, one wave of
+// each per SIMD) run batches of 4 rpw rows on their own LDS halves with
+// their own (LDS counter) barriers, so that one team's batch GEMM and
+// epilogue can run beside the other team's stream phase.
+template <int UNR, int HU, int GA_MAX, int GV_MAX, bool TM = false>
 __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFWaves / 4, kNFWaves / 4))) void utt_narrow_fused_kernel(
     NarrowFusedArgs f) {
+  static_assert(!TM || kNFWaves == 8, "teams of 4 waves: 8-wave workgroups");
   extern __shared__ __attribute__((aligned(16))) float nf_lds[];
   float* hotEP = nf_lds;                                  // [kNFHot][kNFHotRow]: E | P
   float* sT = hotEP + kNFHot * kNFHotRow;                 // [rows][kNFLdp]
@@ -2773,6 +2779,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   float* s_cnt = s_irs + kNFRows;                         // [rows]
   float* s_ok = s_cnt + kNFRows;                          // [rows] 1 = a row of this batch
   float4* s_scr = reinterpret_cast<float4*>(s_ok + kNFRows);  // [waves][64] frame-slot sums
+  unsigned* s_team = reinterpret_cast<unsigned*>(s_scr + (kNFWaves == 8 ? kWave * kNFWaves : 0));  // [2]
 
   const StreamArgs& a = f.s;
   // (holding these pointers in VGPRs instead -- fewer SGPR spills -- measured
@@ -2787,6 +2794,11 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int64_t wid = static_cast<int64_t>(blockIdx.x) * kNFWaves + wave;
+  constexpr int kTW = TM ? 4 : kNFWaves;       // waves of a team (the workgroup: one team)
+  constexpr int kTRT = TM ? 1 : kNFRT;         // MFMA row tiles of a team's batch
+  const int team = TM ? wave >> 2 : 0;
+  const int wt = TM ? wave & 3 : wave;          // wave in its team
+  const int r0 = TM ? 16 * team : 0;            // the team's first LDS row
   const int L = a.L, D = a.D;
   const int UT = D >> 2, UA = a.A >> 2, UV = a.Vd >> 2;
   const int PA = kWave / UA, PV = kWave / UV;
@@ -2827,13 +2839,31 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   for (int c = 0; c < CT; ++c) cmx[c] = z4;
 
   // utterance u of this wave in batch j: row 8 rpw (blockIdx.x + gridDim.x j) + rpw wave + u
+  // (teams: 4 rpw (tg + ntg j) + rpw wt + u, team tg = 2 blockIdx.x + team of ntg)
   const int rpw = f.rpw;
-  const int nbr = kNFWaves * rpw;  // rows of a batch
+  const int nbr = kTW * rpw;  // rows of a batch
   const int nrt = (nbr + 15) / 16;  // MFMA row tiles holding them
   // 32-bit rows and batches (N < 2^31: the launcher checks), 64-bit offsets
   const int N = static_cast<int>(a.N), nb = static_cast<int>(f.nb);
-  auto row_of = [&](int j, int u) -> int {
-    return nbr * (static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) * j) + rpw * wave + u;
+  const int tg = TM ? 2 * static_cast<int>(blockIdx.x) + team : static_cast<int>(blockIdx.x);
+  const int ntg = TM ? 2 * static_cast<int>(gridDim.x) : static_cast<int>(gridDim.x);
+  auto row_of = [&](int j, int u) -> int { return nbr * (tg + ntg * j) + rpw * wt + u; };
+  // the batch barrier: the workgroup's, or the team's 4 waves' (an LDS
+  // arrival counter; every wave of a team runs the same batches)
+  unsigned bar_target = 0;
+  auto bar_batch = [&]() {
+    if constexpr (!TM) {
+      __syncthreads();
+    } else {
+      bar_target += kTW;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) {
+        __hip_atomic_fetch_add(&s_team[team], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(&s_team[team], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < bar_target)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
   };
   auto ld_id = [&](int i) -> int {
     if (NF_ABL & 32) return (i < N && lane < L) ? (lane * 131 + i) % V : -1;
@@ -2863,22 +2893,22 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   // lane (q, g) holds row / column q, K group g of a 16 x 32 fragment
   const int q = lane & 15, g = lane >> 4;
   constexpr int CH = 2 * kNFLdw * 32, PL = kNFLdw * 32;  // image chunk / plane (halves)
-  constexpr int kMaxT = (kNFCT + kNFWaves - 1) / kNFWaves;  // 3 (8 waves) or 2 (12)
+  constexpr int kMaxT = (kNFCT + kTW - 1) / kTW;  // 3 (8 waves), 2 (12) or 5 (teams)
   const int nch = (f.kq_a + f.kq_v) / 32;
   const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(f.img), 0,
                                                        (f.cb_av + nch) * CH * 2, 0x00020000);
   int boff[kMaxT];
 #pragma unroll
   for (int tt = 0; tt < kMaxT; ++tt) {
-    const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+    const int col = 16 * min(wt + kTW * tt, kNFCT - 1) + q;
     boff[tt] = col * 32 + ((g ^ x3_swz(col)) << 3);
   }
-  static_assert(kMaxT == 2 || kMaxT == 3, "column tiles per wave");
-  const int ntt = wave + kNFWaves * (kMaxT - 1) < kNFCT ? kMaxT : kMaxT - 1;  // this wave's column tiles
+  static_assert(kMaxT == 2 || kMaxT == 3 || kMaxT == 5, "column tiles per wave");
+  const int ntt = wt + kTW * (kMaxT - 1) < kNFCT ? kMaxT : kMaxT - 1;  // this wave's column tiles
   float cinv[kMaxT], cc0[kMaxT];  // the tiles' column scales and c0
 #pragma unroll
   for (int tt = 0; tt < kMaxT; ++tt) {
-    const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+    const int col = 16 * min(wt + kTW * tt, kNFCT - 1) + q;
     const bool held = tt < ntt && col < kNFLdp;
     cinv[tt] = held ? f.col_inv[col] : 0.f;
     cc0[tt] = held ? f.c0[col] : 0.f;
@@ -2909,16 +2939,25 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
   // the A rows' pads (K past each piece) stay zero: zeroed once here
   for (int e = tid; e < kNFRows * 2 * kNFK / 8; e += kNFThreads)
     reinterpret_cast<float4*>(sA)[e] = z4;
+  if (TM && tid < 2) s_team[tid] = 0u;
   int rid_n, hs_n, raw = -1;  // the next utterance's ids, weights, hot slots
   float w_n;
   resolve(ld_id(row_of(0, 0)), rid_n, w_n, hs_n);
   __syncthreads();  // hot rows in LDS
+  if (TM && team == 1 && f.team_lag && tg < nb) {
+    // team 1 starts once team 0 (which has a batch if team 1 has) is past its
+    // first stream phase: the teams' phases start out of step
+    if (lane == 0)
+      while (__hip_atomic_load(&s_team[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < static_cast<unsigned>(kTW))
+        __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_wave_barrier();
+  }
   for (int j = 0; j < nb; j += 1) {
-    if (static_cast<int>(blockIdx.x) + static_cast<int>(gridDim.x) * j >= nb) break;
+    if (tg + ntg * j >= nb) break;
     // ------------------------------------------------------------ stream phase
     for (int u = 0; u < rpw; ++u) {
       const int i = row_of(j, u);
-      const int r = rpw * wave + u;  // row in the batch
+      const int r = r0 + rpw * wt + u;  // LDS row
       const bool live = i < N;
       const int rid = rid_n, hs = hs_n;
       const float w = w_n;
@@ -3093,22 +3132,22 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
     // the first image chunk's B fragments load across the barrier
     half8 bh[kMaxT], bl[kMaxT];
     ld_b(0, bh, bl);
-    __syncthreads();
+    bar_batch();
     // ------------------------------------------------------------ MFMA phase
     {
-      f32x4 acc[kNFRT][kMaxT];
+      f32x4 acc[kTRT][kMaxT];
 #pragma unroll
-      for (int rt = 0; rt < kNFRT; ++rt)
+      for (int rt = 0; rt < kTRT; ++rt)
 #pragma unroll
         for (int tt = 0; tt < kMaxT; ++tt) acc[rt][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int c = 0; c < ((NF_ABL & 1) ? 0 : nch); ++c) {
         half8 nh[kMaxT], nl[kMaxT];  // chunk c + 1, in flight during chunk c
         if (c + 1 < nch) ld_b(c + 1, nh, nl);
 #pragma unroll
-        for (int rt = 0; rt < kNFRT; ++rt) {
+        for (int rt = 0; rt < kTRT; ++rt) {
           if (rt < nrt) {
             // (36-row batches: rows past the last are clamped, their results unused)
-            const int rr = kNFRows % 16 == 0 ? 16 * rt + q : min(16 * rt + q, kNFRows - 1);
+            const int rr = r0 + (kNFRows % 16 == 0 ? 16 * rt + q : min(16 * rt + q, kNFRows - 1));
             const int o = (((4 * c + g) ^ q) << 3);
             const half8 ah = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + o);
             const half8 al = *reinterpret_cast<const half8*>(sA + rr * 2 * kNFK + kNFK + o);
@@ -3134,41 +3173,41 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
       // place, each read-modify-write waited for the previous one's store
       // (the compiler cannot tell the rows apart)
       static_assert(kNFCT * 16 <= kNFLdp, "the column tiles lie inside the T rows");
-      float irs[kNFRT][4], tv[kMaxT][kNFRT][4];
+      float irs[kTRT][4], tv[kMaxT][kTRT][4];
 #pragma unroll
-      for (int rt = 0; rt < kNFRT; ++rt)
+      for (int rt = 0; rt < kTRT; ++rt)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) irs[rt][jj] = s_irs[min(16 * rt + 4 * g + jj, kNFRows - 1)];
+        for (int jj = 0; jj < 4; ++jj) irs[rt][jj] = s_irs[r0 + min(16 * rt + 4 * g + jj, kNFRows - 1)];
 #pragma unroll
       for (int tt = 0; tt < kMaxT; ++tt) {
-        const int col = 16 * min(wave + kNFWaves * tt, kNFCT - 1) + q;
+        const int col = 16 * min(wt + kTW * tt, kNFCT - 1) + q;
 #pragma unroll
-        for (int rt = 0; rt < kNFRT; ++rt)
+        for (int rt = 0; rt < kTRT; ++rt)
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
-            tv[tt][rt][jj] = sT[min(16 * rt + 4 * g + jj, kNFRows - 1) * kNFLdp + col];
+            tv[tt][rt][jj] = sT[(r0 + min(16 * rt + 4 * g + jj, kNFRows - 1)) * kNFLdp + col];
       }
 #pragma unroll
       for (int tt = 0; tt < kMaxT; ++tt) {
         if (tt < ntt) {
-          const int col = 16 * (wave + kNFWaves * tt) + q;
+          const int col = 16 * (wt + kTW * tt) + q;
           const float ci = cinv[tt], cc = cc0[tt];
 #pragma unroll
-          for (int rt = 0; rt < kNFRT; ++rt)
+          for (int rt = 0; rt < kTRT; ++rt)
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
               const int rr = 16 * rt + 4 * g + jj;
               if (kNFRows % 16 == 0 ? rt < nrt : rr < nbr)
-                sT[rr * kNFLdp + col] = acc[rt][tt][jj] * (ci * irs[rt][jj]) + tv[tt][rt][jj] + cc;
+                sT[(r0 + rr) * kNFLdp + col] = acc[rt][tt][jj] * (ci * irs[rt][jj]) + tv[tt][rt][jj] + cc;
             }
         }
       }
     }
-    __syncthreads();
+    bar_batch();
     // ------------------------------------------------------------ epilogue
     // wave w finishes rows rpw w .. rpw w + rpw - 1: / total (column D), L2 norm, store
     for (int u = 0; u < rpw; ++u) {
-      const int r = rpw * wave + u;
+      const int r = r0 + rpw * wt + u;
       const int i = row_of(j, u);
       const float* trow = sT + r * kNFLdp;
       const float rt = __builtin_amdgcn_rcpf(trow[D]);  // v_rcp_f32 (1 ulp): the MMB2 bar is 2e-6
@@ -3190,7 +3229,7 @@ __global__ __launch_bounds__(kNFThreads) __attribute__((amdgpu_waves_per_eu(kNFW
         }
       }
     }
-    __syncthreads();  // the T / A rows are rewritten by the next batch
+    bar_batch();  // the T / A rows are rewritten by the next batch
   }
   if (a.cmax_part) {
 #pragma unroll
@@ -3257,17 +3296,35 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   const int64_t cus = stream_cu_count(stream);
   f.rpw = kNFRpw;
   while (f.rpw > 1 && ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw) < cus) --f.rpw;
-  f.nb = ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw);
+  int teams = 0;  // 1: two teams of 4 waves per workgroup, 2: the same, team 1 starting a phase later
+#ifdef MMB_DIAG
+  if (const char* e = getenv("MMB_NF_TEAMS")) teams = atoi(e);
+#endif
+  if (kNFWaves != 8) teams = 0;
+  f.team_lag = teams == 2 ? 1 : 0;
+  // batches: of 8 rpw rows, or of 4 rpw rows per team (two per workgroup)
+  f.nb = ceil_div(n, static_cast<int64_t>(teams ? kNFWaves / 2 : kNFWaves) * f.rpw);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
+#ifdef MMB_DIAG
+    if (kNFWaves == 8)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV, kNFWaves == 8>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
+#endif
     attr = true;
   }
   int64_t grid = stream_cu_count(stream);
   if (colmax && grid > kCmaxRows / kNFWaves) grid = kCmaxRows / kNFWaves;
-  if (grid > f.nb) grid = f.nb;
-  utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
+  if (grid > (teams ? ceil_div(f.nb, int64_t{2}) : f.nb)) grid = teams ? ceil_div(f.nb, int64_t{2}) : f.nb;
+#ifdef MMB_DIAG
+  if (teams) {
+    utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV, kNFWaves == 8><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
+    MMB_LAUNCH_CHECK();
+  } else
+#endif
+    utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
   MMB_LAUNCH_CHECK();
   if (!colmax) return MMB_OK;
   colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(
