@@ -193,20 +193,37 @@ def load_traffic(name, utts_per_launch, tokens, phase="mm2_stream"):
     return None, None
 
 
+# The auxiliary legs (per-rank sizes, the other BASELINE configs) run short
+# steps straight after a model build: the chip needs ~25 ms of load to reach
+# its clocks (r05 traces: the MOSI step 5.98 -> 5.70 -> 5.46 -> 5.23 -> 5.15
+# -> 5.10 -> 5.06 ms over its first steps, the 125k step 3.43 -> 3.11 ms), so
+# their warmup runs at least AUX_WARMUP_S of steps beyond its W.  (The main
+# timed region keeps exactly W: at 1M rows W = 5 steps is 110 ms.)
+AUX_WARMUP_S = 0.1
+
+
 def run_workload(P, inp, gen, steps, warmup, allreduce=None, world=1, rank=0):
-    """FusedStep over `inp`: warmup, then `steps` timed steps bracketed by
-    barrier + synchronize, then the same number of steps again with HIP
-    events around each phase (the per-phase times and the kernels' launch
-    durations; r05: the events are no longer inside the timed region, where
-    their ~12 markers per step added to the stream).  Returns (step,
-    elapsed_s, per-step traces)."""
+    """FusedStep over `inp`: warmup (W steps, and at least AUX_WARMUP_S of
+    them), then `steps` timed steps bracketed by barrier + synchronize, then
+    the same number of steps again with HIP events around each phase (the
+    per-phase times and the kernels' launch durations; r05: the events are no
+    longer inside the timed region, where their ~12 markers per step added to
+    the stream).  Returns (step, elapsed_s, per-step traces)."""
     import torch
     import torch.distributed as dist
 
     U = inp["ids"].shape[0]
     step = P.FusedStep(inp, gen.networks(), allreduce=allreduce, n_total=U * world, row0=rank * U)
-    for _ in range(warmup):
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    done = 0
+    # (time-based only on one rank: every rank must run the same number of
+    # all-reduces)
+    while done < warmup or (world == 1 and time.perf_counter() - w0 < AUX_WARMUP_S and done < 1000):
         step.run()
+        done += 1
+        if done >= warmup:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1234,6 +1251,7 @@ def main():
         prs[str(U)] = {"utts": U, "ms_per_step": round(ms_per_step, 4), "value": round(value, 1),
                        "phase_ms": out["phase_ms"]}
         out["per_rank_steps"] = prs
+        out["aux_warmup_min_s"] = AUX_WARMUP_S  # per_rank_steps / configs_measured warmup floor
         proj = {}
         for n_r in (2, 4, 8):
             key = str(U // n_r)
