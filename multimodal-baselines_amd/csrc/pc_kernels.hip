@@ -880,6 +880,212 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
   }
 }
 
+// ------------------------------------------------------------------ Gram i8, x staged in LDS (r05, tools build)
+// gram_i8l_kernel's digits, parts, tiles and level sums, but x reaches LDS by
+// buffer_load ... lds (16 bytes a lane, no VGPR destination) two chunks ahead
+// into two stages, the digit buffer is indexed by the part's own features (two
+// of the three groups: <= kGsF at d <= 304), and each chunk is sliced by every
+// wave from its stage, then multiplied (one digit buffer: 53 KB digits + 2 x
+// 53 KB stages).  The x prefetch registers of gram_i8l_kernel (32 per thread)
+// are gone; the loads stay in flight across the raw barriers (counted vmcnt).
+constexpr int kGsF = 208;                          // a part's features at most
+constexpr int kGsBuf = kGiDig * kGsF * kGiRows;    // one chunk's digits (bytes)
+constexpr int kGsStage = kGiRows * kGsF * 4;       // one chunk's x (bytes)
+constexpr size_t kGsLds = kGsBuf + 2 * static_cast<size_t>(kGsStage);
+
+template <int DIAG, class S>
+__global__ __launch_bounds__(S::kNT) void gram_i8s_kernel(const float* __restrict__ x,
+                                                         const unsigned* __restrict__ colmax,
+                                                         int64_t N, int D, int nt, int64_t chunk,
+                                                         int xcd_map, GlParts parts,
+                                                         double* __restrict__ part) {
+  constexpr int MT = S::kMT, NT = S::kNT, kIt = S::kIt, NW = S::kNW;
+  // ALL of the kernel's LDS in this one array (a second __shared__ object can
+  // make the compiler wait vmcnt(0) before LDS reads: cdna_hip_programming.md)
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_gs[];
+  unsigned char* const dig = s_gs;
+  float* const stage0 = reinterpret_cast<float*>(s_gs + kGsBuf);
+  float* const stage1 = reinterpret_cast<float*>(s_gs + kGsBuf + kGsStage);
+  int range, p;
+  if (xcd_map) {
+    const int b = blockIdx.x, sx = b >> 3;
+    range = (b & 7) + 8 * (sx / S::kP);
+    p = sx % S::kP;
+  } else {
+    range = blockIdx.x / S::kP;
+    p = blockIdx.x % S::kP;
+  }
+  const GlPart& pt = parts.p[p];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int npt = pt.n;
+  if (npt <= 0) return;
+  const int f0 = pt.f0, n0 = pt.n0, f1 = pt.f1;
+  const int nf = n0 + pt.n1;  // <= kGsF, a multiple of 4 (the launcher checks)
+  auto loc = [&](int f) { return f < f0 + n0 ? f - f0 : n0 + f - f1; };
+  const int per = (npt + NW - 1) / NW;
+  const int q0 = wave * per;
+  int ti[MT], tj[MT], la[MT], lb[MT];
+  int ntl = 0;
+#pragma unroll
+  for (int q = 0; q < MT; ++q) {
+    ti[q] = tj[q] = 0;
+    if (q < per && q0 + q < npt) {
+      const int t = pt.tile[q0 + q];
+      ti[q] = t & 255;
+      tj[q] = t >> 8;
+      ntl = q + 1;
+    }
+    la[q] = loc(16 * ti[q]);
+    lb[q] = loc(16 * tj[q]);
+  }
+  i32x4 lev[MT][kGlLev];
+#pragma unroll
+  for (int q = 0; q < MT; ++q)
+#pragma unroll
+    for (int l = 0; l < kGlLev; ++l) lev[q][l] = i32x4{0, 0, 0, 0};
+
+  const int64_t r0 = range * chunk;
+  const int64_t r1 = min(N, r0 + chunk);
+  const int nrows = static_cast<int>(r1 > r0 ? r1 - r0 : 0);
+  const int nchunks = (nrows + kGiRows - 1) / kGiRows;
+  // items it = tid + NT u: local feature k = it % nf, 16-row slot kq = it / nf
+  const int nitems = nf * 4;
+  int it_k[kIt], it_kq[kIt], it_e[kIt];
+  bool it_ok[kIt], it_v[kIt];
+#pragma unroll
+  for (int u = 0; u < kIt; ++u) {
+    const int it = tid + NT * u;
+    it_ok[u] = it < nitems;
+    it_k[u] = it_ok[u] ? it % nf : 0;
+    it_kq[u] = it_ok[u] ? it / nf : 0;
+    const int k = it_k[u];
+    const int f = k < n0 ? f0 + k : f1 + k - n0;
+    it_v[u] = it_ok[u] && f < D;  // padding features (f >= D) slice as 0
+    it_e[u] = it_v[u] ? gi_exp(colmax[f]) : 0;
+  }
+  const int nrec = __builtin_amdgcn_readfirstlane(nrows * D * 4);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + r0 * D), 0, nrec, 0x00020000);
+  // chunk c into a stage: float4 unit v = 64 i + lane of its [64][nf] rows
+  // (instruction i = wave, wave + NW, ..., lane-linear 1 KB each); rows past
+  // the range read 0, features past d read the next row (never sliced)
+  const int nq = nf / 4;
+  const int my_dma = (nq - wave + NW - 1) / NW;  // this wave's instructions per chunk
+  auto dma = [&](int c, float* stg) {
+    if constexpr ((DIAG & 8) != 0) return;
+    for (int i = wave; i < nq; i += NW) {
+      const int v = 64 * i + lane;
+      const int row = v / nq, col = 4 * (v - row * nq);
+      const int f = col < n0 ? f0 + col : f1 + col - n0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(stg + 256 * i), 16,
+          ((c * kGiRows + row) * D + f) * 4, 0, 0, 0);
+    }
+  };
+  // wait for this wave's DMAs of the chunk before the newest `younger` ones
+  auto wait_older = [&](int younger) {
+    if (younger >= 7)
+      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else if (younger == 6)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  auto slice_item = [&](int u, const float* stg, int rows_left) {
+    if constexpr ((DIAG & 4) != 0) return;
+    if (it_ok[u]) {
+      const int k = it_k[u], kq = it_kq[u], e = it_e[u];
+      // every load issued, then masked (a per-element branch around each
+      // load waited for it: 16 dependent LDS round trips)
+      const int live = it_v[u] ? min(rows_left - 16 * kq, 16) : 0;
+      float xv[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xv[j] = stg[(16 * kq + j) * nf + k];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xv[j] = j < live ? xv[j] : 0.f;
+      unsigned w[4][kGiDig];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        gi_planes(gi_vbias(xv[4 * g + 0], e), gi_vbias(xv[4 * g + 1], e), gi_vbias(xv[4 * g + 2], e),
+                  gi_vbias(xv[4 * g + 3], e), w[g]);
+      const int slot = kq ^ gi_swz(k);
+#pragma unroll
+      for (int a = 0; a < kGiDig; ++a)
+        *reinterpret_cast<uint4*>(dig + ((a * kGsF + k) * 4 + slot) * 16) =
+            make_uint4(w[0][a], w[1][a], w[2][a], w[3][a]);
+    }
+  };
+  const int lf = lane & 15, lsl = lane >> 4;
+  auto rd = [&](int fl, int a) {
+    return *reinterpret_cast<const i32x4*>(dig + ((a * kGsF + fl) * 4 + (lsl ^ gi_swz(fl))) * 16);
+  };
+
+  if (nchunks > 0) dma(0, stage0);
+  if (nchunks > 1) dma(1, stage1);
+  for (int c = 0; c < nchunks; ++c) {
+    float* stg = (c & 1) ? stage1 : stage0;
+    wait_older(c + 1 < nchunks ? my_dma : 0);  // this wave's chunk-c DMAs have landed
+    barrier();  // every wave's chunk c is in the stage; chunk c - 1's MFMA reads are done
+#pragma unroll
+    for (int u = 0; u < kIt; ++u) slice_item(u, stg, nrows - c * kGiRows);
+    barrier();  // the digits are complete; the stage is free
+    if (c + 2 < nchunks) dma(c + 2, stg);
+#pragma unroll
+    for (int q = 0; q < MT; ++q) {
+      if (q < ntl) {
+        i32x4 A[kGiDig], Bd[kGiDig];
+#pragma unroll
+        for (int a = 0; a < kGiDig; ++a) A[a] = rd(la[q] + lf, a);
+#pragma unroll
+        for (int b = 0; b < kGiDig; ++b) Bd[b] = rd(lb[q] + lf, b);
+#pragma unroll
+        for (int b = 0; b < kGiDig; ++b) {
+          if constexpr ((DIAG & 1) != 0) {
+            asm volatile("" ::"v"(Bd[b]));
+          } else {
+#pragma unroll
+            for (int a = 0; a < kGiDig; ++a)
+              if (a + b < kGlLev)
+                lev[q][a + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[a], Bd[b], lev[q][a + b], 0, 0, 0);
+          }
+        }
+        if constexpr ((DIAG & 1) != 0) {
+#pragma unroll
+          for (int a = 0; a < kGiDig; ++a) asm volatile("" ::"v"(A[a]));
+        }
+      }
+    }
+  }
+  // the range's partials, as gram_i8l_kernel
+  const int T = nt * (nt + 1) / 2;
+  double* pr = part + static_cast<int64_t>(range) * T * 256;
+  const int lc = lane & 15, lr = 4 * (lane >> 4);
+#pragma unroll
+  for (int q = 0; q < MT; ++q) {
+    if (q < ntl) {
+      const int tau = ti[q] * nt - ti[q] * (ti[q] - 1) / 2 + (tj[q] - ti[q]);
+      const int fj = tj[q] * 16 + lc;
+      const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
+      const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int fi = ti[q] * 16 + lr + e;
+        const int ei = fi < D ? gi_exp(colmax[fi]) : 0;
+        const bool bad = (fi < D && !isfinite(__uint_as_float(colmax[fi]))) || !okj;
+        double sum = static_cast<double>(lev[q][0][e]);
+#pragma unroll
+        for (int l = 1; l < kGlLev; ++l) sum = fma(sum, 256.0, static_cast<double>(lev[q][l][e]));
+        pr[static_cast<int64_t>(tau) * 256 + (lr + e) * 16 + lc] =
+            bad ? __builtin_nan("") : ldexp(sum, ei + ej - 44);
+      }
+    }
+  }
+}
+
 // product shape: three workgroups per range (80 ranges), 8 waves, <= 8 tiles
 // per wave, each slicing two of three feature groups (<= 2 items per
 // thread), staggered slicing between SIMD partners (r05, tools/gram_ab.py at
@@ -3281,13 +3487,45 @@ static int gram_i8l_block(const float* x, const uint32_t* colmax, int64_t n, int
   return MMB_OK;
 }
 
+// The staged kernel on one block of rows (shape S, feature-group parts of
+// <= kGsF features each), then the range reduction.
+template <int DIAG, class S>
+static int gram_i8s_block(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
+                          int accumulate, double* part, hipStream_t stream) {
+  const GramLPlan q = gram_i8l_plan<S, true>(n, d);
+  int tiles = 0;
+  for (int k = 0; k < q.P; ++k) {
+    const GlPart& pk = q.parts.p[k];
+    MMB_REQUIRE(pk.n <= S::kPartMax);
+    MMB_REQUIRE(pk.n0 + pk.n1 <= kGsF && (pk.n0 + pk.n1) % 4 == 0 && pk.n0 % 16 == 0);
+    MMB_REQUIRE((pk.n0 + pk.n1) * 4 <= S::kIt * S::kNT);
+    tiles += pk.n;
+  }
+  MMB_REQUIRE(tiles == q.T);
+  MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8s_kernel<DIAG, S>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kGsLds));
+    attr = true;
+  }
+  gram_i8s_kernel<DIAG, S><<<S::kP * q.R, S::kNT, kGsLds, stream>>>(x, colmax, n, d, q.nt, q.chunk,
+                                                                    q.xcd, q.parts, part);
+  MMB_LAUNCH_CHECK();
+  const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
+  if (rc != MMB_OK) return rc;
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
 #ifdef MMB_DIAG
 // tools build: the level-sum kernel's shape (MMB_GRAM_I8_SHAPE: 0 the
 // product's three feature-group parts x 8 waves x 8 tiles, 1 four triangle
 // runs x 8 waves x 6 tiles, 2 three triangle runs x 8 waves x 8 tiles, 3 the
 // product with LDS reads free to cross tiles, 4 the product with the next
 // tile's first B digit prefetched, 5 the product without the staggered
-// slicing) and its timing-only ablations
+// slicing, 6 x staged in LDS by DMA: gram_i8s_kernel) and its timing-only
+// ablations
 static int gram_i8_shape() {
   const char* e = getenv("MMB_GRAM_I8_SHAPE");
   return e ? atoi(e) : 0;
@@ -3413,6 +3651,14 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
       case 3: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0x100, false, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
       case 4: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, true, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
       case 5: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
+      case 6:  // x staged in LDS (gram_i8s_kernel), the product's parts
+        switch (gram_i8_diag()) {
+          case 1: rc = gram_i8s_block<1, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
+          case 4: rc = gram_i8s_block<4, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
+          case 12: rc = gram_i8s_block<12, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
+          default: rc = gram_i8s_block<0, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
+        }
+        break;
       default: rc = gram_i8l_block_diag<GlProduct, true>(xb, colmax, nb, d, g, acc, part, stream); break;
     }
 #else

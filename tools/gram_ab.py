@@ -14,7 +14,8 @@ the product shape's
 timing-only ablations (MMB_GRAM_DIAG 1 no MFMAs, 4 no slicing, 12 no slicing
 and no x loads, 13 only barriers / LDS / epilogue), and 84 / 85 row ranges
 (252 / 255 workgroups, the parts of a range then on different XCDs;
-MMB_GRAM_RANGES) instead of 80, alternated over rounds;
+MMB_GRAM_RANGES) instead of 80, and x staged in LDS by DMA (MMB_GRAM_I8_SHAPE
+6: gram_i8s_kernel, with its ablations), alternated over rounds;
 HIP events around `reps` back-to-back calls (kernel + range reduction).
 Also each variant's max |G - G_f64| / max |G_f64| against the exact f64 Gram.
 """
@@ -48,6 +49,10 @@ VARIANTS = {
     "abl_skeleton": {"MMB_GRAM_DIAG": "13"},
     "ranges84": {"MMB_GRAM_RANGES": "84"},
     "ranges85": {"MMB_GRAM_RANGES": "85"},
+    "staged": {"MMB_GRAM_I8_SHAPE": "6"},
+    "staged_no_mfma": {"MMB_GRAM_I8_SHAPE": "6", "MMB_GRAM_DIAG": "1"},
+    "staged_no_slice": {"MMB_GRAM_I8_SHAPE": "6", "MMB_GRAM_DIAG": "4"},
+    "staged_no_slice_no_dma": {"MMB_GRAM_I8_SHAPE": "6", "MMB_GRAM_DIAG": "12"},
 }
 
 
@@ -84,7 +89,10 @@ def main():
     ap.add_argument("--n", type=int, nargs="+", default=[1_000_000, 125_000])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", nargs="+", default=None, help="a subset of VARIANTS (the product always)")
     args = ap.parse_args()
+    variants = {k: v for k, v in VARIANTS.items()
+                if args.variants is None or k in args.variants or k == "levels_groups3_stagger"}
     dev = torch.device("cuda", 0)
     nmax = max(args.n)
     inp = synth.device_workload(nmax, 40, 400_000, seed=1, device=dev)
@@ -103,18 +111,23 @@ def main():
         G64 = P.gram(x, None, ws=ws).clone()
         G = torch.empty_like(G64)
         res = {}
-        for name, kv in VARIANTS.items():
+        Gp = None
+        for name, kv in variants.items():
             with_env(kv, lambda: P.gram_i8(x, cm, G, ws=ws))
             torch.cuda.synchronize()
-            res[name] = {"err_vs_f64": float((G - G64).abs().max() / G64.abs().max()), "ms": []}
+            if name == "levels_groups3_stagger":
+                Gp = G.clone()
+            res[name] = {"err_vs_f64": float((G - G64).abs().max() / G64.abs().max()), "ms": [],
+                         "same_as_product": None if Gp is None else bool(torch.equal(G, Gp))}
         for _ in range(args.rounds):
-            for name, kv in VARIANTS.items():
+            for name, kv in variants.items():
                 res[name]["ms"].append(round(with_env(kv, lambda: timed(
                     lambda: P.gram_i8(x, cm, G, ws=ws), args.reps)), 4))
         for name in res:
             res[name]["ms_min"] = min(res[name]["ms"])
         out[str(n)] = res
-        print(json.dumps({"n": n, **{k: (v["ms_min"], v["err_vs_f64"]) for k, v in res.items()}}),
+        print(json.dumps({"n": n, **{k: (v["ms_min"], v["err_vs_f64"], v["same_as_product"])
+                                     for k, v in res.items()}}),
               flush=True)
     print(json.dumps(out), flush=True)
 
