@@ -3,7 +3,7 @@
 #   tests   the full -m gpu suite (one process), sha of the tree in the log
 #   robust  tests/test_gpu_robustness.py + tests/test_gpu_variants.py only
 #   smoke   __graft_entry__.smoke()
-#   bench   the default bench line (N = 1, every configs_measured leg)
+#   bench   the driver's bench line (N = 1, --steps 20 --warmup 5, every configs_measured leg)
 #   main    bench.py --only-main (headline only, no CPU leg)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
@@ -30,7 +30,7 @@ for step in "$@"; do
       tail -1 "$OUT/smoke.log"
       ;;
     bench)
-      timeout -k 10 600 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
+      timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
       ;;
     main)
       timeout -k 10 300 python3 -u bench.py --only-main --no-cpu-baseline --steps 10 --warmup 3 \
