@@ -37,7 +37,8 @@ def _child(group, tmp_path):
     return r.stdout
 
 
-@pytest.mark.parametrize("group", ["projection", "fused_order", "remove_rows", "gram", "timeouts"])
+@pytest.mark.parametrize("group", ["projection", "fused_order", "remove_rows", "gram", "narrow_teams",
+                                   "timeouts"])
 def test_variants_agree(gpu, tmp_path, group):
     _child(group, tmp_path)
 

@@ -5,7 +5,8 @@ no environment variable.  The variants the design notes measured -- the
 projection's 32x32x16 / un-pipelined / register-A (3) / 256-row (4) /
 register-B (6) kernels and its tile-layout epilogue, the stream kernel's
 load/store policies and grid sizes, the fused kernel's group-at-a-time and
-pipelined streamers and its unbalanced tail, the one-row PC removal -- live in
+pipelined streamers and its unbalanced tail, the narrow fused kernel's
+4-wave teams, the int8 Gram with x staged in LDS, the one-row PC removal -- live in
 the tools build, libmmb_diag.so (`make diag`, -DMMB_DIAG), where MMB_* knobs
 select them per launch.  This script runs in a child process that loads
 that build explicitly (mmb_lib.load(path), tests/test_gpu_variants.py) and asserts
@@ -208,13 +209,47 @@ def check_remove_rows(dev):
 def check_gram_schedules(dev):
     """The int8 Gram's timing-only ablations are wrong by design; its product
     schedule (MMB_GRAM_DIAG unset) must equal the product library's Gram --
-    checked here against the exact f64 Gram to the int8 format's 2e-9."""
-    x = torch.randn(5000, 300, device=dev) * 0.3
-    G8 = P.gram_i8(x, P.colmax(x))
-    G64 = P.gram(x, None)
-    torch.cuda.synchronize()
-    assert (G8 - G64).abs().max().item() <= 2e-9 * G64.abs().max().item()
-    print("gram: int8 schedule within 2e-9 of f64")
+    checked here against the exact f64 Gram to the int8 format's 2e-9 -- and
+    the kernel with x staged in LDS by DMA (MMB_GRAM_I8_SHAPE=6,
+    gram_i8s_kernel: the same digits and exact level sums) equals it bit for
+    bit, a partial last chunk included (77,777 rows)."""
+    for n in (5000, 77_777):
+        g = torch.Generator(device=dev).manual_seed(n)
+        x = torch.randn(n, 300, generator=g, device=dev) * 0.3
+        cm = P.colmax(x)
+        G8 = P.gram_i8(x, cm).clone()
+        with knobs(MMB_GRAM_I8_SHAPE=6):
+            Gs = P.gram_i8(x, cm).clone()
+        G64 = P.gram(x, None)
+        torch.cuda.synchronize()
+        assert (G8 - G64).abs().max().item() <= 2e-9 * G64.abs().max().item(), n
+        assert torch.equal(G8, Gs), n
+    print("gram: int8 schedule within 2e-9 of f64; the LDS-staged kernel bit-identical")
+
+
+def check_narrow_teams(dev):
+    """The narrow fused kernel (MOSI widths) run as two 4-wave teams with their
+    own 16-row batches, LDS halves and barriers (MMB_NF_TEAMS=1, and =2 with
+    team 1 a stream phase late) against the product's 32-row workgroup
+    batches: every row is computed the same way whichever team takes it, so
+    x, aux, the MMB2 and SIF rows, the column bounds and the PC are
+    bit-identical -- 1, 2 and 4 utterances per wave (N = 1284, 6000, 40,000)."""
+    for n in (1284, 6000, 40_000):
+        inp = synth.device_workload(n, 20, 3016, A=76, Vd=48, seed=70 + n % 97, device=dev)
+        st = P.FusedStep(inp, _gen(dev, 76, 48).networks(), narrow_fused=True)
+        assert st.narrow_fused
+        outs = {}
+        for v in ("0", "1", "2"):
+            with knobs(MMB_NF_TEAMS=v):
+                st.run(check=True)
+                torch.cuda.synchronize()
+            # (colmax: None below the int8 Gram's row threshold)
+            outs[v] = [None if t is None else t.clone()
+                       for t in (st.x, st.aux, st.mmb2, st.sif, st.colmax, st.pc)]
+        for v in ("1", "2"):
+            for a, b in zip(outs["0"], outs[v]):
+                assert (a is None and b is None) or torch.equal(a, b), (n, v)
+    print("narrow teams: two 4-wave teams bit-identical to the workgroup batches")
 
 
 def check_timeouts(dev):
@@ -281,7 +316,7 @@ def check_timeouts(dev):
 GROUPS = {"projection": check_projection, "fused_streamer": check_fused_streamer,
           "fused_order": check_fused_order,
           "remove_rows": check_remove_rows, "gram": check_gram_schedules,
-          "timeouts": check_timeouts}
+          "narrow_teams": check_narrow_teams, "timeouts": check_timeouts}
 
 
 def main(argv):
