@@ -189,7 +189,8 @@ def load_traffic(name, utts_per_launch, tokens, phase="mm2_stream"):
         tj = json.load(f)
     if (tj.get("utts_per_launch") == utts_per_launch and tj.get("tokens") == tokens
             and tj.get("phase", "mm2_stream") == phase):
-        return tj.get("mm2_stream_hbm_bytes_per_launch"), f"profiles/{fn} ({tj.get('tag')})"
+        sha = f", tree {tj['tree_sha']}" if tj.get("tree_sha") else ""
+        return tj.get("mm2_stream_hbm_bytes_per_launch"), f"profiles/{fn} ({tj.get('tag')}{sha})"
     return None, None
 
 
