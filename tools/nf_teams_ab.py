@@ -9,6 +9,7 @@ median kernel and step times (HIP events), and whether the variants' rows
 are bit-identical to the product's.
 
     python tools/nf_teams_ab.py [--n 1000000 1284] [--steps 4] [--rounds 3]
+    python tools/nf_teams_ab.py --knob MMB_NF_ILP --values 0 2   (utterance pairs, r05)
 """
 import argparse
 import json
@@ -20,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multimodal-baselines_amd")]
 import mmb_lib  # noqa: E402
 
-mmb_lib.load(os.path.join(ROOT, "tools", "diag", "libmmb_diag.so"))
+# (MMB_TOOLS_LIB: another tools-build library, e.g. one with other NF_* build knobs)
+mmb_lib.load(os.environ.get("MMB_TOOLS_LIB", os.path.join(ROOT, "tools", "diag", "libmmb_diag.so")))
 import torch  # noqa: E402
 
 import models  # noqa: E402
@@ -28,6 +30,7 @@ import pipeline as P  # noqa: E402
 import synth  # noqa: E402
 
 VARIANTS = {"one_batch": "0", "teams": "1", "teams_lag": "2"}
+KNOB = "MMB_NF_TEAMS"
 
 
 def main():
@@ -36,7 +39,16 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", nargs="+", default=list(VARIANTS))
+    ap.add_argument("--knob", default=None, help="another tools-build knob, e.g. MMB_NF_ILP, with "
+                                                 "--values (variant name = value)")
+    ap.add_argument("--values", nargs="+", default=None)
     args = ap.parse_args()
+    global KNOB
+    if args.knob:
+        KNOB = args.knob
+        VARIANTS.clear()
+        VARIANTS.update({f"{args.knob}={v}": v for v in args.values})
+        args.variants = list(VARIANTS)
     dev = torch.device("cuda", 0)
     T, V, A, Vd = 20, 3016, 76, 48
     for n in args.n:
@@ -48,7 +60,7 @@ def main():
         outs = {}
         for _ in range(args.rounds):
             for name in args.variants:
-                os.environ["MMB_NF_TEAMS"] = VARIANTS[name]
+                os.environ[KNOB] = VARIANTS[name]
                 st.run()
                 torch.cuda.synchronize()
                 for _ in range(args.steps):
@@ -62,7 +74,7 @@ def main():
                     res[name]["step"].append(a.elapsed_time(b))
                 st.check()
                 outs[name] = [t.clone() for t in (st.x, st.mmb2, st.sif)]
-        os.environ.pop("MMB_NF_TEAMS", None)
+        os.environ.pop(KNOB, None)
         base = outs[args.variants[0]]
         same = {k: all(torch.equal(u, v) for u, v in zip(base, o)) for k, o in outs.items()}
         out = {k: {m: round(statistics.median(v), 4) for m, v in d.items()} for k, d in res.items()}
