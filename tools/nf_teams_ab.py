@@ -9,7 +9,9 @@ median kernel and step times (HIP events), and whether the variants' rows
 are bit-identical to the product's.
 
     python tools/nf_teams_ab.py [--n 1000000 1284] [--steps 4] [--rounds 3]
-    python tools/nf_teams_ab.py --knob MMB_NF_ILP --values 0 2   (utterance pairs, r05)
+    python tools/nf_teams_ab.py --knob NAME --values V0 V1 ...   (another narrow-kernel knob;
+        r05's utterance-pair knob MMB_NF_ILP was measured this way, profiles/r05_narrow/pairs_ab.txt,
+        and removed)
 """
 import argparse
 import json
@@ -39,7 +41,7 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", nargs="+", default=list(VARIANTS))
-    ap.add_argument("--knob", default=None, help="another tools-build knob, e.g. MMB_NF_ILP, with "
+    ap.add_argument("--knob", default=None, help="another tools-build knob, with "
                                                  "--values (variant name = value)")
     ap.add_argument("--values", nargs="+", default=None)
     args = ap.parse_args()
