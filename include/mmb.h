@@ -252,7 +252,9 @@ int mmb_mm2_split_pieces(const float* wm, int d, int a, int vd, int ldw, void* i
  * launch) instead of a second pass over x.  colmax_ws: scratch of
  * mmb_mm2_colmax_ws_bytes(d) bytes (its last 16 bytes: the batch counter of
  * mmb_mm2_stream_project's dynamic batch order, zeroed by that call itself;
- * one launch at a time per workspace).                                      */
+ * one launch at a time per workspace).  ABI note (r05): the size grew by those
+ * 16 bytes; a workspace sized by hand from the r04 formula (8192 x d floats)
+ * is too small and nothing can check it -- always size it with this call.   */
 size_t mmb_mm2_colmax_ws_bytes(int d);
 
 /* Padded width (row stride) of the per-utterance sums: roundup(2(d+a+vd), 32). */

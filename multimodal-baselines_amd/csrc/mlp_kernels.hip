@@ -693,9 +693,10 @@ static int launch_train_mc(const TrainArgs& a, size_t lds, hipStream_t stream) {
   // launch cooperatively where the device supports it (the runtime then
   // refuses a grid that cannot be co-resident instead of dispatching part of
   // it behind other work; the bounded waits stay as the last line)
-  int dev = 0, n_cu = 0, per_cu = 0, coop = 0;
+  // (the CUs of the stream: a CU-masked stream co-schedules fewer)
+  int dev = 0, per_cu = 0, coop = 0;
+  const int n_cu = stream_cu_count(stream);
   hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev);
   if (e == hipSuccess)
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(

@@ -1208,6 +1208,7 @@ __global__ void xt_omega_kernel(const TX* __restrict__ num, const float* __restr
 // columns (every load of a lane independent), then a fixed-order DPP wave sum
 // per column.  The thread-per-output kernel above walked all N rows as one
 // dependent chain of loads: 59 us for a 229-row split (r04 dataset_splits).
+constexpr int64_t kXtOmegaWaveMaxN = 4096;  // rows up to which the launchers pick it
 template <typename TX>
 __global__ __launch_bounds__(256) void xt_omega_wave_kernel(const TX* __restrict__ num,
                                                             const float* __restrict__ cnt,
@@ -2218,9 +2219,12 @@ constexpr int kPmKs = 6;   // k-steps of G per wave: ceil(kP16MaxD / 4 / kPmPw)
 constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
 
 #ifdef MMB_DIAG
-// tools build: a test shortens the bounded waits to drive the timeout path
-// (mmb_diag_pc_wait_iters)
+// tools build: a test shortens the bounded waits (mmb_diag_pc_wait_iters) and
+// names one workgroup that never arrives (mmb_diag_pc_skip_arrival), so the
+// count a wait polls for cannot be reached whatever the arrival skew: the
+// timeout path runs deterministically
 __device__ int g_pm_wait_iters = 1 << 20;
+__device__ int g_pm_skip_wg = -1;
 #endif
 __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned* abort_w,
                                         int32_t* flag) {
@@ -2252,6 +2256,9 @@ __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned
 // waits pass before the other workgroups' tiles are written.
 __device__ __forceinline__ bool pm_arrive(unsigned* ctr, int T, int r, unsigned* abort_w,
                                           int32_t* flag) {
+#ifdef MMB_DIAG
+  if (static_cast<int>(blockIdx.x) == g_pm_skip_wg) return true;  // never arrives
+#endif
   const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old >= static_cast<unsigned>(T * r) && old < static_cast<unsigned>(T * (r + 1))) return true;
   __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2960,6 +2967,13 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   if (!transposed) p16_gram2<kPnNW>(sY, sY, sT, sZ, sY, sW, Dp, k, part);
   PC_MARK(40);
   p16_tail<kPnNW>(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT, !transposed);
+  // a workspace handed over with a stale count in (0, T) lets the final wait
+  // pass early; the overshooting arrivals set the abort word.  Re-read it
+  // after the tail so a PC that raced them is overwritten with NaN (the flag
+  // word stays the primary signal)
+  __syncthreads();
+  if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    for (int e = tid; e < npc * D; e += kPnNT) pc_out[e] = __builtin_nan("");
   PC_PROBE_FLUSH();
 }
 
@@ -3696,7 +3710,9 @@ extern "C" int mmb_gram_finish(int64_t n_plan, int d, double* g, int accumulate,
 extern "C" int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d,
                             const double* omega, int k, double* z0, hipStream_t stream) {
   MMB_REQUIRE(num && omega && z0 && n >= 0 && d > 0 && k > 0);
-  if (k <= 16)  // (the solver's k = npc + 10 <= 16)
+  // the wave kernel is for the transposed branch's small splits: at large N
+  // each of its d waves would re-read all of Omega (N x k)
+  if (k <= 16 && n <= kXtOmegaWaveMaxN)  // (the solver's k = npc + 10 <= 16)
     xt_omega_wave_kernel<float><<<static_cast<int>(ceil_div(d, 4)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
   else
     xt_omega_kernel<float><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
@@ -3852,7 +3868,7 @@ extern "C" int mmb_gram_f64(const double* x, int64_t n, int d, double* g, int ac
 extern "C" int mmb_xt_omega_f64(const double* x, int64_t n, int d, const double* omega, int k,
                                 double* z0, hipStream_t stream) {
   MMB_REQUIRE(x && omega && z0 && n >= 0 && d > 0 && k > 0);
-  if (k <= 16)
+  if (k <= 16 && n <= kXtOmegaWaveMaxN)
     xt_omega_wave_kernel<double><<<static_cast<int>(ceil_div(d, 4)), 256, 0, stream>>>(x, nullptr, n, d, omega, k, z0);
   else
     xt_omega_kernel<double><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(
@@ -3879,6 +3895,14 @@ extern "C" int mmb_pc_remove_f64(const double* x, int64_t n, int d, const double
 extern "C" int mmb_diag_pc_wait_iters(int iters) {
   MMB_REQUIRE(iters >= 1);
   const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_pm_wait_iters), &iters, sizeof(int));
+  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
+}
+
+// tools build: workgroup wg of the multi-workgroup solve skips its arrivals
+// (-1: none, the product behaviour); every wait of the launch then times out
+extern "C" int mmb_diag_pc_skip_arrival(int wg) {
+  MMB_REQUIRE(wg >= -1);
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_pm_skip_wg), &wg, sizeof(int));
   return e == hipSuccess ? MMB_OK : static_cast<int>(e);
 }
 #endif

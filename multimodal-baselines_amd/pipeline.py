@@ -476,6 +476,7 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
     if s.dtype != (torch.float16 if s_half else torch.float32):
         raise L.MMBError("s buffer dtype does not match s_half")
     V = table.shape[0] if table is not None else 0
+    _check_colmax_ws(colmax_ws, d)
     L.call("mmb_mm2_stream", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32), L.ptr(text_dense),
            L.ptr(emb_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
            L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag), L.ptr(colmax),
@@ -523,6 +524,7 @@ def mm2_stream_project_narrow(n, t, d, a, vd, audio, visual, proj: "MMB2Projecti
                torch.empty((n, d), dtype=torch.float32, device=dev))
     num, aux, mmb2 = out
     proj.enable_text_cache(table, wtab32)
+    _check_colmax_ws(colmax_ws, d)
     L.call("mmb_mm2_stream_project_narrow", L.ptr(ids32), L.ptr(table), table.shape[0],
            L.ptr(wtab32), L.ptr(proj.text_cache), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
            L.ptr(proj.wpieces), L.ptr(proj.c0), L.ptr(num), L.ptr(aux), L.ptr(mmb2), L.ptr(flag),
@@ -544,11 +546,23 @@ def mm2_stream_project(n, t, d, a, vd, audio, visual, proj: "MMB2Projection", id
     num, aux, mmb2 = out
     proj.enable_pieces()
     V = table.shape[0] if table is not None else 0
+    _check_colmax_ws(colmax_ws, d)
     L.call("mmb_mm2_stream_project", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32),
            L.ptr(text_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
            L.ptr(proj.wpieces), L.ptr(proj.c0), L.ptr(num), L.ptr(aux), L.ptr(mmb2), L.ptr(flag),
            L.ptr(colmax), L.ptr(colmax_ws), L.stream_ptr())
     return num, aux, mmb2
+
+
+def _check_colmax_ws(colmax_ws, d: int) -> None:
+    """The C ABI takes the workspace as a bare pointer; the mirror checks its
+    size (mmb_mm2_colmax_ws_bytes grew by 16 bytes in r05, include/mmb.h)."""
+    if colmax_ws is None:
+        return
+    need = int(L.query("mmb_mm2_colmax_ws_bytes", d))
+    have = colmax_ws.numel() * colmax_ws.element_size()
+    if have < need:
+        raise L.MMBError(f"colmax_ws holds {have} bytes; mmb_mm2_colmax_ws_bytes({d}) = {need}")
 
 
 def s_buffer(n: int, kp: int, s_half: bool, device) -> torch.Tensor:

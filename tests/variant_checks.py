@@ -253,12 +253,16 @@ def check_narrow_teams(dev):
 
 
 def check_timeouts(dev):
-    """The bounded hand-over waits' timeout path, driven by cutting the tools
-    build's wait budget to one poll (mmb_diag_fused_wait_iters /
-    mmb_diag_pc_wait_iters): the fused stream + projection kernel and the
-    multi-workgroup PC solve end (no hang), report MMB_FLAG_SYNC_TIMEOUT, and
-    FusedStep.check raises RuntimeError; with the product budget restored
-    the same step and solve reproduce their results bit for bit."""
+    """The bounded hand-over waits' timeout path: the fused stream +
+    projection kernel with its wait budget cut to one poll
+    (mmb_diag_fused_wait_iters), the multi-workgroup PC solve with
+    workgroup 1 never arriving (mmb_diag_pc_skip_arrival) -- the count its
+    waits poll for cannot be reached whatever the arrival skew, so the
+    timeout is deterministic (r05: a one-poll budget alone raced the
+    co-resident workgroups' arrivals and passed on the driver's box).  Both
+    end (no hang), report MMB_FLAG_SYNC_TIMEOUT, leave a NaN PC, and the
+    callers raise RuntimeError; with the product behaviour restored the same
+    step and solve reproduce their results bit for bit."""
     lib = L.load()
     inp = synth.device_workload(20_000, 40, 20_000, seed=81, device=dev)
     step = P.FusedStep(inp, _gen(dev).networks(), stream_project=True)
@@ -288,7 +292,8 @@ def check_timeouts(dev):
     torch.cuda.synchronize()
     assert int(flag.item()) == 0
     try:
-        assert lib.mmb_diag_pc_wait_iters(1) == 0
+        assert lib.mmb_diag_pc_wait_iters(256) == 0
+        assert lib.mmb_diag_pc_skip_arrival(1) == 0
         pcx = P.pc_solve(G, z0, 1, False, flag=flag)
         torch.cuda.synchronize()
         assert int(flag.item()) & L.MMB_FLAG_SYNC_TIMEOUT
@@ -304,6 +309,7 @@ def check_timeouts(dev):
             else:
                 raise AssertionError("a no-flag PC solve did not raise on the hand-over timeout")
     finally:
+        assert lib.mmb_diag_pc_skip_arrival(-1) == 0
         assert lib.mmb_diag_pc_wait_iters(1 << 20) == 0
     flag.zero_()
     P.solve_workspace(300, dev)[:16].zero_()  # an aborted solve leaves its control words set
