@@ -215,6 +215,29 @@ int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const floa
                    int vd, float* num_out, void* s_out, int s_half, float* aux_out,
                    int32_t* flag, uint32_t* colmax, void* colmax_ws, hipStream_t stream);
 
+/* mmb_mm2_stream for a few long rows (POM's splits: 100 / 203 transcripts of
+ * 1089 / 1357 tokens), split over workgroups: every utterance is cut into P
+ * token / frame ranges (parts = 0: mmb_mm2_stream_split_parts, about one
+ * workgroup per CU in all; parts > 0: that many, at most t), each range
+ * summed by a text, an audio and a visual workgroup of its own whose
+ * partial sums go to ws (mmb_mm2_stream_split_ws_bytes(n, t, d, a, vd, parts) bytes,
+ * caller-owned scratch), and a second kernel adds an utterance's partials in
+ * fixed part order and writes the same outputs as mmb_mm2_stream (x, s in
+ * the s_half format asked for, aux, colmax; n <= 8192 with colmax).  Rows are
+ * deterministic and equal mmb_mm2_stream's to the f32 order of the token and
+ * frame sums.
+ * replaces: the frame loops of sif2.estimate_embedding_overall_gpu2
+ *   /root/reference/sif2.py:181-205 at the per-split call sites
+ *   /root/reference/simplesif.py:308-311 (POM's long transcripts)          */
+int mmb_mm2_stream_split_parts(int64_t n, int t);
+size_t mmb_mm2_stream_split_ws_bytes(int64_t n, int t, int d, int a, int vd, int parts);
+int mmb_mm2_stream_split(const int32_t* ids, const float* table, int64_t v, const float* wtab32,
+                         const float* text_dense, const float* emb_dense, const float* w_dense,
+                         const float* audio, const float* visual, int64_t n, int t, int d, int a,
+                         int vd, float* num_out, void* s_out, int s_half, float* aux_out,
+                         int32_t* flag, uint32_t* colmax, void* colmax_ws, int parts, void* ws,
+                         size_t ws_bytes, hipStream_t stream);
+
 /* mmb_mm2_stream and mmb_mm2_project_x3 in ONE kernel (the bench step's
  * MMB2 path): the same num (x), aux[0..1] and colmax outputs as mmb_mm2_stream
  * (aux[2] is the text piece's scale) and the MMB2 rows of mmb_mm2_project_x3

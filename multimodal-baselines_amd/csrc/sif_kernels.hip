@@ -130,6 +130,46 @@ __device__ __forceinline__ void stage_token(const StreamArgs& a, int64_t i, int 
 // (flagged) are dropped: they contribute nothing (sif_functions.py:8-15).
 constexpr int kStageIters = (kTokChunk + kNT - 1) / kNT;
 
+// The text rows of a staged token chunk (workgroup kernels): row slot rT
+// of the chunk's nkeep kept tokens, CT column units of VT floats at cT.
+// Branch-free per row (a negative offset loads row 0 and contributes
+// nothing) and SPLIT (the weighted sum over a different dense tensor) a
+// template argument, so the TU unrolled rows' loads issue together: a
+// runtime `split_emb` test per row put a branch and a wait for that row's
+// load after every load (r06: the gfx950 ISA of the split-part kernel).
+template <bool MM2, bool SPLIT, int VT, int TU>
+__device__ __forceinline__ void text_rows(const float* tsrc, const float* esrc, const int64_t* s_off,
+                                          const float* s_w, int nkeep, int rT, int RT, int cT,
+                                          float (&num)[VT], float (&sx)[VT], float (&sxx)[VT]) {
+#pragma unroll TU
+  for (int t = rT; t < nkeep; t += RT) {
+    const float w = s_w[t];
+    const int64_t off = s_off[t];
+    const bool ok = off >= 0;
+    const int64_t o = ok ? off : 0;
+    float v[VT];
+    ldv<VT>(tsrc + o + cT * VT, v);
+#pragma unroll
+    for (int e = 0; e < VT; ++e) v[e] = ok ? v[e] : 0.f;
+    if constexpr (SPLIT) {
+      float u[VT];
+      ldv<VT>(esrc + o + cT * VT, u);
+#pragma unroll
+      for (int e = 0; e < VT; ++e) num[e] = fmaf(w, ok ? u[e] : 0.f, num[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VT; ++e) num[e] = fmaf(w, v[e], num[e]);
+    }
+    if constexpr (MM2) {
+#pragma unroll
+      for (int e = 0; e < VT; ++e) {
+        sx[e] += v[e];
+        sxx[e] = fmaf(v[e], v[e], sxx[e]);
+      }
+    }
+  }
+}
+
 // FU: frame rows (and TU: text rows) per thread in flight -- 4 / 4 when the
 // grid fills the chip (occupancy hides the latency); for a few hundred long
 // rows (dataset splits: one workgroup per CU at most, so one workgroup's
@@ -215,33 +255,10 @@ __global__ __launch_bounds__(NT) void utt_stream_kernel(StreamArgs a) {
         // 0 and contributes nothing, so the unrolled iterations keep their
         // loads in flight together (a `continue` per token would wait on
         // each load right after its branch)
-#pragma unroll TU
-        for (int t = rT; t < nkeep; t += RT) {
-          const float w = s_w[t];
-          const int64_t off = s_off[t];
-          const bool ok = off >= 0;
-          const int64_t o = ok ? off : 0;
-          float v[VT];
-          ldv<VT>(tsrc + o + cT * VT, v);
-#pragma unroll
-          for (int e = 0; e < VT; ++e) v[e] = ok ? v[e] : 0.f;
-          if (split_emb) {
-            float u[VT];
-            ldv<VT>(esrc + o + cT * VT, u);
-#pragma unroll
-            for (int e = 0; e < VT; ++e) num[e] = fmaf(w, ok ? u[e] : 0.f, num[e]);
-          } else {
-#pragma unroll
-            for (int e = 0; e < VT; ++e) num[e] = fmaf(w, v[e], num[e]);
-          }
-          if constexpr (MM2) {
-#pragma unroll
-            for (int e = 0; e < VT; ++e) {
-              sx[e] += v[e];
-              sxx[e] = fmaf(v[e], v[e], sxx[e]);
-            }
-          }
-        }
+        if (split_emb)
+          text_rows<MM2, true, VT, TU>(tsrc, esrc, s_off, s_w, nkeep, rT, RT, cT, num, sx, sxx);
+        else
+          text_rows<MM2, false, VT, TU>(tsrc, esrc, s_off, s_w, nkeep, rT, RT, cT, num, sx, sxx);
       }
       __syncthreads();
     }
@@ -405,6 +422,321 @@ __global__ __launch_bounds__(NT) void utt_stream_kernel(StreamArgs a) {
   }
   if (MM2 && a.cmax_part) {  // this workgroup's column bounds (mmb_gram_i8)
     float* pr = a.cmax_part + static_cast<int64_t>(blockIdx.x) * a.D;
+    if (tid < a.D) pr[tid] = cmx0;
+    if (tid + NT < a.D) pr[tid + NT] = cmx1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Few long rows split over workgroups (r06; POM's splits: 100 / 203
+// transcripts of 1089 / 1357 aligned tokens).  One workgroup per utterance
+// (utt_stream_kernel) puts 100 / 203 workgroups on 256 CUs, each a
+// 1,089-1,357-frame chain: 0.21 / 0.42 of 8 TB/s.  Here every utterance is
+// cut into P ranges of Lc tokens / frames and each range has a text and a
+// frame workgroup, in ONE launch: the text workgroups (blocks [0, N Pt):
+// token staging, the kept rows' gather, the counts) first, then the frame
+// workgroups (one modality each, audio then visual: pure streams, no
+// staging, no barrier before their reduction), each writing PARTIAL sums; utt_split_finish_kernel adds
+// an utterance's partials in fixed part order and finishes the row as
+// utt_stream_kernel does (x = num / count, the s row, aux, the row scale,
+// the column bounds) -- writing the fp16 hi / lo planes directly, so the
+// s_half path needs no split_rows pass.  Deterministic; against the
+// one-workgroup kernel only the f32 order of the token and frame sums
+// differs (with one range it is the same order: bit-identical).
+//
+// Workspace (floats): text partials [N][Pt][Wt] = [num (D) | Sx_e (D) |
+// Sxx_e (D) | count_nonzero(w), sum w, row-0 tokens, their weight sum] (row
+// 0 excluded from the sums, as utt_stream_kernel), then frame partials
+// [N][Pf][Wf] = [Sx_a (A) | Sxx_a (A) | Sx_v (Vd) | Sxx_v (Vd)].
+struct SplitPlan {
+  int Pt, Lt, Pf, Lf;  // text / frame parts per utterance and their lengths
+  int Wt, Wf;          // partial row strides (floats, multiples of 4)
+};
+inline SplitPlan split_plan_of(int t, int d, int a, int vd, int Pf) {
+  SplitPlan q;
+  q.Lf = (t + Pf - 1) / Pf;
+  q.Pf = (t + q.Lf - 1) / q.Lf;  // no empty part
+  // the text ranges are the frame ranges (over kTokChunk tokens they are
+  // staged chunk by chunk): with one range the sums run in the one-workgroup
+  // kernel's order.  One LDS chunk per text workgroup instead measured no
+  // faster (POM valid 57.5 vs 55.3 us, r06 tools/split_ab.py)
+  q.Lt = q.Lf;
+  q.Pt = q.Pf;
+  q.Wt = (3 * d + 4 + 3) / 4 * 4;
+  q.Wf = (2 * a + 2 * vd + 3) / 4 * 4;
+  return q;
+}
+
+template <int VT, int VA, int VV, int FU = 16, int TU = 8>
+__global__ __launch_bounds__(kNT) void utt_split_part_kernel(StreamArgs a, SplitPlan q,
+                                                             float* __restrict__ part) {
+  constexpr int NT = kNT;
+  constexpr int kRF = NT * 4;
+  constexpr int kSI = (kTokChunk + NT - 1) / NT;
+  __shared__ int64_t s_off[kTokChunk];
+  __shared__ float s_w[kTokChunk];
+  __shared__ float s_red[4 * kRF];
+  __shared__ float s_sc[4][NT / kWave];
+  __shared__ int s_keep[kSI][NT / kWave];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), wave = tid / kWave;
+  const int64_t ntext = a.N * q.Pt;
+  if (static_cast<int64_t>(blockIdx.x) < ntext) {
+    // ---- a token range: staging, the kept rows, the counts
+    const int64_t i = blockIdx.x / q.Pt;
+    const int p = static_cast<int>(blockIdx.x - i * q.Pt);
+    const int tb = p * q.Lt, te = min(a.L, tb + q.Lt);
+    const int CT = a.D / VT, RT = NT / CT;
+    const int rT = tid / CT, cT = tid - rT * CT;
+    const bool actT = rT < RT;
+    const float* tsrc = a.ids ? a.table : a.text_dense;
+    const float* esrc = a.ids ? a.table : a.emb_dense;
+    const bool gather = a.ids != nullptr;
+    float num[VT], sx[VT], sxx[VT];
+#pragma unroll
+    for (int e = 0; e < VT; ++e) num[e] = sx[e] = sxx[e] = 0.f;
+    float cntp = 0.f, swp = 0.f, c0p = 0.f, w0p = 0.f;
+    for (int t0 = tb; t0 < te; t0 += kTokChunk) {  // the range in LDS chunks
+      const int tl = min(kTokChunk, te - t0);
+      int64_t off_k[kSI];
+      float w_k[kSI];
+      int rank_k[kSI];
+      bool keep_k[kSI];
+#pragma unroll
+      for (int k = 0; k < kSI; ++k) {
+        const int t = tid + k * NT;
+        int64_t off = -1;
+        float w = 0.f;
+        if (t < tl) {
+          stage_token(a, i, t0 + t, off, w);
+          cntp += (w != 0.f) ? 1.f : 0.f;
+          swp += w;
+          if (gather && off == 0) {
+            c0p += 1.f;
+            w0p += w;
+          }
+        }
+        const bool keep = t < tl && (gather ? off > 0 : true);
+        const unsigned long long bal = __ballot(keep);
+        rank_k[k] = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) s_keep[k][wave] = __popcll(bal);
+        off_k[k] = off;
+        w_k[k] = w;
+        keep_k[k] = keep;
+      }
+      __syncthreads();
+      int nkeep = 0;
+#pragma unroll
+      for (int k = 0; k < kSI; ++k) {
+        for (int v = 0; v < NT / kWave; ++v) {
+          if (keep_k[k] && v == wave) {
+            s_off[nkeep + rank_k[k]] = off_k[k];
+            s_w[nkeep + rank_k[k]] = w_k[k];
+          }
+          nkeep += s_keep[k][v];
+        }
+      }
+      __syncthreads();
+      if (actT) {
+        if (esrc != tsrc)
+          text_rows<true, true, VT, TU>(tsrc, esrc, s_off, s_w, nkeep, rT, RT, cT, num, sx, sxx);
+        else
+          text_rows<true, false, VT, TU>(tsrc, esrc, s_off, s_w, nkeep, rT, RT, cT, num, sx, sxx);
+      }
+      __syncthreads();
+    }
+    cntp = wave_sum(cntp);
+    swp = wave_sum(swp);
+    c0p = wave_sum(c0p);
+    w0p = wave_sum(w0p);
+    if (lane == 0) {
+      s_sc[0][wave] = cntp;
+      s_sc[1][wave] = swp;
+      s_sc[2][wave] = c0p;
+      s_sc[3][wave] = w0p;
+    }
+    if (actT) {
+#pragma unroll
+      for (int e = 0; e < VT; ++e) {
+        const int f = rT * a.D + cT * VT + e;
+        s_red[f] = num[e];
+        s_red[kRF + f] = sx[e];
+        s_red[2 * kRF + f] = sxx[e];
+      }
+    }
+    __syncthreads();
+    float* prow = part + (i * q.Pt + p) * static_cast<int64_t>(q.Wt);
+    for (int f = tid; f < a.D; f += NT) {  // the row slots summed in order
+      float n_ = 0.f, x1 = 0.f, x2 = 0.f;
+      for (int r = 0; r < RT; ++r) {
+        n_ += s_red[r * a.D + f];
+        x1 += s_red[kRF + r * a.D + f];
+        x2 += s_red[2 * kRF + r * a.D + f];
+      }
+      prow[f] = n_;
+      prow[a.D + f] = x1;
+      prow[2 * a.D + f] = x2;
+    }
+    if (tid < 4) {
+      float sc = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT / kWave; ++w) sc += s_sc[tid][w];
+      prow[3 * a.D + tid] = sc;
+    }
+    return;
+  }
+  // ---- a frame range of ONE modality (audio workgroups, then visual)
+  const int64_t b = blockIdx.x - ntext;
+  const bool vis = b >= a.N * q.Pf;
+  const int64_t bm = vis ? b - a.N * q.Pf : b;
+  const int64_t i = bm / q.Pf;
+  const int p = static_cast<int>(bm - i * q.Pf);
+  const int tb = p * q.Lf, te = min(a.L, tb + q.Lf);
+  float* prow = part + ntext * q.Wt + (i * q.Pf + p) * static_cast<int64_t>(q.Wf);
+  auto stream = [&](const float* src, int F, float* out, auto vec) {
+    constexpr int VF = decltype(vec)::value;
+    const int CF = F / VF, RF = NT / CF;
+    const int rF = tid / CF, cF = tid - rF * CF;
+    float sm[VF], sq[VF];
+#pragma unroll
+    for (int e = 0; e < VF; ++e) sm[e] = sq[e] = 0.f;
+    if (rF < RF) {
+      const float* base = src + (i * a.L) * F + cF * VF;
+#pragma unroll FU
+      for (int t = tb + rF; t < te; t += RF) {
+        float v[VF];
+        ldv_nt<VF>(base + static_cast<int64_t>(t) * F, v);
+#pragma unroll
+        for (int e = 0; e < VF; ++e) {
+          sm[e] += v[e];
+          sq[e] = fmaf(v[e], v[e], sq[e]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < VF; ++e) {
+        const int f = rF * F + cF * VF + e;
+        s_red[f] = sm[e];
+        s_red[kRF + f] = sq[e];
+      }
+    }
+    __syncthreads();
+    for (int f = tid; f < F; f += NT) {  // the row slots summed in order
+      float x1 = 0.f, x2 = 0.f;
+      for (int r = 0; r < RF; ++r) {
+        x1 += s_red[r * F + f];
+        x2 += s_red[kRF + r * F + f];
+      }
+      out[f] = x1;
+      out[F + f] = x2;
+    }
+  };
+  if (vis)
+    stream(a.visual, a.Vd, prow + 2 * a.A, std::integral_constant<int, VV>{});
+  else
+    stream(a.audio, a.A, prow, std::integral_constant<int, VA>{});
+}
+
+// The partials of utterance i (blockIdx.x) in part order, then the row's
+// epilogue of utt_stream_kernel: row 0 once for its tokens, x, the s row
+// (fp32, or the fp16 hi / lo planes of s * rs), aux, the column bounds of
+// this workgroup (grid = N <= kCmaxRows rows of cmax_part).  Thread tid owns
+// columns f = tid + NT j (j < kSplitJ) of [num | Sx_e | Sxx_e | frame sums]
+// and walks each kind's parts in order, all kSplitJ loads of a part issued
+// together (a loop over the parts per column was a chain of P dependent L2
+// round trips per column).
+constexpr int kSplitJ = 7;  // ceil((3 * 320 + 4 * 320) / kNT): every partial column
+__global__ __launch_bounds__(kNT) void utt_split_finish_kernel(StreamArgs a, SplitPlan q,
+                                                               const float* __restrict__ part) {
+  constexpr int NT = kNT;
+  extern __shared__ float s_row[];  // s_half: the fp32 row before the split
+  __shared__ float s_m[NT / kWave];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const int64_t i = blockIdx.x;
+  const int K = 2 * (a.D + a.A + a.Vd);
+  const int D3 = 3 * a.D, W = a.D + K;  // text columns; all partial columns
+  const float* pt = part + i * q.Pt * static_cast<int64_t>(q.Wt);
+  const float* pf = part + a.N * q.Pt * static_cast<int64_t>(q.Wt) + i * q.Pf * static_cast<int64_t>(q.Wf);
+  float acc[kSplitJ], sc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < kSplitJ; ++j) acc[j] = 0.f;
+#pragma unroll 2
+  for (int p = 0; p < q.Pt; ++p) {
+    const float* pr = pt + static_cast<int64_t>(p) * q.Wt;
+    float v[kSplitJ], u[4];
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) {
+      const int f = tid + NT * j;
+      v[j] = f < D3 ? pr[f] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) u[c] = pr[D3 + c];  // (a broadcast: every lane the same word)
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) acc[j] += v[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sc[c] += u[c];
+  }
+#pragma unroll 2
+  for (int p = 0; p < q.Pf; ++p) {
+    const float* pr = pf + static_cast<int64_t>(p) * q.Wf - D3;
+    float v[kSplitJ];
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) {
+      const int f = tid + NT * j;
+      v[j] = (f >= D3 && f < W) ? pr[f] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) acc[j] += v[j];
+  }
+  const float cnt = sc[0], sw = sc[1], c0 = sc[2], w0 = sc[3];
+  float cmx0 = 0.f, cmx1 = 0.f, smax = 0.f;
+#pragma unroll
+  for (int j = 0; j < kSplitJ; ++j) {
+    const int f = tid + NT * j;
+    if (f >= W) continue;
+    float v = acc[j];
+    if (f < a.D) {  // the weighted text sum: row 0 once for its c0 tokens (gather mode)
+      const float e0 = (c0 > 0.f) ? a.table[f] : 0.f;
+      v = fmaf(w0, e0, v);
+      const float xf = v / cnt;
+      a.num_out[i * a.D + f] = xf;
+      if (f < NT) cmx0 = bmax(cmx0, fabsf(xf)); else cmx1 = bmax(cmx1, fabsf(xf));
+      continue;
+    }
+    const int g = f - a.D;  // s column
+    if (g < 2 * a.D) {
+      const float e0 = (c0 > 0.f) ? a.table[g < a.D ? g : g - a.D] : 0.f;
+      v = g < a.D ? fmaf(c0, e0, v) : fmaf(c0 * e0, e0, v);
+    }
+    smax = fmaxf(smax, fabsf(v));
+    if (a.s_half) s_row[g] = v; else a.s_out[i * a.Kp + g] = v;
+  }
+  smax = wave_max(smax);
+  if (lane == 0) s_m[wave] = smax;
+  __syncthreads();
+  float m = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / kWave; ++w) m = fmaxf(m, s_m[w]);
+  const float rs = row_scale(m);
+  if (a.s_half) {
+    _Float16* hi = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * static_cast<int64_t>(a.Kp);
+    for (int f = tid; f < a.Kp; f += NT) {
+      const float x = f < K ? s_row[f] * rs : 0.f;
+      const _Float16 h = static_cast<_Float16>(x);
+      hi[f] = h;
+      hi[a.Kp + f] = static_cast<_Float16>(x - static_cast<float>(h));
+    }
+  } else {
+    for (int f = K + tid; f < a.Kp; f += NT) a.s_out[i * a.Kp + f] = 0.f;
+  }
+  if (tid == 0) {
+    if (cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+    a.aux_out[i] = cnt;
+    a.aux_out[a.N + i] = sw;
+    a.aux_out[2 * a.N + i] = rs;
+  }
+  if (a.cmax_part) {
+    float* pr = a.cmax_part + i * a.D;
     if (tid < a.D) pr[tid] = cmx0;
     if (tid + NT < a.D) pr[tid + NT] = cmx1;
   }
@@ -2566,6 +2898,109 @@ extern "C" int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v,
   if (rc != MMB_OK || !s_half) return rc;
   split_rows_kernel<<<static_cast<unsigned>(n), 256, s.Kp * sizeof(float), stream>>>(
       s.s_out, aux_out + 2 * n, s.Kp);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+// Ranges per utterance of the few-long-rows path: about one workgroup per
+// CU in all (3 per range: text, audio, visual), no range under
+// kSplitMinTok frames.  r06 sweep (tools/split_ab.py, graph-timed, POM's
+// real splits): fewer, longer streams win -- valid (100 x 1089) 55.3 / 62.9
+// / 64.8 / 64.8 us at 1 / 2 / 3 / 4 ranges, test (203 x 1357) 126 / 135 /
+// 125 / 145 us; the one-workgroup kernel 89.7 / 134 us; a plain read of the
+// same frame bytes (probe, 512 workgroups) 40.5 / 97 us.
+constexpr int kSplitMinTok = 64;
+static int split_parts(int64_t n, int t, int cus) {
+  if (n <= 0 || t <= 0) return 1;
+  const int64_t want = ceil_div(static_cast<int64_t>(cus), 3 * n);
+  const int64_t cap = std::max<int64_t>(1, t / kSplitMinTok);
+  return static_cast<int>(std::max<int64_t>(1, std::min(want, cap)));
+}
+
+extern "C" int mmb_mm2_stream_split_parts(int64_t n, int t) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+    (void)hipGetLastError();
+    cus = 256;
+  }
+  return split_parts(n, t, cus);
+}
+
+static size_t split_ws_floats(int64_t n, const SplitPlan& q) {
+  return static_cast<size_t>(n) * (static_cast<size_t>(q.Pt) * q.Wt + static_cast<size_t>(q.Pf) * q.Wf);
+}
+
+extern "C" size_t mmb_mm2_stream_split_ws_bytes(int64_t n, int t, int d, int a_, int vd, int parts) {
+  if (n <= 0 || t <= 0 || d <= 0 || a_ <= 0 || vd <= 0) return 0;
+  const int P = parts > 0 ? std::min(parts, t) : mmb_mm2_stream_split_parts(n, t);
+  return split_ws_floats(n, split_plan_of(t, d, a_, vd, P)) * sizeof(float);
+}
+
+template <int VT, int VA, int VV>
+static int launch_split(const StreamArgs& a, const SplitPlan& q, float* part, hipStream_t stream) {
+  const int64_t grid = a.N * (q.Pt + 2 * q.Pf);
+  utt_split_part_kernel<VT, VA, VV><<<static_cast<unsigned>(grid), kNT, 0, stream>>>(a, q, part);
+  MMB_LAUNCH_CHECK();
+  const size_t lds = a.s_half ? static_cast<size_t>(2 * (a.D + a.A + a.Vd)) * sizeof(float) : 0;
+  utt_split_finish_kernel<<<static_cast<unsigned>(a.N), kNT, lds, stream>>>(a, q, part);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+extern "C" int mmb_mm2_stream_split(const int32_t* ids, const float* table, int64_t v,
+                                    const float* wtab32, const float* text_dense,
+                                    const float* emb_dense, const float* w_dense, const float* audio,
+                                    const float* visual, int64_t n, int t, int d, int a_, int vd,
+                                    float* num_out, void* s_out, int s_half, float* aux_out,
+                                    int32_t* flag, uint32_t* colmax, void* colmax_ws, int parts,
+                                    void* ws, size_t ws_bytes, hipStream_t stream) {
+  MMB_REQUIRE(n >= 0 && t > 0 && d > 0 && a_ > 0 && vd > 0 && parts >= 0);
+  MMB_REQUIRE(colmax == nullptr || (colmax_ws != nullptr && d <= 2 * kNT && n <= kCmaxRows));
+  MMB_REQUIRE(audio && visual && num_out && s_out && aux_out && (s_half == 0 || s_half == 1));
+  if (ids) {
+    MMB_REQUIRE(table && v > 0 && (wtab32 || w_dense));
+  } else {
+    MMB_REQUIRE(text_dense && emb_dense && w_dense);
+  }
+  if (n == 0) {
+    if (colmax) {
+      const hipError_t e = static_cast<hipError_t>(zero_words_async(colmax, d, stream));
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return MMB_OK;
+  }
+  const int P = parts > 0 ? std::min(parts, t) : mmb_mm2_stream_split_parts(n, t);
+  const SplitPlan q = split_plan_of(t, d, a_, vd, P);
+  MMB_REQUIRE(ws && ws_bytes >= split_ws_floats(n, q) * sizeof(float));
+  MMB_REQUIRE(n * (q.Pt + 2 * q.Pf) <= (int64_t{1} << 31) - 1);
+  MMB_REQUIRE(3 * d + 2 * a_ + 2 * vd <= kSplitJ * kNT);  // the finish kernel's columns
+  StreamArgs s{};
+  s.cmax_part = colmax ? static_cast<float*>(colmax_ws) : nullptr;
+  s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.w_dense = w_dense;
+  s.text_dense = text_dense; s.emb_dense = emb_dense; s.audio = audio; s.visual = visual;
+  s.N = n; s.L = t; s.D = d; s.A = a_; s.Vd = vd; s.Kp = mmb_mm2_k(d, a_, vd);
+  s.num_out = num_out; s.s_out = static_cast<float*>(s_out); s.aux_out = aux_out; s.flag = flag;
+  s.s_half = s_half;
+  const bool vt = (d % 4 == 0) && (ids ? aligned16(table) : (aligned16(text_dense) && aligned16(emb_dense)));
+  const bool va = (a_ % 4 == 0) && aligned16(audio);
+  const bool vv = (vd % 4 == 0) && aligned16(visual);
+  MMB_REQUIRE(d / (vt ? 4 : 1) <= kNT && a_ / (va ? 4 : 1) <= kNT && vd / (vv ? 4 : 1) <= kNT);
+  float* part = static_cast<float*>(ws);
+  int rc;
+  switch ((vt ? 4 : 0) | (va ? 2 : 0) | (vv ? 1 : 0)) {
+    case 7: rc = launch_split<4, 4, 4>(s, q, part, stream); break;
+    case 6: rc = launch_split<4, 4, 1>(s, q, part, stream); break;
+    case 5: rc = launch_split<4, 1, 4>(s, q, part, stream); break;
+    case 4: rc = launch_split<4, 1, 1>(s, q, part, stream); break;
+    case 3: rc = launch_split<1, 4, 4>(s, q, part, stream); break;
+    case 2: rc = launch_split<1, 4, 1>(s, q, part, stream); break;
+    case 1: rc = launch_split<1, 1, 4>(s, q, part, stream); break;
+    default: rc = launch_split<1, 1, 1>(s, q, part, stream); break;
+  }
+  if (rc != MMB_OK || !colmax) return rc;
+  colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(
+      static_cast<const float*>(colmax_ws), static_cast<int>(n), d, colmax);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

@@ -64,6 +64,10 @@ SIGNATURES = {
     "mmb_mm2_stream": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _I,
                             _P, _P, _P, _P, _P]),
     "mmb_mm2_colmax_ws_bytes": (_S, [_I]),
+    "mmb_mm2_stream_split_parts": (_I, [_L, _I]),
+    "mmb_mm2_stream_split_ws_bytes": (_S, [_L, _I, _I, _I, _I, _I]),
+    "mmb_mm2_stream_split": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P,
+                                  _I, _P, _P, _P, _P, _I, _P, _S, _P]),
     "mmb_mm2_stream_project_supported": (_I, [_I, _I, _I, _I]),
     "mmb_mm2_stream_project": (_I, [_P, _P, _L, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _P, _P,
                                     _P, _P, _P, _P, _P, _P, _P]),

@@ -456,16 +456,32 @@ def ctypes_ptr_array(ptrs):
     return (ctypes.c_void_p * len(ptrs))(*ptrs)
 
 
+def split_parts(n: int, t: int) -> int:
+    """Token / frame ranges per utterance of the few-long-rows stream path
+    (mmb_mm2_stream_split_parts: a text, an audio and a visual workgroup per
+    range, about one workgroup per CU in all)."""
+    return int(L.query("mmb_mm2_stream_split_parts", n, t))
+
+
+def split_ws(n: int, t: int, d: int, a: int, vd: int, device, parts: int = 0) -> torch.Tensor:
+    """Scratch of mmb_mm2_stream_split (its per-range partial rows)."""
+    nb = int(L.query("mmb_mm2_stream_split_ws_bytes", n, t, d, a, vd, parts))
+    return torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
+
+
 def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=None,
                text_dense=None, emb_dense=None, w_dense=None, flag=None, out=None,
-               s_half: bool = True, colmax=None, colmax_ws=None):
+               s_half: bool = True, colmax=None, colmax_ws=None, split=None, parts: int = 0):
     """a6-a8 frame sums.  Returns (x, s, aux): x [n, d] the a2 rows (weighted
     text sum / count_nonzero(w)), aux [3, n] (count, total weight, row scale).
     s_half=True (default) writes s as fp16 [n, 2*kp] (hi | lo planes of the
     row-scaled sums, the x3 projection's A operand); s_half=False writes fp32
     [n, kp] for the fp32-MFMA projection.  With `colmax` ([d] int32) and
     `colmax_ws` (mmb_mm2_colmax_ws_bytes) the kernel also writes the column
-    bounds max_i |x[i, j]| (float bits) for mmb_gram_i8."""
+    bounds max_i |x[i, j]| (float bits) for mmb_gram_i8.  With `split` (a
+    split_ws scratch) every utterance's tokens / frames are cut into `parts`
+    ranges (0: split_parts) summed by their own workgroups, then added in
+    part order (mmb_mm2_stream_split: a few long rows, POM's splits)."""
     kp, _ = mm2_dims(d, a, vd)
     dev = audio.device
     if out is None:
@@ -477,6 +493,13 @@ def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=Non
         raise L.MMBError("s buffer dtype does not match s_half")
     V = table.shape[0] if table is not None else 0
     _check_colmax_ws(colmax_ws, d)
+    if split is not None:
+        L.call("mmb_mm2_stream_split", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32),
+               L.ptr(text_dense), L.ptr(emb_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual),
+               n, t, d, a, vd, L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag),
+               L.ptr(colmax), L.ptr(colmax_ws), int(parts), L.ptr(split),
+               split.numel() * split.element_size(), L.stream_ptr())
+        return num, s, aux
     L.call("mmb_mm2_stream", L.ptr(ids32), L.ptr(table), V, L.ptr(wtab32), L.ptr(text_dense),
            L.ptr(emb_dense), L.ptr(w_dense), L.ptr(audio), L.ptr(visual), n, t, d, a, vd,
            L.ptr(num), L.ptr(s), int(s_half), L.ptr(aux), L.ptr(flag), L.ptr(colmax),
@@ -658,6 +681,10 @@ def side_cu_set(n_cu: int, side: int, layout: str = "balanced") -> list[int]:
 # the int8 Gram pays from tens of thousands of rows up.
 GRAM_I8_MIN_ROWS = 1 << 15
 
+# Steps of at most this many rows fork the projection beside the Gram -> PC
+# solve chain (FusedStep.fork): latency-bound kernels side by side.
+FORK_PROJECTION_MAX_ROWS = 4096
+
 
 class FusedStep:
     """One pass of the north-star hot path over a batch of utterances resident
@@ -700,7 +727,8 @@ class FusedStep:
                  n_total: int | None = None, row0: int = 0, chunks: int | None = None,
                  side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True,
                  gram_kind: str | None = None, stream_project: bool | None = None,
-                 narrow_fused: bool | None = None, check_each_run: bool = False):
+                 narrow_fused: bool | None = None, check_each_run: bool = False,
+                 fork_projection: bool | None = None, split_stream: bool | None = None):
         self.inp = inputs
         self.check_each_run = check_each_run
         self.ids = inputs["ids"]
@@ -780,6 +808,23 @@ class FusedStep:
             self.colmax_ws = torch.empty((nb + 15) // 16 * 16, dtype=torch.uint8, device=dev)
         else:
             self.colmax = self.colmax_ws = None
+        # a few long rows (POM's splits): every utterance's tokens and each
+        # modality's frames on workgroups of their own (mmb_mm2_stream_split),
+        # so 100-203 rows fill the chip instead of one workgroup each
+        self.split = None
+        if split_stream is None:
+            split_stream = True
+        if (split_stream and not self.stream_project and not self.narrow_fused
+                and len(self.bounds) == 1
+                and self.t > 64 and 0 < self.n <= L.cu_count(dev)):
+            self.split = split_ws(self.n, self.t, self.d, self.a, self.vd, dev)
+        # small steps (the dataset splits): the projection runs on a forked
+        # stream beside the Gram -> PC solve chain, and the removal is its own
+        # small launch, instead of the projection waiting for the PC to fuse
+        # the removal into its tail (that saves an HBM pass only at scale)
+        if fork_projection is None:
+            fork_projection = self.n <= FORK_PROJECTION_MAX_ROWS
+        self.fork = torch.cuda.Stream(device=dev) if self.fused_remove and fork_projection else None
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
         self.main = None
@@ -859,7 +904,7 @@ class FusedStep:
                    inp["visual"][r0:r1], ids32=self.ids[r0:r1], table=self.table,
                    wtab32=inp["wtab"], flag=self.flag, s_half=self.s_half,
                    out=(self.x[r0:r1], self.s[r0:r1], self.aux_of(c)),
-                   colmax=self.colmax, colmax_ws=self.colmax_ws)
+                   colmax=self.colmax, colmax_ws=self.colmax_ws, split=self.split)
 
     def _consume_chunk(self, c: int):
         r0, r1 = self.bounds[c]
@@ -904,7 +949,7 @@ class FusedStep:
             self.check()
         return out
 
-    def _run(self, trace):
+    def _run(self, trace, fork: bool = True):
         def mark(name):
             if trace is None:
                 return _NullSpan()
@@ -952,6 +997,29 @@ class FusedStep:
             return self.sif, self.mmb2
         with mark("mm2_stream"):
             self._stream_chunk(0)  # every CU
+        if self.fork is not None:
+            # the projection beside the Gram -> solve chain; with fork=False
+            # (inside a concurrent StepGraph) the same kernels in one stream,
+            # so the rows are the forked step's bit for bit
+            caller = torch.cuda.current_stream(self.table.device)
+            side = self.fork if fork else caller
+            if fork:
+                side.wait_stream(caller)
+            with torch.cuda.stream(side):
+                with mark("mm2_project"):
+                    mm2_project(self.s, self.x, self.aux_of(0), self.proj, out=self.mmb2)
+            with mark("gram"):
+                if self.gram_i8:
+                    gram_i8(self.x, self.colmax, self.G, ws=self.gws)
+                else:
+                    gram(self.x, None, self.G, ws=self.gws)
+            pc = self._solve(trace, mark)
+            with mark("pc_remove"):
+                remove_pc(self.x, None, pc, out=self.sif)
+            if fork:
+                caller.wait_stream(side)
+            self.pc = pc
+            return self.sif, self.mmb2
         if self.fused_remove:
             with mark("gram"):
                 if self.gram_i8:
@@ -1045,10 +1113,17 @@ class StepGraph:
                 self.outs = [st._run(None) for st in self.steps]
             else:
                 self.outs = []
+                # the steps run WITHOUT their forked projection here: the
+                # splits' branches already overlap, and with the forks the
+                # replay ran the branches one after the other (POM's two
+                # splits 0.505 ms concurrent vs 0.503 serial; without 0.436,
+                # r06 tools/pom_graph_ab.py); a fork joined back to its
+                # branch stream also segfaulted the capture
+                # (tools/dbg/fork_graph_probe.py)
                 for st, br in zip(self.steps, self._branches):
                     br.wait_stream(cap)
                     with torch.cuda.stream(br):
-                        self.outs.append(st._run(None))
+                        self.outs.append(st._run(None, fork=False))
                 for br in self._branches:
                     cap.wait_stream(br)
             for i, st in enumerate(self.steps):

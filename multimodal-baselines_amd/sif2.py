@@ -100,16 +100,19 @@ def estimate_embedding_overall_gpu2(data, masks, networks, sentence_weights, emb
                            f"do not match [N={n}, L, D={d}] / [N, L]")
     proj = P.MMB2Projection(networks, d, a, vd, t, dev)
     half = P.x3_supported(proj)
+    # a few long rows (POM's splits): tokens and frames on workgroups of their own
+    split = (P.split_ws(n, t, d, a, vd, dev)
+             if t > 64 and 0 < n <= L.cu_count(dev) else None)
     if emb.shape[1] == t:
         num, s, aux = P.mm2_stream(n, t, d, a, vd, audio, visual, text_dense=text, emb_dense=emb,
-                                   w_dense=sw, s_half=half)
+                                   w_dense=sw, s_half=half, split=split)
     else:
         # L != T: frame sums with zero text weights, then the weighted average
         # of the L rows (a2 over the [N*L, D] rows as a table)
         l = emb.shape[1]
         num, s, aux = P.mm2_stream(n, t, d, a, vd, audio, visual, text_dense=text,
                                    emb_dense=text, w_dense=torch.zeros((n, t), device=dev),
-                                   s_half=half)
+                                   s_half=half, split=split)
         if n * l >= 2 ** 31:
             raise ValueError("N * L must be < 2^31")
         rows = torch.arange(n * l, device=dev, dtype=torch.int32).view(n, l)

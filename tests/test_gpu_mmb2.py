@@ -281,8 +281,8 @@ def test_fused_pc_removal_matches_separate_kernel(gpu, N):
     inp = synth.device_workload(N, T, V, A=300, Vd=300, seed=21, device=gpu)
     torch.manual_seed(0)
     gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
-    fused = P.FusedStep(inp, gen.networks(), stream_project=False)
-    assert fused.fused_remove
+    fused = P.FusedStep(inp, gen.networks(), stream_project=False, fork_projection=False)
+    assert fused.fused_remove and fused.fork is None
     trace = {}
     s1, m1 = [t.clone() for t in fused.run(trace=trace)]
     assert "mm2_project+pc_remove" in trace and "pc_remove" not in trace
