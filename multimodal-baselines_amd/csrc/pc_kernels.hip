@@ -2621,7 +2621,8 @@ constexpr int kPnGu = (kPmMaxT * 256 + kPnPw * kWave - 1) / (kPnPw * kWave);  //
 // ABL (tools build only, timing ablations, results invalid): 1 skips the
 // round's B_{r+1} / W_{r+1} update, 2 skips the round's factor
 template <int ABL = 0>
-__global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __restrict__ G, int D,
+__global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __restrict__ G,
+                                                               const double* __restrict__ G2, int D,
                                                                const double* __restrict__ z0, int k,
                                                                int npc, int n_iter, int transposed,
                                                                double* __restrict__ pc_out,
@@ -2643,18 +2644,25 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   unsigned* ctr = ctl;
   unsigned* abort_w = ctl + 1;
 
-  // this workgroup's 16 rows of G as MFMA A fragments on waves 0-6 (G
-  // symmetric: row p of the tile = column p, 16 consecutive doubles per k-row:
-  // coalesced); wave 7 is free for the k x k factor that overlaps the rest
+  // this workgroup's 16 rows of the round's matrix as MFMA A fragments on
+  // waves 0-6 (symmetric: row p of the tile = column p, 16 consecutive
+  // doubles per k-row: coalesced); wave 7 is free for the k x k factor that
+  // overlaps the rest.  Since r06 the first n_sq = n_iter / 2 rounds multiply
+  // by G2 = G G (gram_square_kernel), each standing for two power
+  // iterations: span(G^7 Z0) is the same span, so the PC is sklearn's to
+  // rounding, with 4 exchange rounds instead of 7; the remaining round(s) and
+  // the tail use G itself
+  const int n_sq = G2 ? n_iter / 2 : 0;
   double ga[kPnKs];
-  {
+  auto load_rows = [&](const double* M) {
     const int p = t * 16 + (lane & 15);
 #pragma unroll
     for (int j = 0; j < kPnKs; ++j) {
       const int q = 4 * (wave + kPnPw * j) + (lane >> 4);
-      ga[j] = (wave < kPnPw && p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
+      ga[j] = (wave < kPnPw && p < D && q < D) ? M[static_cast<int64_t>(q) * D + p] : 0.0;
     }
-  }
+  };
+  load_rows(n_sq > 0 ? G2 : G);
   // waves 0-6: their partial products of this tile of G with a [Dp][16] block
   auto tile_partials = [&](const double* B) {
     if (wave < kPnPw) {
@@ -2795,7 +2803,9 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
 
   int x = 0;  // the exchange
   const int T0 = T, k0 = k;
-  for (int r = 0; r < n_iter; ++r) {
+  const int n_rounds = n_sq + (n_iter - 2 * n_sq);
+  for (int r = 0; r < n_rounds; ++r) {
+    if (r == n_sq && n_sq > 0) load_rows(G);  // G2's rounds done
     {
       // the round's LDS addresses, bounds and per-lane indices are rebuilt
       // from an opaque zero every round: left loop-invariant, the compiler
@@ -2888,6 +2898,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
     PC_MARK(45 + 2 * r);
   }
 
+  if (n_rounds == n_sq && n_sq > 0) load_rows(G);  // (n_iter even: the tail's product is by G)
   // the round entering the tail (r04's): the factor of W beside the partials
   // of G_t B, then the block Z of the tail.  The direct branch's tail is a
   // generalised eigenproblem on span(Z), invariant to the basis, so its block
@@ -2975,6 +2986,50 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   if (__hip_atomic_load(abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
     for (int e = tid; e < npc * D; e += kPnNT) pc_out[e] = __builtin_nan("");
   PC_PROBE_FLUSH();
+}
+
+// G2 = G G for the multi-workgroup solve's squared rounds (r06): one
+// workgroup per upper-triangle 16 x 16 tile (a <= b), its 4 waves splitting
+// the MFMA k-steps (f64 16x16x4) and summed in wave order; each element is
+// written at (i, j) and (j, i) by ONE thread, so G2 is exactly symmetric.
+// ~190 workgroups of ~19 k-steps each: a few microseconds on the whole chip
+// against the ~6.7 us of each exchange round it saves (3 of 7 at n_iter = 7).
+constexpr int kSqNT = 256;
+__global__ __launch_bounds__(kSqNT) void gram_square_kernel(const double* __restrict__ G, int D,
+                                                            double* __restrict__ G2) {
+  __shared__ double part[kSqNT / kWave][256];
+  const int T = (D + 15) / 16;
+  int rem = blockIdx.x, a = 0;  // blockIdx -> (a, b), a <= b, row-major over the upper triangle
+  while (rem >= T - a) {
+    rem -= T - a;
+    ++a;
+  }
+  const int b = a + rem;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int Ks = (D + 3) / 4;
+  const int pa = a * 16 + (lane & 15), pb = b * 16 + (lane & 15);
+  f64x4 acc = {0, 0, 0, 0};
+#pragma unroll 5
+  for (int st = wave; st < Ks; st += kSqNT / kWave) {
+    const int q = 4 * st + (lane >> 4);
+    const bool okq = q < D;
+    // A[i][k] = G[a16 + i][q] = G[q][a16 + i] (symmetric), B[k][j] = G[q][b16 + j]
+    const double x = (okq && pa < D) ? G[static_cast<int64_t>(q) * D + pa] : 0.0;
+    const double y = (okq && pb < D) ? G[static_cast<int64_t>(q) * D + pb] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) part[wave][((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+  __syncthreads();
+  const int e = threadIdx.x, i = e >> 4, j = e & 15;
+  double v = 0.0;
+#pragma unroll
+  for (int w = 0; w < kSqNT / kWave; ++w) v += part[w][e];
+  const int r = a * 16 + i, c = b * 16 + j;
+  if (r < D && c < D && (a != b || i <= j)) {
+    G2[static_cast<int64_t>(r) * D + c] = v;
+    G2[static_cast<int64_t>(c) * D + r] = v;
+  }
 }
 
 inline size_t p16_lds_bytes(int d) {
@@ -3743,7 +3798,9 @@ extern "C" int mmb_pc_solve(const double* g, int d, const double* z0, int k, int
 
 extern "C" size_t mmb_pc_solve_mc_ws_bytes(int d) {
   const int T = (d > 0 ? d : 0) / 16 + 1;
-  return 16 + static_cast<size_t>(2) * T * 512 * sizeof(double);  // control words | tiles
+  const size_t dd = static_cast<size_t>(d > 0 ? d : 0) * (d > 0 ? d : 0);
+  // control words | tiles | G2 (r06: the squared rounds' matrix)
+  return 16 + static_cast<size_t>(2) * T * 512 * sizeof(double) + dd * sizeof(double);
 }
 
 extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
@@ -3755,6 +3812,17 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
   const int T = (d + 15) / 16;
   unsigned* ctl = static_cast<unsigned*>(ws);  // arrival counter, abort word (16-byte block)
   double* xbuf = reinterpret_cast<double*>(static_cast<char*>(ws) + 16);
+  double* g2 = xbuf + static_cast<size_t>(2) * (d / 16 + 1) * 512;  // (mmb_pc_solve_mc_ws_bytes)
+  // squared rounds for the top component only: npc = 2 lost the second
+  // component's last digits (3.4e-9 of the reference's g3b rows against the
+  // 1e-9 bar) -- G2 keeps the dominant directions to rounding, not the
+  // smaller ones the later components live in
+  if (n_iter >= 2 && npc == 1) {
+    gram_square_kernel<<<T * (T + 1) / 2, kSqNT, 0, stream>>>(g, d, g2);
+    MMB_LAUNCH_CHECK();
+  } else {
+    g2 = nullptr;
+  }
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve_mc_kernel<0>),
@@ -3791,12 +3859,12 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
     auto kern = abl == 1 ? pc_solve_mc_kernel<1> : abl == 2 ? pc_solve_mc_kernel<2> : pc_solve_mc_kernel<3>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(p16_lds_bytes(kP16MaxD)));
-    kern<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out, xbuf, ctl, flag);
+    kern<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, d, z0, k, npc, n_iter, transposed, pc_out, xbuf, ctl, flag);
     MMB_LAUNCH_CHECK();
     return MMB_OK;
   }
 #endif
-  pc_solve_mc_kernel<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
+  pc_solve_mc_kernel<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, d, z0, k, npc, n_iter, transposed,
                                                               pc_out, xbuf, ctl, flag);
   MMB_LAUNCH_CHECK();
   return MMB_OK;

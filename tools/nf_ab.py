@@ -27,6 +27,17 @@ def main():
     ap.add_argument("--workload", choices=["mosi", "synthetic"], default="mosi",
                     help="synthetic: the headline configs[3] step (T 40, 3 x 300-d, V 400k)")
     args = ap.parse_args()
+    # the launched instantiation must be in the library's code object: HIP
+    # aborts the process otherwise (r05: libmmb_nf_w12_2_1_4_2.so)
+    import re
+    sys.path.insert(0, os.path.join(ROOT, "tools", "ab_libs"))
+    import symcheck
+    name = os.path.basename(args.lib)
+    m = re.match(r"libmmb_nf_w(\d+)_(\d+)_(\d+)_(\d+)_(\d+)", name)
+    want = (symcheck.narrow_symbol(*map(int, m.groups()[1:])) if m else None)
+    if want and want not in symcheck.device_symbols(os.path.abspath(args.lib)):
+        print(f"{name}: {want} not in its gfx950 code object; not loaded", flush=True)
+        return 2
     mmb_lib.load(os.path.abspath(args.lib))
     import torch
     import models
@@ -69,4 +80,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
