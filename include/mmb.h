@@ -135,6 +135,19 @@ int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n
  * arrival count outside the round's range); pc_out is then NaN and ws must
  * be re-zeroed before the next call.
  * replaces: sif_functions.compute_pc /root/reference/sif_functions.py:58-67 */
+/* The step's status word in one launch: out[0] = flag[0] | (nonfinite_bit if
+ * any of the n values of pc is not finite), flag nullable (0).  What a
+ * checked step (pipeline.FusedStep.status) reads back with one sync; the
+ * eight elementwise torch kernels it replaced were ~40 us of every dataset
+ * split's graph (r06 kernel trace).  A host-side helper of the drop-in's
+ * error behaviour (sif_functions.py:65-67: TruncatedSVD rejects NaN).     */
+int mmb_step_status(const int32_t* flag, const double* pc, int n, int32_t nonfinite_bit,
+                    int32_t* out, hipStream_t stream);
+
+/* (r06) the multi-workgroup solve runs the first n_iter / 2 products by
+ * G2 = G G (one extra launch, gram_square_kernel; npc = 1 only): ws holds
+ * G2 too, so mmb_pc_solve_mc_ws_bytes grew by d * d * 8 bytes (an ABI change:
+ * size ws with this call).                                                  */
 size_t mmb_pc_solve_mc_ws_bytes(int d);
 int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
                     int transposed, double* pc_out, void* ws, int32_t* flag, hipStream_t stream);

@@ -1222,6 +1222,9 @@ __global__ __launch_bounds__(256) void xt_omega_wave_kernel(const TX* __restrict
   double acc[kK];
 #pragma unroll
   for (int j = 0; j < kK; ++j) acc[j] = 0.0;
+  // (unrolled by 4: the rows' loads of 4 iterations in flight together; the
+  // per-lane sum order is unchanged)
+#pragma unroll 4
   for (int64_t n = lane; n < N; n += kWave) {
     const double xv = static_cast<double>(load_x(num, cnt, n, p, D));
 #pragma unroll
@@ -3008,16 +3011,23 @@ __global__ __launch_bounds__(kSqNT) void gram_square_kernel(const double* __rest
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int Ks = (D + 3) / 4;
   const int pa = a * 16 + (lane & 15), pb = b * 16 + (lane & 15);
-  f64x4 acc = {0, 0, 0, 0};
-#pragma unroll 5
-  for (int st = wave; st < Ks; st += kSqNT / kWave) {
+  // every k-step's two operands loaded before the first MFMA (<= 20 k-steps
+  // per wave at D <= 320): the kernel is one round trip of G reads, not one
+  // per k-step group
+  constexpr int kSqKs = (kP16MaxD / 4 + kSqNT / kWave - 1) / (kSqNT / kWave);  // 20
+  double x[kSqKs], y[kSqKs];
+#pragma unroll
+  for (int u = 0; u < kSqKs; ++u) {
+    const int st = wave + (kSqNT / kWave) * u;
     const int q = 4 * st + (lane >> 4);
-    const bool okq = q < D;
+    const bool okq = st < Ks && q < D;
     // A[i][k] = G[a16 + i][q] = G[q][a16 + i] (symmetric), B[k][j] = G[q][b16 + j]
-    const double x = (okq && pa < D) ? G[static_cast<int64_t>(q) * D + pa] : 0.0;
-    const double y = (okq && pb < D) ? G[static_cast<int64_t>(q) * D + pb] : 0.0;
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+    x[u] = (okq && pa < D) ? G[static_cast<int64_t>(q) * D + pa] : 0.0;
+    y[u] = (okq && pb < D) ? G[static_cast<int64_t>(q) * D + pb] : 0.0;
   }
+  f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < kSqKs; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[u], y[u], acc, 0, 0, 0);
 #pragma unroll
   for (int reg = 0; reg < 4; ++reg) part[wave][((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
   __syncthreads();
@@ -3792,6 +3802,23 @@ extern "C" int mmb_pc_solve(const double* g, int d, const double* z0, int k, int
   } else {
     pc_solve_kernel<<<1, kSolveNT, 0, stream>>>(g, d, z0, k, npc, n_iter, transposed, pc_out);
   }
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
+
+__global__ __launch_bounds__(256) void step_status_kernel(const int32_t* __restrict__ flag,
+                                                          const double* __restrict__ pc, int n,
+                                                          int32_t bit, int32_t* __restrict__ out) {
+  bool bad = false;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) bad |= !isfinite(pc[e]);
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) out[0] = (flag ? flag[0] : 0) | (bad ? bit : 0);
+}
+
+extern "C" int mmb_step_status(const int32_t* flag, const double* pc, int n, int32_t nonfinite_bit,
+                               int32_t* out, hipStream_t stream) {
+  MMB_REQUIRE(pc && out && n >= 0);
+  step_status_kernel<<<1, 256, 0, stream>>>(flag, pc, n, nonfinite_bit, out);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

@@ -47,6 +47,7 @@ SIGNATURES = {
     "mmb_xt_omega": (_I, [_P, _P, _L, _I, _P, _I, _P, _P]),
     "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "mmb_pc_solve_mc_ws_bytes": (_S, [_I]),
+    "mmb_step_status": (_I, [_P, _P, _I, _I, _P, _P]),
     "mmb_pc_solve_mc": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "mmb_pc_remove": (_I, [_P, _P, _L, _I, _P, _I, _P, _P, _P]),
     "mmb_gram_f64": (_I, [_P, _L, _I, _P, _I, _P, _P]),

@@ -868,8 +868,13 @@ class FusedStep:
         pc = getattr(self, "pc", None)
         if pc is None:
             return torch.add(flag, 0, out=out)
-        nonfinite = (~torch.isfinite(pc)).any().to(torch.int32)
-        return torch.add(flag, nonfinite * PC_NONFINITE, out=out)
+        if out is None:
+            out = torch.empty(1, dtype=torch.int32, device=flag.device)
+        # one launch (mmb_step_status): eight elementwise torch kernels here
+        # were ~40 us of every dataset split's graph (r06 kernel trace)
+        L.call("mmb_step_status", L.ptr(flag), L.ptr(pc), pc.numel(), PC_NONFINITE, L.ptr(out),
+               L.stream_ptr())
+        return out
 
     def raise_status(self, v: int):
         """check()'s verdict on a status word read back (status())."""

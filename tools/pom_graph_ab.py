@@ -27,6 +27,7 @@ import synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=40)
 ap.add_argument("--dataset", default="pom")
+ap.add_argument("--variants", default="split_fork,split_nofork,nosplit_fork,nosplit_nofork")
 args = ap.parse_args()
 dev = L.require_gpu()
 if args.dataset == "pom":
@@ -42,6 +43,7 @@ variants = {"split_fork": dict(), "split_nofork": dict(fork_projection=False),
             "nosplit_fork": dict(split_stream=False),
             "nosplit_nofork": dict(split_stream=False, fork_projection=False)}
 graphs = {}
+variants = {k: v for k, v in variants.items() if k in args.variants.split(",")}
 for name, kw in variants.items():
     steps = [P.FusedStep(inp, gen.networks(), **kw) for inp in inps]
     graphs[name] = {"each": [P.StepGraph(st) for st in steps],
