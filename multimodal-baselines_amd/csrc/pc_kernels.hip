@@ -2902,21 +2902,93 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   }
 
   if (n_rounds == n_sq && n_sq > 0) load_rows(G);  // (n_iter even: the tail's product is by G)
-  // the round entering the tail (r04's): the factor of W beside the partials
-  // of G_t B, then the block Z of the tail.  The direct branch's tail is a
-  // generalised eigenproblem on span(Z), invariant to the basis, so its block
-  // stays implicit (Y_t = H_t M^T; workgroup 0 forms Z's rows); a failed
-  // pivot (MGS^2) or the transposed branch (an orthonormal Q: CholeskyQR2)
-  // forms explicit rows
-  if (wave == kPnPw) {
-    p16_eq_chol<false>(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);
-  } else {
-    tile_partials(sY);
+  if (!transposed) {
+    // The direct branch's last round (r06) as an implicit round: the RAW
+    // product H_t = G_t B is exchanged beside the factor of W (as in the
+    // loop), and workgroup 0 alone forms Z = B M^T and G Z = H M^T after the
+    // join -- the factor no longer precedes the exchange (r05: factor 5.6 us,
+    // then the Y_t exchange 4.5 us, back to back).  The other workgroups
+    // arrive without waiting; workgroup 0 waits for all T and, once the
+    // factor held, returns the counter to zero.  A failed factor (pivot <= 0)
+    // falls through to the explicit MGS^2 block below with exchange x + 1:
+    // every workgroup is still there (they return only after the join).
+    if (wave == kPnPw) {
+      p16_eq_chol<false>(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);
+    } else {
+      tile_partials(sY);
+      bar_pw();
+      tile_sum(sHt, true);  // H_t^T
+      bar_pw();
+      if (wave == 0) {
+        double* xb = xbuf + static_cast<int64_t>(x & 1) * T * 256;
+        wave_lds_sync();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = lane + kWave * u;
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(xb + t * 256 + e),
+                             __builtin_bit_cast(unsigned long long, sHt[e]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          if (!pm_arrive(ctr, T, x, abort_w, flag)) {
+            s_abort = 1;
+          } else if (t == 0) {
+            if (!pm_wait(ctr, static_cast<unsigned>(T * (x + 1)), abort_w, flag)) s_abort = 1;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          }
+        }
+      }
+    }
+    __syncthreads();  // the join: M, s_fail, the arrival
+    PC_MARK(44 + 2 * n_iter);
+    if (aborted()) return;
+    if (!s_fail) {
+      if (t != 0) return;  // the tail runs on workgroup 0 only
+      if (tid == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      p16_rmul<kPnNW, true>(sY, sM2, part, Dp);  // Z = B M^T (into the scratch block)
+      gather(sZ, x, kPnNT);                        // H as T transposed tiles
+      __syncthreads();
+      for (int tt = wave; tt < T; tt += kPnNW) {  // G Z = H M^T (sY free: B is in Z)
+        f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const int m = 4 * st + (lane >> 4);
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sZ[tt * 256 + m * 16 + (lane & 15)],
+                                                     sM2[m * kP16W + (lane & 15)], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) sY[(tt * 16 + (lane >> 4) + 4 * reg) * kP16W + (lane & 15)] = acc[reg];
+      }
+      __syncthreads();
+      double* zb = part;  // Z into sZ's place, the H tiles' block becomes the scratch
+      part = sZ;
+      sZ = zb;
+      PC_MARK(45 + 2 * n_iter);
+    } else {
+      // the explicit block's exchange follows: no workgroup may arrive at
+      // x + 1 before all T arrived at x (pm_arrive's range check), so the
+      // workgroups that did not wait above wait now
+      if (t != 0 && tid == 0 && !pm_wait(ctr, static_cast<unsigned>(T * (x + 1)), abort_w, flag))
+        s_abort = 1;
+      __syncthreads();
+      if (aborted()) return;
+      ++x;
+    }
   }
-  __syncthreads();
-  PC_MARK(44 + 2 * n_iter);
-  const bool explicit_z = transposed || s_fail;
-  if (explicit_z) {
+  // the transposed branch (an orthonormal Q: CholeskyQR2 rows) and a failed
+  // pivot (MGS^2): explicit rows Z, then the final exchange of Y_t = G_t Z
+  if (transposed || s_fail) {
+    if (transposed) {  // (the direct branch factored above)
+      if (wave == kPnPw) {
+        p16_eq_chol<false>(sW, sL, sLi, sM, sd, k, lane, &s_fail, sM2);
+      } else {
+        tile_partials(sY);
+      }
+      __syncthreads();
+      PC_MARK(44 + 2 * n_iter);
+    }
     if (s_fail) {  // the equilibrated rows, orthonormalised by MGS^2
       for (int e = tid; e < Dp * kP16W; e += kPnNT) {
         const int p = e / kP16W, j = e % kP16W;
@@ -2948,34 +3020,14 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       }
     }
     tile_product(sZ, sYt);  // Y_t = G_t Z
-  } else {
-    tile_sum(sHt, true);  // H_t^T, H_t = G_t B (its partials formed beside the Cholesky)
+    if (wave == 0) publish(sYt, x, true);
+    if (t != 0) return;  // the tail runs on workgroup 0 only
     __syncthreads();
-    if (wave == 0) {  // Y_t = H_t M^T from the transposes (conflict-free reads)
-      f64x4 acc = {0, 0, 0, 0};
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int m = 4 * st + (lane >> 4);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sHt[m * 16 + (lane & 15)], sM2[m * 16 + (lane & 15)],
-                                                   acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) sYt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
-    }
+    PC_MARK(45 + 2 * n_iter);
+    if (aborted()) return;
+    gather(sY, x, kPnNT);  // G Z
+    __syncthreads();
   }
-  if (wave == 0) publish(sYt, x, true);
-  if (t != 0) return;  // the tail runs on workgroup 0 only
-  // workgroup 0 forms Z = B M^T for the tail while wave 0 waits for the
-  // other workgroups' tiles (before r05 the product preceded its publish,
-  // and every workgroup waited for it).  (Keeping B's tiles transposed for
-  // conflict-free A reads here cost the round's update more than it saved:
-  // the transposed stores are the conflicted pattern, r05x.)
-  if (!explicit_z) p16_rmul<kPnNW, true>(sY, sM2, sZ, Dp);
-  __syncthreads();
-  PC_MARK(45 + 2 * n_iter);
-  if (aborted()) return;
-  gather(sY, x, kPnNT);  // G Z
-  __syncthreads();
   // the direct branch's two Grams in one pass: H = (G Z)^T (G Z), W = Z^T G Z
   // (the transposed branch forms its own Q^T G Q in the tail)
   if (!transposed) p16_gram2<kPnNW>(sY, sY, sT, sZ, sY, sW, Dp, k, part);

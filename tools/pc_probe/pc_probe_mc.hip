@@ -51,21 +51,22 @@ int main() {
     (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(mmb::g_pc_probe), sizeof(t));
     auto us = [&](int i, int j) { return (double)(t[j] - t[i]) * 1e3 / rate; };
     printf("rep %d rc %d: kernel+memset %.1f us | gram0 %.1f", rep, rc, ms * 1e3, us(0, 1));
-    // r05 rounds: wave 0's partials + publish + wait, its gather, the join
-    // (wave 15's factor), then B_{r+1} = H M^T and W_{r+1}
+    // rounds (r06: 4 at n_iter = 7, the first three by G2): wave 0's partials
+    // + publish + wait, its gather, the join (the last wave's factor), then
+    // B_{r+1} = H M^T and W_{r+1}
     int prev = 1;
-    for (int r = 0; r < 7; ++r) {
+    for (int r = 0; r < 4; ++r) {
       printf(" | r%d pub+wait %.1f gather %.1f join %.1f rmul+W %.1f", r, us(prev, 2 + 3 * r),
              us(2 + 3 * r, 3 + 3 * r), us(3 + 3 * r, 44 + 2 * r), us(44 + 2 * r, 45 + 2 * r));
       prev = 45 + 2 * r;
     }
-    printf(" | last: chol %.1f Y+pub+wait %.1f", us(prev, 44 + 14), us(44 + 14, 45 + 14));
+    printf(" | last: chol || H pub+wait %.1f Z, gather, GZ %.1f", us(prev, 44 + 14), us(44 + 14, 45 + 14));
     printf(" | tail gather+grams %.1f rr %.1f eig %.1f out %.1f", us(45 + 14, 40), us(40, 41), us(41, 42),
            us(42, 43));
     printf(" | last eq-chol %.2f (equilibrate %.2f factor %.2f substitute %.2f store %.2f)", us(30, 34),
            us(30, 37), us(37, 38), us(38, 39), us(39, 34));
     printf(" | tail chol: factor %.2f substitute %.2f", us(31, 32), us(32, 33));
-    printf(" | r6 rmul+W: tiles %.2f barrier %.2f sum %.2f\n", us(44 + 12, 35), us(35, 36), us(36, 45 + 12));
+    printf(" | r3 rmul+W: tiles %.2f barrier %.2f sum %.2f\n", us(44 + 6, 35), us(35, 36), us(36, 45 + 6));
   }
   int32_t hflag = 0;
   (void)hipMemcpy(&hflag, flag, 4, hipMemcpyDeviceToHost);
