@@ -149,6 +149,16 @@ int mmb_step_status(const int32_t* flag, const double* pc, int n, int32_t nonfin
  * G2 too, so mmb_pc_solve_mc_ws_bytes grew by d * d * 8 bytes (an ABI change:
  * size ws with this call).                                                  */
 size_t mmb_pc_solve_mc_ws_bytes(int d);
+/* The transposed branch (n < d) of mmb_pc_solve_mc from the rows themselves:
+ * z0 = X^T omega [n, k] (x f32 [n, d], the a2 rows) and G2 formed in ONE
+ * launch into ws (which holds both; mmb_pc_solve_mc_ws_bytes), then the
+ * solve -- where mmb_xt_omega + mmb_pc_solve_mc took two launches before
+ * it.  The same z0 (the same per-lane sums) and PC.
+ * replaces: sif_functions.compute_pc for a split of n < d rows
+ *   /root/reference/sif_functions.py:58-67 (sklearn extmath.py:562-566)    */
+int mmb_pc_solve_mc_xt(const double* g, int d, const float* x, int64_t n, const double* omega,
+                       int k, int npc, int n_iter, double* pc_out, void* ws, int32_t* flag,
+                       hipStream_t stream);
 int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
                     int transposed, double* pc_out, void* ws, int32_t* flag, hipStream_t stream);
 
@@ -273,6 +283,26 @@ int mmb_mm2_stream_project(const int32_t* ids, const float* table, int64_t v,
                            int a, int vd, const void* wpieces, const float* c0, float* num_out,
                            float* aux_out, float* mmb2_out, int32_t* flag, uint32_t* colmax,
                            void* colmax_ws, hipStream_t stream);
+
+/* mmb_mm2_project_x3_rmpc for a few rows (the dataset splits: 100-1,284
+ * rows put one or a few workgroups through the whole K loop), split over K:
+ * slices (0: mmb_mm2_project_x3_split_slices) workgroups per 128-row tile
+ * each run a contiguous range of the 32-deep K chunks and write their raw
+ * accumulators to ws (mmb_mm2_project_x3_split_ws_bytes(n, k, slices) bytes,
+ * 16-byte aligned scratch), then one launch sums each tile's slices in slice
+ * order and runs the same row-wise epilogue (ldw = 320, 256 <= d < 320;
+ * other shapes, or one slice, take mmb_mm2_project_x3_rmpc unchanged).  MMB2
+ * and PC-removed rows equal the one-pass kernel's to the f32 order of the K
+ * sum.
+ * replaces: the projections of sif2.estimate_embedding_overall_gpu2
+ *   /root/reference/sif2.py:187-207 at the per-split call sites
+ *   /root/reference/simplesif.py:308-311                                   */
+int mmb_mm2_project_x3_split_slices(int64_t n, int k);
+size_t mmb_mm2_project_x3_split_ws_bytes(int64_t n, int k, int slices);
+int mmb_mm2_project_x3_split(const void* s_split, const float* num, const float* aux,
+                             const void* wsplit, int ldw, const float* c0, int64_t n, int k, int d,
+                             float* out, const double* pc, float* sif_out, int slices, void* ws,
+                             size_t ws_bytes, hipStream_t stream);
 
 /* The fp16 hi/lo split of wm [k, ldw] (mmb_mm2_prepare) in piece order for
  * mmb_mm2_stream_project: each modality's 2 w_m rows [Sx_m | Sxx_m] padded

@@ -808,12 +808,17 @@ __device__ __forceinline__ void x3_row_epilogue(f32x4 (&acc)[NI][NT], float* sac
 // epilogue (accumulators kept live), bit 1 stages A chunk 0 every time
 // (L2-resident A), bit 2 B chunk 0 every time, bit 3 drops the MFMAs (the
 // fragment reads kept live)
-template <int CT, bool ROWEPI, bool PIPE = false, int DIAG = 0>
+// SPLIT (r06, a few rows: POM's 100 / 203-row splits ran the whole K loop on
+// one or two workgroups, ~75 us): workgroup (tile, slice) = (blockIdx.x /
+// nsl, blockIdx.x % nsl) runs chunks [slice * cps, (slice + 1) * cps) of the
+// K loop and writes its raw accumulators to `part` for x3_splitk_finish_kernel.
+template <int CT, bool ROWEPI, bool PIPE = false, int DIAG = 0, bool SPLIT = false>
 __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
     const _Float16* __restrict__ img, const float* __restrict__ col_inv,
     const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
-    const double* __restrict__ pc, float* __restrict__ sif) {
+    const double* __restrict__ pc, float* __restrict__ sif, int nsl = 1, int cps = 0,
+    f32x4* __restrict__ part = nullptr) {
   constexpr int LDW = 64 * CT;
   constexpr int BBUF = x3_bbuf_halves<CT>();
   constexpr int BQ = BBUF * 2 / 16 / kXT;  // 16-byte pieces per thread per B chunk (= CT)
@@ -833,8 +838,12 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   // D[row 4(l>>4)+j][col l&15])
   const int wr = wave >> 2, wc = wave & 3;
   const int lq = lane >> 4, lc = lane & 15;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
-  const int nch = Kp / kXK;
+  const int tile = SPLIT ? static_cast<int>(blockIdx.x) / nsl : static_cast<int>(blockIdx.x);
+  const int slice = SPLIT ? static_cast<int>(blockIdx.x) - tile * nsl : 0;
+  const int64_t n0 = static_cast<int64_t>(tile) * kXM;
+  // this workgroup's chunks [kc0, kc0 + nch) (all of K unless SPLIT)
+  const int kc0 = SPLIT ? slice * cps : 0;
+  const int nch = SPLIT ? min(cps, Kp / kXK - kc0) : Kp / kXK;
 
   // A piece g = q * kXT + tid of a chunk: plane g >> 9, row (g >> 2) & 127,
   // LDS slot position g & 3 <- data slot (g & 3) ^ swz(row); rows past N
@@ -849,7 +858,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   }
   auto stage_a = [&](int c) {
     if ((DIAG & 64) && c >= 3) return;
-    const int cc = (DIAG & 2) ? 0 : min(c, nch - 1);
+    const int cc = (DIAG & 2) ? 0 : kc0 + min(c, nch - 1);
     _Float16* dst = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
 #pragma unroll
     for (int q = 0; q < AQ; ++q)
@@ -857,7 +866,7 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
   };
   auto stage_b = [&](int c) {
     if ((DIAG & 32) && c >= 2) return;
-    const int cc = (DIAG & 4) ? 0 : min(c, nch - 1);
+    const int cc = (DIAG & 4) ? 0 : kc0 + min(c, nch - 1);
     const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
     _Float16* dst = bring + (c & (kXBbuf - 1)) * BBUF;
 #pragma unroll
@@ -1021,6 +1030,17 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int t = 0; t < CT; ++t) asm volatile("" ::"v"(acc[i][t]));
+    return;
+  }
+  if constexpr (SPLIT) {  // the raw accumulators as rows [kXM][LDW] (16 lanes: 64 contiguous bytes)
+    float* pw = reinterpret_cast<float*>(part) + static_cast<int64_t>(blockIdx.x) * kXM * LDW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pw[(wr * 64 + 16 * i + 4 * lq + j) * LDW + (wc * CT + t) * 16 + lc] = acc[i][t][j];
     return;
   }
 
@@ -1549,6 +1569,99 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3e_kernel(
 template <int CT>
 constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(float); }
 
+// The split-K slices' rows, one wave per row (blockIdx.x * 4 + wave): the
+// slices' raw accumulator rows [kXM][320] summed in slice order (every
+// slice's two float4 columns of a lane in flight together), then the row-wise
+// epilogue's arithmetic of x3_row_epilogue on the same lane columns (4 l..,
+// 256 + 4 l..) in the same order -- so the fused PC removal's rows are the
+// one-pass kernel's bit for bit and the MMB2 rows differ only by the K sum's
+// f32 order.  (The 64-row pass of x3_row_epilogue itself ran ~23 us per 64
+// rows on one workgroup: its staging barriers and dependent loads, which a
+// full chip of tiles hides and two workgroups do not.)
+constexpr int kXSplitMax = 16;  // slices the finish sums (the launcher's cap)
+__global__ __launch_bounds__(256) void x3_splitk_rows_kernel(
+    const float* __restrict__ part, int nsl, const float* __restrict__ num,
+    const float* __restrict__ aux, const float* __restrict__ col_inv, const float* __restrict__ c0,
+    int64_t N, int D, float* __restrict__ out, const double* __restrict__ pc, float* __restrict__ sif) {
+  constexpr int LDW = 320;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int64_t tile = row / kXM;
+  const int rl = static_cast<int>(row - tile * kXM);
+  const int U = D >> 2;
+  const bool u1 = lane + 64 < U;
+  const int c0a = 4 * lane, c1a = 256 + 4 * min(lane, 15);
+  const int c0x = 4 * min(lane, U - 1), c1x = 4 * min(lane + 64, U - 1);
+  f32x4 v0[kXSplitMax], v1[kXSplitMax];
+  const float* pr = part + (tile * nsl * kXM + rl) * LDW;
+#pragma unroll
+  for (int sl = 0; sl < kXSplitMax; ++sl) {
+    const float* q = pr + static_cast<int64_t>(min(sl, nsl - 1)) * kXM * LDW;
+    v0[sl] = *reinterpret_cast<const f32x4*>(q + c0a);
+    v1[sl] = *reinterpret_cast<const f32x4*>(q + c1a);
+  }
+  const float4 xa = *reinterpret_cast<const float4*>(num + row * D + c0x);
+  const float4 xb = *reinterpret_cast<const float4*>(num + row * D + c1x);
+  const float cn = aux[row], tw = aux[N + row];
+  const float irs = 1.f / aux[2 * N + row];
+  const int cA = min(c0a, LDW - 4), cB = c1a;
+  const float civ[8] = {col_inv[cA], col_inv[cA + 1], col_inv[cA + 2], col_inv[cA + 3],
+                        col_inv[cB], col_inv[cB + 1], col_inv[cB + 2], col_inv[cB + 3]};
+  const float cav[8] = {c0[cA], c0[cA + 1], c0[cA + 2], c0[cA + 3], c0[cB], c0[cB + 1], c0[cB + 2], c0[cB + 3]};
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sl = 0; sl < kXSplitMax; ++sl) {
+    if (sl < nsl) {
+      s0 += v0[sl];
+      s1 += v1[sl];
+    }
+  }
+  const float av[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+  float y[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = (e < 4 ? c0a : 256 + 4 * lane) + (e & 3);
+    const bool in = e < 4 ? lane < U : u1;
+    const float add = (in && col < D) ? text_sum(xv[e], cn) : (col == D ? tw : 0.f);
+    y[e] = av[e] * (civ[e] * irs) + add + cav[e];
+  }
+  const int lane_tot = (D - 256) >> 2, e_tot = (D - 256) & 3;  // column D in unit 1
+  const float ysel = e_tot == 0 ? y[4] : e_tot == 1 ? y[5] : e_tot == 2 ? y[6] : y[7];
+  const float tot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ysel), lane_tot));
+  const float rt = 1.f / tot;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const bool in = e < 4 ? lane < U : u1;
+    y[e] *= rt;
+    if (in) ss = fmaf(y[e], y[e], ss);
+  }
+  const float inv = 1.f / sqrtf(wave_sum_dpp_f32(ss));
+  float* orow = out + row * D;
+  if (lane < U) *reinterpret_cast<float4*>(orow + c0x) = make_float4(y[0] * inv, y[1] * inv, y[2] * inv, y[3] * inv);
+  if (u1) *reinterpret_cast<float4*>(orow + c1x) = make_float4(y[4] * inv, y[5] * inv, y[6] * inv, y[7] * inv);
+  if (pc) {
+    double pv[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pv[e] = lane < U ? pc[c0x + e] : 0.0;
+      pv[4 + e] = u1 ? pc[c1x + e] : 0.0;
+    }
+    double dot = 0.0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dot = fma(static_cast<double>(xv[e]), pv[e], dot);
+    dot = wave_sum_dpp(dot);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = static_cast<float>(static_cast<double>(xv[e]) - dot * pv[e]);
+    float* srow = sif + row * D;
+    if (lane < U) *reinterpret_cast<float4*>(srow + c0x) = make_float4(o[0], o[1], o[2], o[3]);
+    if (u1) *reinterpret_cast<float4*>(srow + c1x) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
 // Projection kernel variant: 0 = 32x32x16 MFMA tiles (wave = 32 rows x 32 CT
 // columns), 1 = 16x16x32 tiles (wave = 64 rows x 16 CT columns: 18 instead of
 // 24 fragment reads per chunk), 2 = the 16x16x32 kernel with the
@@ -1866,6 +1979,67 @@ extern "C" int mmb_mm2_project_x3_rmpc(const void* s_split, const float* num, co
     case 5: return launch_project_x3<5>(s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, stream);
     default: return MMB_EINVAL;  // d >= 320: the chunk rings exceed the 160 KB LDS
   }
+}
+
+// split-K plan of the x3 projection for a few rows (r06): about one
+// workgroup per 4 CUs in all, at least 4 chunks per slice; 1 = no split
+// (the row tiles alone fill the chip, or K is short).  Only the row-wise
+// epilogue's shapes (ldw = 320, 256 <= d < 320) split.
+static int x3_split_slices(int64_t n, int k, int cus) {
+  const int64_t tiles = ceil_div(n, kXM);
+  const int nch = k / kXK;
+  const int64_t want = cus / (4 * std::max<int64_t>(1, tiles));
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({want, nch / 4, kXSplitMax})));
+}
+
+extern "C" int mmb_mm2_project_x3_split_slices(int64_t n, int k) {
+  return x3_split_slices(n, k, stream_cu_count(nullptr));
+}
+
+extern "C" size_t mmb_mm2_project_x3_split_ws_bytes(int64_t n, int k, int slices) {
+  if (n <= 0 || k < kXK) return 0;
+  const int nsl = slices > 0 ? slices : mmb_mm2_project_x3_split_slices(n, k);
+  return static_cast<size_t>(ceil_div(n, kXM)) * nsl * kXM * 320 * sizeof(float);
+}
+
+extern "C" int mmb_mm2_project_x3_split(const void* s_split, const float* num, const float* aux,
+                                        const void* wsplit, int ldw, const float* c0, int64_t n,
+                                        int k, int d, float* out, const double* pc, float* sif_out,
+                                        int slices, void* ws, size_t ws_bytes, hipStream_t stream) {
+  MMB_REQUIRE(slices >= 0);
+  const int nsl = slices > 0 ? std::min({slices, std::max(1, k / kXK), kXSplitMax})
+                             : mmb_mm2_project_x3_split_slices(n, k);
+  auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool rowepi = ldw == 320 && ldw == mmb_mm2_ldw(d) && d >= 256 && d % 4 == 0 && a16(num) &&
+                      a16(out) && (sif_out == nullptr || a16(sif_out));
+  if (nsl < 2 || !rowepi || n <= 0)  // nothing to split: the one-pass kernel
+    return mmb_mm2_project_x3_rmpc(s_split, num, aux, wsplit, ldw, c0, n, k, d, out, pc, sif_out, stream);
+  MMB_REQUIRE(s_split && num && aux && wsplit && c0 && out && k % 32 == 0 && k >= 32);
+  MMB_REQUIRE((pc == nullptr) == (sif_out == nullptr));
+  MMB_REQUIRE(a16(s_split) && a16(wsplit) && a16(ws));
+  const int64_t tiles = ceil_div(n, kXM);
+  MMB_REQUIRE(ws && ws_bytes >= static_cast<size_t>(tiles) * nsl * kXM * 320 * sizeof(float));
+  MMB_REQUIRE(tiles * nsl <= (int64_t{1} << 31) - 1);
+  const _Float16* s = static_cast<const _Float16*>(s_split);
+  const _Float16* img = static_cast<const _Float16*>(wsplit);
+  const float* ci = reinterpret_cast<const float*>(img + 2 * static_cast<size_t>(ldw) * k);
+  constexpr size_t ldsb = x3b_lds_bytes<5>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<5, true, true, 0, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
+    attr = true;
+  }
+  const int cps = static_cast<int>(ceil_div(k / kXK, nsl));  // chunks per slice
+  const int nse = static_cast<int>(ceil_div(k / kXK, cps));   // slices holding >= 1 chunk (<= nsl)
+  f32x4* part = static_cast<f32x4*>(ws);
+  mm2_project_x3b_kernel<5, true, true, 0, true><<<static_cast<unsigned>(tiles * nse), kXT, ldsb, stream>>>(
+      s, num, aux, img, ci, c0, n, k, d, out, pc, sif_out, nse, cps, part);
+  MMB_LAUNCH_CHECK();
+  x3_splitk_rows_kernel<<<static_cast<unsigned>(ceil_div(n, 4)), 256, 0, stream>>>(
+      reinterpret_cast<const float*>(part), nse, num, aux, ci, c0, n, d, out, pc, sif_out);
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
 }
 
 extern "C" int mmb_mm2_project_x3(const void* s_split, const float* num, const float* aux,

@@ -1208,36 +1208,55 @@ __global__ void xt_omega_kernel(const TX* __restrict__ num, const float* __restr
 // columns (every load of a lane independent), then a fixed-order DPP wave sum
 // per column.  The thread-per-output kernel above walked all N rows as one
 // dependent chain of loads: 59 us for a 229-row split (r04 dataset_splits).
-constexpr int64_t kXtOmegaWaveMaxN = 4096;  // rows up to which the launchers pick it
-template <typename TX>
+// X^T Omega for the transposed branch's small splits (N < d rows, k <= 16)
+// on the f64 matrix pipe: workgroup `blk` owns the 16-feature tile blk of z0
+// (all k <= 16 columns: one 16x16 output tile), its 4 waves split the N / 4
+// MFMA k-steps (v_mfma_f64_16x16x4f64, A = X^T rows, B = Omega rows; every
+// k-step's operands loaded before the first MFMA) and their sums are added in
+// wave order.  (r05's wave per feature read 64 rows per load instruction and
+// chained its iterations: 5 / 11 us at 100 / 203 rows, r06 kernel trace; a
+// lane-per-feature loop over the rows with Omega in LDS measured 31 us.)
+constexpr int kXtK = 16;
+constexpr int kXtMaxN = 320;  // rows (the branch has N < d <= 320)
+template <typename TX, bool CNT>
+__device__ __forceinline__ void xt_omega_wave_body(const TX* __restrict__ num, const float* __restrict__ cnt,
+                                                   int64_t N, int D, const double* __restrict__ om, int k,
+                                                   double* __restrict__ z0, int blk) {
+  __shared__ double s_part[4][256];
+  constexpr int kS = (kXtMaxN / 4 + 3) / 4;  // k-steps per wave (20)
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int n_ = static_cast<int>(N);
+  const int p = blk * 16 + (lane & 15), j = lane & 15;
+  double xa[kS], ob[kS];
+#pragma unroll
+  for (int u = 0; u < kS; ++u) {
+    const int n = 4 * (wave + 4 * u) + (lane >> 4);
+    const bool ok = n < n_;
+    xa[u] = (ok && p < D) ? static_cast<double>(CNT ? load_x(num, cnt, n, p, D)
+                                                    : num[static_cast<int64_t>(n) * D + p])
+                          : 0.0;
+    ob[u] = (ok && j < k) ? om[static_cast<int64_t>(n) * k + j] : 0.0;
+  }
+  f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < kS; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[u], ob[u], acc, 0, 0, 0);
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) s_part[wave][((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+  __syncthreads();
+  const int e = threadIdx.x;
+  if (e < 256) {
+    const double v = s_part[0][e] + s_part[1][e] + s_part[2][e] + s_part[3][e];
+    const int pr = blk * 16 + (e >> 4), jc = e & 15;
+    if (pr < D && jc < k) z0[pr * k + jc] = v;
+  }
+}
+template <typename TX, bool CNT = false>
 __global__ __launch_bounds__(256) void xt_omega_wave_kernel(const TX* __restrict__ num,
                                                             const float* __restrict__ cnt,
                                                             int64_t N, int D,
                                                             const double* __restrict__ om, int k,
                                                             double* __restrict__ z0) {
-  constexpr int kK = 16;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int p = blockIdx.x * (blockDim.x / kWave) + static_cast<int>(threadIdx.x / kWave);
-  if (p >= D) return;
-  double acc[kK];
-#pragma unroll
-  for (int j = 0; j < kK; ++j) acc[j] = 0.0;
-  // (unrolled by 4: the rows' loads of 4 iterations in flight together; the
-  // per-lane sum order is unchanged)
-#pragma unroll 4
-  for (int64_t n = lane; n < N; n += kWave) {
-    const double xv = static_cast<double>(load_x(num, cnt, n, p, D));
-#pragma unroll
-    for (int j = 0; j < kK; ++j)
-      if (j < k) acc[j] = fma(xv, om[n * k + j], acc[j]);
-  }
-#pragma unroll
-  for (int j = 0; j < kK; ++j) {
-    if (j < k) {
-      const double s = wave_sum_dpp(acc[j]);
-      if (lane == 0) z0[p * k + j] = s;
-    }
-  }
+  xt_omega_wave_body<TX, CNT>(num, cnt, N, D, om, k, z0, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ pc_solve
@@ -3050,11 +3069,11 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
 // ~190 workgroups of ~19 k-steps each: a few microseconds on the whole chip
 // against the ~6.7 us of each exchange round it saves (3 of 7 at n_iter = 7).
 constexpr int kSqNT = 256;
-__global__ __launch_bounds__(kSqNT) void gram_square_kernel(const double* __restrict__ G, int D,
-                                                            double* __restrict__ G2) {
+__device__ __forceinline__ void gram_square_tile(const double* __restrict__ G, int D,
+                                                 double* __restrict__ G2, int blk) {
   __shared__ double part[kSqNT / kWave][256];
   const int T = (D + 15) / 16;
-  int rem = blockIdx.x, a = 0;  // blockIdx -> (a, b), a <= b, row-major over the upper triangle
+  int rem = blk, a = 0;  // blk -> (a, b), a <= b, row-major over the upper triangle
   while (rem >= T - a) {
     rem -= T - a;
     ++a;
@@ -3092,6 +3111,27 @@ __global__ __launch_bounds__(kSqNT) void gram_square_kernel(const double* __rest
     G2[static_cast<int64_t>(r) * D + c] = v;
     G2[static_cast<int64_t>(c) * D + r] = v;
   }
+}
+__global__ __launch_bounds__(kSqNT) void gram_square_kernel(const double* __restrict__ G, int D,
+                                                            double* __restrict__ G2) {
+  gram_square_tile(G, D, G2, blockIdx.x);
+}
+
+// The transposed branch's start in ONE launch (r06): workgroups [0, nsq)
+// square G (gram_square_tile), the next ceil(D / 4) form z0 = X^T Omega_n
+// (xt_omega_wave_kernel's body: one wave per feature).  Two launches of ~5
+// and ~11 us back to back before the solve of every dataset split (POM's
+// and MOSI's small ones: n < d).
+__global__ __launch_bounds__(kSqNT) void pc_prep_kernel(const double* __restrict__ G, int D,
+                                                        double* __restrict__ G2, int nsq,
+                                                        const float* __restrict__ X, int64_t N,
+                                                        const double* __restrict__ om, int k,
+                                                        double* __restrict__ z0) {
+  if (static_cast<int>(blockIdx.x) < nsq) {
+    gram_square_tile(G, D, G2, blockIdx.x);
+    return;
+  }
+  xt_omega_wave_body<float, false>(X, nullptr, N, D, om, k, z0, static_cast<int>(blockIdx.x) - nsq);
 }
 
 inline size_t p16_lds_bytes(int d) {
@@ -3829,8 +3869,10 @@ extern "C" int mmb_xt_omega(const float* num, const float* cnt, int64_t n, int d
   MMB_REQUIRE(num && omega && z0 && n >= 0 && d > 0 && k > 0);
   // the wave kernel is for the transposed branch's small splits: at large N
   // each of its d waves would re-read all of Omega (N x k)
-  if (k <= 16 && n <= kXtOmegaWaveMaxN)  // (the solver's k = npc + 10 <= 16)
-    xt_omega_wave_kernel<float><<<static_cast<int>(ceil_div(d, 4)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
+  if (k <= kXtK && n <= kXtMaxN && cnt)  // (the solver's k = npc + 10 <= 16)
+    xt_omega_wave_kernel<float, true><<<static_cast<int>(ceil_div(d, 16)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
+  else if (k <= kXtK && n <= kXtMaxN)
+    xt_omega_wave_kernel<float><<<static_cast<int>(ceil_div(d, 16)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
   else
     xt_omega_kernel<float><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(num, cnt, n, d, omega, k, z0);
   MMB_LAUNCH_CHECK();
@@ -3878,9 +3920,21 @@ extern "C" int mmb_step_status(const int32_t* flag, const double* pc, int n, int
 extern "C" size_t mmb_pc_solve_mc_ws_bytes(int d) {
   const int T = (d > 0 ? d : 0) / 16 + 1;
   const size_t dd = static_cast<size_t>(d > 0 ? d : 0) * (d > 0 ? d : 0);
-  // control words | tiles | G2 (r06: the squared rounds' matrix)
-  return 16 + static_cast<size_t>(2) * T * 512 * sizeof(double) + dd * sizeof(double);
+  // control words | tiles | G2 (r06: the squared rounds' matrix) | z0
+  // (mmb_pc_solve_mc_xt: X^T Omega, d x 16)
+  return 16 + static_cast<size_t>(2) * T * 512 * sizeof(double) + dd * sizeof(double) +
+         static_cast<size_t>(d > 0 ? d : 0) * kP16W * sizeof(double);
 }
+
+// squared rounds for the top component only: npc = 2 lost the second
+// component's last digits (3.4e-9 of the reference's g3b rows against the
+// 1e-9 bar) -- G2 keeps the dominant directions to rounding, not the smaller
+// ones the later components live in
+static bool solve_squares(int npc, int n_iter) { return n_iter >= 2 && npc == 1; }
+
+static int launch_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
+                           int transposed, double* pc_out, void* ws, int32_t* flag, bool g2_ready,
+                           hipStream_t stream);
 
 extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
                                int transposed, double* pc_out, void* ws, int32_t* flag,
@@ -3888,19 +3942,37 @@ extern "C" int mmb_pc_solve_mc(const double* g, int d, const double* z0, int k, 
   MMB_REQUIRE(g && z0 && pc_out && ws && d > 1 && d <= kP16MaxD && k >= 1 && k <= kP16W);
   MMB_REQUIRE(npc >= 1 && npc <= k && n_iter >= 0);
   MMB_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0);
+  return launch_solve_mc(g, d, z0, k, npc, n_iter, transposed, pc_out, ws, flag, false, stream);
+}
+
+extern "C" int mmb_pc_solve_mc_xt(const double* g, int d, const float* x, int64_t n,
+                                  const double* omega, int k, int npc, int n_iter, double* pc_out,
+                                  void* ws, int32_t* flag, hipStream_t stream) {
+  MMB_REQUIRE(g && x && omega && pc_out && ws && d > 1 && d <= kP16MaxD && k >= 1 && k <= kP16W);
+  MMB_REQUIRE(n >= 1 && n < d && n <= kXtMaxN && npc >= 1 && npc <= k && n_iter >= 0);
+  MMB_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0);
+  const int T = (d + 15) / 16;
+  double* g2 = reinterpret_cast<double*>(static_cast<char*>(ws) + 16) + static_cast<size_t>(2) * (d / 16 + 1) * 512;
+  double* z0 = g2 + static_cast<size_t>(d) * d;
+  const int nsq = solve_squares(npc, n_iter) ? T * (T + 1) / 2 : 0;
+  pc_prep_kernel<<<nsq + static_cast<int>(ceil_div(d, 16)), kSqNT, 0, stream>>>(
+      g, d, g2, nsq, x, n, omega, k, z0);
+  MMB_LAUNCH_CHECK();
+  return launch_solve_mc(g, d, z0, k, npc, n_iter, 1, pc_out, ws, flag, true, stream);
+}
+
+static int launch_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
+                           int transposed, double* pc_out, void* ws, int32_t* flag, bool g2_ready,
+                           hipStream_t stream) {
   const int T = (d + 15) / 16;
   unsigned* ctl = static_cast<unsigned*>(ws);  // arrival counter, abort word (16-byte block)
   double* xbuf = reinterpret_cast<double*>(static_cast<char*>(ws) + 16);
   double* g2 = xbuf + static_cast<size_t>(2) * (d / 16 + 1) * 512;  // (mmb_pc_solve_mc_ws_bytes)
-  // squared rounds for the top component only: npc = 2 lost the second
-  // component's last digits (3.4e-9 of the reference's g3b rows against the
-  // 1e-9 bar) -- G2 keeps the dominant directions to rounding, not the
-  // smaller ones the later components live in
-  if (n_iter >= 2 && npc == 1) {
+  if (!solve_squares(npc, n_iter)) {
+    g2 = nullptr;
+  } else if (!g2_ready) {
     gram_square_kernel<<<T * (T + 1) / 2, kSqNT, 0, stream>>>(g, d, g2);
     MMB_LAUNCH_CHECK();
-  } else {
-    g2 = nullptr;
   }
   static bool attr = false;
   if (!attr) {
@@ -4015,8 +4087,8 @@ extern "C" int mmb_gram_f64(const double* x, int64_t n, int d, double* g, int ac
 extern "C" int mmb_xt_omega_f64(const double* x, int64_t n, int d, const double* omega, int k,
                                 double* z0, hipStream_t stream) {
   MMB_REQUIRE(x && omega && z0 && n >= 0 && d > 0 && k > 0);
-  if (k <= 16 && n <= kXtOmegaWaveMaxN)
-    xt_omega_wave_kernel<double><<<static_cast<int>(ceil_div(d, 4)), 256, 0, stream>>>(x, nullptr, n, d, omega, k, z0);
+  if (k <= kXtK && n <= kXtMaxN)
+    xt_omega_wave_kernel<double><<<static_cast<int>(ceil_div(d, 16)), 256, 0, stream>>>(x, nullptr, n, d, omega, k, z0);
   else
     xt_omega_kernel<double><<<static_cast<int>(ceil_div(static_cast<int64_t>(d) * k, 256)), 256, 0, stream>>>(
         x, nullptr, n, d, omega, k, z0);

@@ -48,6 +48,7 @@ SIGNATURES = {
     "mmb_pc_solve": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "mmb_pc_solve_mc_ws_bytes": (_S, [_I]),
     "mmb_step_status": (_I, [_P, _P, _I, _I, _P, _P]),
+    "mmb_pc_solve_mc_xt": (_I, [_P, _I, _P, _L, _P, _I, _I, _I, _P, _P, _P, _P]),
     "mmb_pc_solve_mc": (_I, [_P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "mmb_pc_remove": (_I, [_P, _P, _L, _I, _P, _I, _P, _P, _P]),
     "mmb_gram_f64": (_I, [_P, _L, _I, _P, _I, _P, _P]),
@@ -84,6 +85,10 @@ SIGNATURES = {
     "mmb_mm2_project": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
     "mmb_mm2_project_x3": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P]),
     "mmb_mm2_project_x3_rmpc": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P, _P, _P]),
+    "mmb_mm2_project_x3_split_slices": (_I, [_L, _I]),
+    "mmb_mm2_project_x3_split_ws_bytes": (_S, [_L, _I, _I]),
+    "mmb_mm2_project_x3_split": (_I, [_P, _P, _P, _P, _I, _P, _L, _I, _I, _P, _P, _P, _I, _P, _S,
+                                      _P]),
     "mmb_mlp_forward": (_I, [_P, _P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_eval": (_I, [_P, _P, _P, _L, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmb_mlp_forward_train": (_I, [_P, _L, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),

@@ -599,14 +599,31 @@ def x3_supported(proj: "MMB2Projection") -> bool:
     return proj.ldw <= 320
 
 
-def mm2_project(s, num, aux, proj: MMB2Projection, out=None, pc=None, sif_out=None):
+def project_split_ws(n: int, kp: int, device, slices: int = 0):
+    """Scratch of the split-K projection (mmb_mm2_project_x3_split), or None
+    where the rows alone fill the chip (one slice)."""
+    if int(L.query("mmb_mm2_project_x3_split_slices", n, kp)) < 2 and slices < 2:
+        return None
+    nb = int(L.query("mmb_mm2_project_x3_split_ws_bytes", n, kp, slices))
+    return torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
+
+
+def mm2_project(s, num, aux, proj: MMB2Projection, out=None, pc=None, sif_out=None, split=None,
+                slices: int = 0):
     """fp16 s (s_half stream output): the fp16 hi/lo split MFMA GEMM
     (mmb_mm2_project_x3); fp32 s: the fp32-MFMA GEMM.  Same epilogue.
     With `pc` ([1, D] f64) and `sif_out` the x3 kernel also writes the
-    PC-removed a2 rows (mmb_mm2_project_x3_rmpc, fp16 s only)."""
+    PC-removed a2 rows (mmb_mm2_project_x3_rmpc, fp16 s only).  With `split`
+    (project_split_ws) a few rows' K loop runs over several workgroups per
+    row tile (mmb_mm2_project_x3_split, fp16 s)."""
     n = num.shape[0]
     if out is None:
         out = torch.empty((n, proj.d), dtype=torch.float32, device=num.device)
+    if split is not None and s.dtype == torch.float16:
+        L.call("mmb_mm2_project_x3_split", L.ptr(s), L.ptr(num), L.ptr(aux), L.ptr(proj.wsplit),
+               proj.ldw, L.ptr(proj.c0), n, proj.kp, proj.d, L.ptr(out), L.ptr(pc),
+               L.ptr(sif_out), int(slices), L.ptr(split), split.numel(), L.stream_ptr())
+        return out
     if pc is not None:
         if s.dtype != torch.float16 or pc.shape[0] != 1 or sif_out is None:
             raise L.MMBError("fused PC removal needs fp16 s, npc = 1 and sif_out")
@@ -825,6 +842,9 @@ class FusedStep:
         if fork_projection is None:
             fork_projection = self.n <= FORK_PROJECTION_MAX_ROWS
         self.fork = torch.cuda.Stream(device=dev) if self.fused_remove and fork_projection else None
+        # a few rows: the projection's K loop split over workgroups
+        self.proj_split = (project_split_ws(self.n, kp, dev)
+                           if self.s is not None and self.s_half and len(self.bounds) == 1 else None)
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
         self.main = None
@@ -914,7 +934,8 @@ class FusedStep:
     def _consume_chunk(self, c: int):
         r0, r1 = self.bounds[c]
         aux = self.aux_of(c)
-        mm2_project(self.s[r0:r1], self.x[r0:r1], aux, self.proj, out=self.mmb2[r0:r1])
+        mm2_project(self.s[r0:r1], self.x[r0:r1], aux, self.proj, out=self.mmb2[r0:r1],
+                    split=self.proj_split)  # (None past one chunk)
         if self.gram_parts:
             L.call("mmb_gram_part", L.ptr(self.x[r0:r1]), None, r1 - r0,
                    self.step_rows, self.d, int(c > 0), L.ptr(self.gws.buf), L.stream_ptr())
@@ -926,6 +947,16 @@ class FusedStep:
     def _solve(self, trace, mark):
         """G (this rank's rows) -> pc: Omega, RCCL all-reduce of G, the solve."""
         d, k = self.d, self.npc + N_OVERSAMPLES
+        if (self.n_total < d and self.allreduce is None and self.solve_ws is not None
+                and k <= 16):
+            # the transposed branch, unsharded: X^T Omega and the squared
+            # matrix in one launch in front of the solve (mmb_pc_solve_mc_xt)
+            om = omega(self.n_total, k, self.table.device)
+            with mark("pc_solve"):
+                L.call("mmb_pc_solve_mc_xt", L.ptr(self.G), d, L.ptr(self.x), self.n, L.ptr(om), k,
+                       self.npc, N_ITER, L.ptr(self.pc_buf), L.ptr(self.solve_ws), L.ptr(self.flag),
+                       L.stream_ptr())
+            return self.pc_buf
         with mark("pc_start"):
             if self.n_total >= d:
                 z0, transposed = omega(d, k, self.table.device), False
@@ -1012,7 +1043,8 @@ class FusedStep:
                 side.wait_stream(caller)
             with torch.cuda.stream(side):
                 with mark("mm2_project"):
-                    mm2_project(self.s, self.x, self.aux_of(0), self.proj, out=self.mmb2)
+                    mm2_project(self.s, self.x, self.aux_of(0), self.proj, out=self.mmb2,
+                                split=self.proj_split)
             with mark("gram"):
                 if self.gram_i8:
                     gram_i8(self.x, self.colmax, self.G, ws=self.gws)
@@ -1034,7 +1066,7 @@ class FusedStep:
             pc = self._solve(trace, mark)
             with mark("mm2_project+pc_remove"):
                 mm2_project(self.s, self.x, self.aux_of(0), self.proj, out=self.mmb2, pc=pc,
-                            sif_out=self.sif)
+                            sif_out=self.sif, split=self.proj_split)
             self.pc = pc
             return self.sif, self.mmb2
         if nb > 1:

@@ -124,5 +124,5 @@ def estimate_embedding_overall_gpu2(data, masks, networks, sentence_weights, emb
         # the reference squeezes the batch dim away (sif2.py:200-201) and then
         # fails in cs.norm(dim=1) (:207); keep that error behaviour
         raise IndexError("Dimension out of range (expected to be in range of [-1, 0], but got 1)")
-    cs = P.mm2_project(s, num, aux, proj)
+    cs = P.mm2_project(s, num, aux, proj, split=P.project_split_ws(n, proj.kp, dev))
     return cs.to(home)

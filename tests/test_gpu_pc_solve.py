@@ -111,3 +111,28 @@ def test_deterministic_and_graph_replay(gpu):
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, pc) and int(flag.item()) == 0
+
+
+@pytest.mark.parametrize("n,npc", [(100, 1), (229, 1), (180, 2), (7, 1)])
+def test_transposed_start_in_one_launch(gpu, n, npc):
+    """mmb_pc_solve_mc_xt (X^T Omega and G2 in one launch, then the solve)
+    against mmb_xt_omega + mmb_pc_solve_mc: the same z0 sums, the same PC
+    bit for bit; and against the oracle."""
+    import mmb_lib as L
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = (0.4 * torch.randn(n, 300, generator=g) + 0.3 * torch.randn(300, generator=g)).to(gpu)
+    k = npc + P.N_OVERSAMPLES
+    G = (x.double().T @ x.double()).contiguous()
+    om = P.omega(n, k, gpu)
+    z0 = P.xt_omega(x, None, om)
+    flag = torch.zeros(1, dtype=torch.int32, device=gpu)
+    ref = P.pc_solve(G, z0, npc, True, flag=flag).clone()
+    ws = torch.zeros(L.query("mmb_pc_solve_mc_ws_bytes", 300), dtype=torch.uint8, device=gpu)
+    pc = torch.empty((npc, 300), dtype=torch.float64, device=gpu)
+    L.call("mmb_pc_solve_mc_xt", L.ptr(G), 300, L.ptr(x), n, L.ptr(om), k, npc, P.N_ITER, L.ptr(pc),
+           L.ptr(ws), L.ptr(flag), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 0 and not bool(ws[:16].any())
+    assert torch.equal(pc, ref)
+    oracle = O.pc_from_gram(G.cpu().numpy(), z0.cpu().numpy(), npc, True)
+    assert np.abs(pc.cpu().numpy() - oracle).max() < 1e-10

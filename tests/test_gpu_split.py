@@ -11,7 +11,10 @@ part order.  Checked here:
     gathered or dense text, fp32 or fp16 hi / lo s, scalar-width frames;
   * the FusedStep with the split stream (and the projection forked beside
     the PC solve) equals the one-workgroup step to the removal's dot order,
-    and both meet the oracle (sif_functions / sif2, 1e-5).
+    and both meet the oracle (sif_functions / sif2, 1e-5);
+  * the split-K projection (mmb_mm2_project_x3_split) against the one-pass
+    kernel: MMB2 rows to the K sum's f32 order, the fused PC removal's rows
+    bit for bit (they depend on x and the PC only), ragged row tiles.
 """
 import numpy as np
 import pytest
@@ -181,3 +184,30 @@ def test_split_step_vs_one_workgroup_step_and_oracle(gpu, golden, mode):
     ref_mm2 = M.estimate_embedding_overall_gpu2(M.concat_inputs(text, audio[r], visual[r]),
                                                  M.params_from_module(gen.cpu()), sw, text)
     assert M.row_rel_err(m1[torch.as_tensor(r, device=gpu)].cpu().numpy(), ref_mm2) < 1e-5
+
+
+@pytest.mark.parametrize("n", [2, 5, 100, 129, 203, 700, 1000])
+def test_split_k_projection_vs_one_pass(gpu, n):
+    inp = synth.device_workload(n, 40, 5000, A=300, Vd=300, seed=60 + n, device=gpu)
+    torch.manual_seed(3)
+    gen = models.AudioVisualGeneratorMultimodal(300, 300, 300, norm=None).to(gpu)
+    st = P.FusedStep(inp, gen.networks(), stream_project=False, fork_projection=False,
+                     split_stream=False)
+    st.run(check=True)
+    proj, s_, x, aux = st.proj, st.s, st.x, st.aux_of(0)
+    pc = st.pc.clone()
+    ref = P.mm2_project(s_, x, aux, proj).clone()
+    sif_ref = torch.empty_like(x)
+    ref2 = P.mm2_project(s_, x, aux, proj, pc=pc, sif_out=sif_ref).clone()
+    assert torch.equal(ref, ref2)
+    for slices in (0, 2, 3, 7, 57):
+        ws = torch.empty(max(16, L.query("mmb_mm2_project_x3_split_ws_bytes", n, proj.kp, slices)),
+                         dtype=torch.uint8, device=gpu)
+        got = P.mm2_project(s_, x, aux, proj, split=ws, slices=slices).clone()
+        again = P.mm2_project(s_, x, aux, proj, split=ws, slices=slices).clone()
+        sif = torch.empty_like(x)
+        got2 = P.mm2_project(s_, x, aux, proj, pc=pc, sif_out=sif, split=ws, slices=slices)
+        torch.cuda.synchronize()
+        assert torch.equal(got, again) and torch.equal(got, got2), slices
+        assert torch.equal(sif, sif_ref), slices
+        assert M.row_rel_err(got.cpu().numpy(), ref.cpu().numpy()) < 1e-6, slices
