@@ -738,6 +738,13 @@ class FusedStep:
     stream kernel slows by about what the projection hides (8 chunks, shared
     CUs / 64 balanced side CUs / 96 'high' side CUs: 28.5 / 30.7 / 28.8 ms per
     step against 28.6 ms unpipelined), so the default is one chunk.
+
+    Small steps (the dataset splits, r06): `split_stream` cuts
+    a few long rows over workgroups (mmb_mm2_stream_split), `split_projection`
+    runs the projection split-K (mmb_mm2_project_x3_split; K summed in another
+    f32 order than the one-pass kernel), and `fork_projection` runs it on a
+    side stream beside Gram -> PC solve; each is chosen by shape when left at
+    its default.
     """
 
     def __init__(self, inputs: dict, networks: dict, npc: int = 1, allreduce=None,
@@ -745,7 +752,8 @@ class FusedStep:
                  side_cus: int = 0, side_layout: str = "balanced", fuse_remove: bool = True,
                  gram_kind: str | None = None, stream_project: bool | None = None,
                  narrow_fused: bool | None = None, check_each_run: bool = False,
-                 fork_projection: bool | None = None, split_stream: bool | None = None):
+                 fork_projection: bool | None = None, split_stream: bool | None = None,
+                 split_projection: bool = True):
         self.inp = inputs
         self.check_each_run = check_each_run
         self.ids = inputs["ids"]
@@ -844,7 +852,8 @@ class FusedStep:
         self.fork = torch.cuda.Stream(device=dev) if self.fused_remove and fork_projection else None
         # a few rows: the projection's K loop split over workgroups
         self.proj_split = (project_split_ws(self.n, kp, dev)
-                           if self.s is not None and self.s_half and len(self.bounds) == 1 else None)
+                           if split_projection and self.s is not None and self.s_half
+                           and len(self.bounds) == 1 else None)
         self.gws = GramWorkspace(max(r1 - r0 for r0, r1 in self.bounds), self.d, dev)
         self.side = torch.cuda.Stream(device=dev) if len(self.bounds) > 1 else None
         self.main = None

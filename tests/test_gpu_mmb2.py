@@ -75,8 +75,13 @@ def test_fused_id_path_equals_dense_path(gpu, golden, case):
     ids32 = torch.as_tensor(ids, dtype=torch.int32, device=gpu)
     au, vi = torch.tensor(audio, device=gpu), torch.tensor(visual, device=gpu)
     proj = P.MMB2Projection(gen.to(gpu).networks(), 300, A, Vd, t, gpu)
-    num, s, aux = P.mm2_stream(n, t, 300, A, Vd, au, vi, ids32=ids32, table=table, wtab32=wtab)
-    fused = P.mm2_project(s, num, aux, proj)
+    # the drop-in's launch choices (sif2.py): split stream for a few long
+    # rows, split-K projection for a few rows -- the same sum orders
+    split = (P.split_ws(n, t, 300, A, Vd, gpu)
+             if t > 64 and 0 < n <= L.cu_count(gpu) else None)
+    num, s, aux = P.mm2_stream(n, t, 300, A, Vd, au, vi, ids32=ids32, table=table, wtab32=wtab,
+                               split=split)
+    fused = P.mm2_project(s, num, aux, proj, split=P.project_split_ws(n, proj.kp, gpu))
     if max(A, Vd) <= 128:  # the narrow-frame kernel: frame sums in another f32 order
         assert M.row_rel_err(fused.cpu().numpy(), dense.cpu().numpy()) < 1e-6
     else:
@@ -615,8 +620,11 @@ def test_stream_project_matches_two_kernel_step(gpu, N, T, A, Vd):
     gen = models.AudioVisualGeneratorMultimodal(300, A, Vd, norm=None).to(gpu)
     # the int8 Gram (its column bounds compared below) at every N
     a = P.FusedStep(inp, gen.networks(), stream_project=True, gram_kind="i8")
-    b = P.FusedStep(inp, gen.networks(), stream_project=False, gram_kind="i8")
-    assert a.stream_project and a.s is None and not b.stream_project
+    # (the one-pass projection: the split-K one sums K in another f32 order,
+    # tests/test_gpu_split.py)
+    b = P.FusedStep(inp, gen.networks(), stream_project=False, gram_kind="i8",
+                    split_projection=False)
+    assert a.stream_project and a.s is None and not b.stream_project and b.proj_split is None
     trace = {}
     s1, m1 = [t.clone() for t in a.run(trace=trace)]
     assert "mm2_stream_project" in trace and "pc_remove" in trace

@@ -5,7 +5,7 @@ set -u
 TAG=${1:-r06full}
 OUT=$PWD/gpurun_out/$TAG; mkdir -p "$OUT"
 ok() { local rc=$1; [ "$rc" -eq 0 ] || { echo "step failed rc=$rc"; exit "$rc"; }; }
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; ok $?
+timeout -k 10 900 python3 -u -m pytest tests -m gpu ${PYX--x} -v --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1; ok $?
 tail -1 "$OUT/pytest.log"
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; ok $?
 tail -1 "$OUT/smoke.log"
