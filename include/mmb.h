@@ -144,10 +144,13 @@ int mmb_pc_solve(const double* g, int d, const double* z0, int k, int npc, int n
 int mmb_step_status(const int32_t* flag, const double* pc, int n, int32_t nonfinite_bit,
                     int32_t* out, hipStream_t stream);
 
-/* (r06) the multi-workgroup solve runs the first n_iter / 2 products by
- * G2 = G G (one extra launch, gram_square_kernel; npc = 1 only): ws holds
- * G2 too, so mmb_pc_solve_mc_ws_bytes grew by d * d * 8 bytes (an ABI change:
- * size ws with this call).                                                  */
+/* (r06) the multi-workgroup solve runs (n_iter - 1) / 2 of its products by
+ * G2 = G G (npc = 1, n_iter >= 3; the first product is by G, and extra
+ * workgroups of the same launch form G2 beside it): ws holds G2 too, so
+ * mmb_pc_solve_mc_ws_bytes grew by d * d * 8 bytes (an ABI change: size ws
+ * with this call), and the third control word counts the squaring
+ * workgroups (the first 16 bytes are still the block a caller re-zeroes
+ * after MMB_FLAG_SYNC_TIMEOUT).                                             */
 size_t mmb_pc_solve_mc_ws_bytes(int d);
 /* The transposed branch (n < d) of mmb_pc_solve_mc from the rows themselves:
  * z0 = X^T omega [n, k] (x f32 [n, d], the a2 rows) and G2 formed in ONE

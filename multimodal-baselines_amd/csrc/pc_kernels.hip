@@ -2611,6 +2611,79 @@ __global__ __launch_bounds__(kP16NT) void pc_solve_mc_v1_kernel(const double* __
 }
 #endif  // MMB_DIAG
 
+// G2 = G G for the multi-workgroup solve's squared rounds (r06): one
+// upper-triangle 16 x 16 tile (a <= b) per 4 waves, which split the MFMA
+// k-steps (f64 16x16x4) and are summed in wave order; each element is written
+// at (i, j) and (j, i) by ONE thread, so G2 is exactly symmetric.  190 tiles
+// of ~19 k-steps each at d = 300.  Run by the solve's own extra workgroups
+// (pc_solve_mc_kernel, beside its first round) or by pc_prep_kernel (the
+// transposed start); the same k-steps per wave and the same sum order either
+// way, so G2 is the same bit for bit.
+constexpr int kSqNT = 256;
+__device__ __forceinline__ void square_tile_ab(int blk, int T, int& a, int& b) {
+  int rem = blk;
+  a = 0;  // blk -> (a, b), a <= b, row-major over the upper triangle
+  while (rem >= T - a) {
+    rem -= T - a;
+    ++a;
+  }
+  b = a + rem;
+}
+// wave wv (0-3) of the tile's group: its k-steps' MFMA partial into part4[wv]
+__device__ __forceinline__ void square_tile_partials(const double* __restrict__ G, int D, int blk,
+                                                     int wv, int lane, double* part4) {
+  const int T = (D + 15) / 16;
+  int a, b;
+  square_tile_ab(blk, T, a, b);
+  const int Ks = (D + 3) / 4;
+  const int pa = a * 16 + (lane & 15), pb = b * 16 + (lane & 15);
+  // every k-step's two operands loaded before the first MFMA (<= 20 k-steps
+  // per wave at D <= 320): one round trip of G reads, not one per k-step group
+  constexpr int kSqKs = (kP16MaxD / 4 + kSqNT / kWave - 1) / (kSqNT / kWave);  // 20
+  double x[kSqKs], y[kSqKs];
+#pragma unroll
+  for (int u = 0; u < kSqKs; ++u) {
+    const int st = wv + (kSqNT / kWave) * u;
+    const int q = 4 * st + (lane >> 4);
+    const bool okq = st < Ks && q < D;
+    // A[i][k] = G[a16 + i][q] = G[q][a16 + i] (symmetric), B[k][j] = G[q][b16 + j]
+    x[u] = (okq && pa < D) ? G[static_cast<int64_t>(q) * D + pa] : 0.0;
+    y[u] = (okq && pb < D) ? G[static_cast<int64_t>(q) * D + pb] : 0.0;
+  }
+  f64x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < kSqKs; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[u], y[u], acc, 0, 0, 0);
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) part4[wv * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+}
+// element e (0-255) of the tile: the four partials in wave order, stored at
+// (i, j) and (j, i); WT: write-through (agent-scope) stores for readers of
+// the same launch on other XCDs
+template <bool WT>
+__device__ __forceinline__ void square_tile_store(int D, double* __restrict__ G2, int blk, int e,
+                                                  const double* part4) {
+  const int T = (D + 15) / 16;
+  int a, b;
+  square_tile_ab(blk, T, a, b);
+  const int i = e >> 4, j = e & 15;
+  double v = 0.0;
+#pragma unroll
+  for (int w = 0; w < kSqNT / kWave; ++w) v += part4[w * 256 + e];
+  const int r = a * 16 + i, c = b * 16 + j;
+  if (r < D && c < D && (a != b || i <= j)) {
+    if (WT) {
+      const unsigned long long bits = __builtin_bit_cast(unsigned long long, v);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(G2 + static_cast<int64_t>(r) * D + c), bits,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(G2 + static_cast<int64_t>(c) * D + r), bits,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      G2[static_cast<int64_t>(r) * D + c] = v;
+      G2[static_cast<int64_t>(c) * D + r] = v;
+    }
+  }
+}
+
 // Since r05 an implicit round exchanges the RAW product H_t = G_t B_r, which
 // needs no factor of W_r, so the equilibrated Cholesky of W_r (the last wave) runs
 // beside the whole exchange -- partials, publish, the wait for the other
@@ -2644,7 +2717,7 @@ constexpr int kPnGu = (kPmMaxT * 256 + kPnPw * kWave - 1) / (kPnPw * kWave);  //
 // round's B_{r+1} / W_{r+1} update, 2 skips the round's factor
 template <int ABL = 0>
 __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __restrict__ G,
-                                                               const double* __restrict__ G2, int D,
+                                                               double* __restrict__ G2, int nsq_wg, int D,
                                                                const double* __restrict__ z0, int k,
                                                                int npc, int n_iter, int transposed,
                                                                double* __restrict__ pc_out,
@@ -2665,17 +2738,46 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   const int t = blockIdx.x;
   unsigned* ctr = ctl;
   unsigned* abort_w = ctl + 1;
+  unsigned* sq_ctr = ctl + 2;  // the squaring workgroups' arrivals
+
+  if (t >= T) {
+    // workgroups T .. T + nsq_wg - 1 (r06b): G2 = G G, two tiles each (waves
+    // 0-3 and 4-7), while the solve's workgroups run their first round by G.
+    // Write-through stores, drained by every wave, then one arrival; the
+    // solve waits for all nsq_wg before its first squared round.  An arrival
+    // that finds the count already met is a workspace handed over dirty.
+    double* part4 = p16_lds + 2 * Dp * kP16W + (wave >> 2) * 4 * 256;
+    const int blk = 2 * (t - T) + (wave >> 2), ntiles = T * (T + 1) / 2;
+    if (blk < ntiles) square_tile_partials(G, D, blk, wave & 3, lane, part4);
+    __syncthreads();
+    if (blk < ntiles) square_tile_store<true>(D, G2, blk, tid & 255, part4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned old = __hip_atomic_fetch_add(sq_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old >= static_cast<unsigned>(nsq_wg)) {
+        __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (flag) atomicOr(flag, MMB_FLAG_SYNC_TIMEOUT);
+      }
+    }
+    return;
+  }
 
   // this workgroup's 16 rows of the round's matrix as MFMA A fragments on
   // waves 0-6 (symmetric: row p of the tile = column p, 16 consecutive
   // doubles per k-row: coalesced); wave 7 is free for the k x k factor that
-  // overlaps the rest.  Since r06 the first n_sq = n_iter / 2 rounds multiply
-  // by G2 = G G (gram_square_kernel), each standing for two power
-  // iterations: span(G^7 Z0) is the same span, so the PC is sklearn's to
-  // rounding, with 4 exchange rounds instead of 7; the remaining round(s) and
-  // the tail use G itself
-  const int n_sq = G2 ? n_iter / 2 : 0;
+  // overlaps the rest.  Since r06 n_sq = (n_iter - 1) / 2 rounds multiply
+  // by G2 = G G, each standing for two power iterations: span(G^7 Z0) =
+  // span(G2^3 G Z0), so the PC is sklearn's to rounding, with 4 exchange
+  // rounds instead of 7.  The schedule is G, then the n_sq rounds by G2, then
+  // what is left (n_iter even: one more) by G, and the tail by G: the first
+  // round needs no G2, so the squaring workgroups of this launch (nsq_wg > 0)
+  // form it beside that round instead of a launch in front of the solve
+  const int n_sq = (G2 && n_iter >= 3) ? (n_iter - 1) / 2 : 0;
   double ga[kPnKs];
+  // (G2 from this launch's squaring workgroups is read after the acquire
+  // that follows their arrivals, so plain loads see it)
   auto load_rows = [&](const double* M) {
     const int p = t * 16 + (lane & 15);
 #pragma unroll
@@ -2684,7 +2786,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       ga[j] = (wave < kPnPw && p < D && q < D) ? M[static_cast<int64_t>(q) * D + p] : 0.0;
     }
   };
-  load_rows(n_sq > 0 ? G2 : G);
+  load_rows(G);
   // waves 0-6: their partial products of this tile of G with a [Dp][16] block
   auto tile_partials = [&](const double* B) {
     if (wave < kPnPw) {
@@ -2768,6 +2870,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
           s_abort = 1;
         } else if (final_x) {
           __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sq_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // acquire: the gather reads the other workgroups' tiles only after
         // their arrivals were observed (the barrier that follows releases the
@@ -2825,9 +2928,20 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
 
   int x = 0;  // the exchange
   const int T0 = T, k0 = k;
-  const int n_rounds = n_sq + (n_iter - 2 * n_sq);
+  const int n_rounds = n_iter - n_sq;  // 1 + n_sq + (n_iter - 1 - 2 n_sq)
   for (int r = 0; r < n_rounds; ++r) {
-    if (r == n_sq && n_sq > 0) load_rows(G);  // G2's rounds done
+    if (n_sq > 0 && r == 1) {
+      if (nsq_wg > 0) {  // G2 from this launch's squaring workgroups
+        if (tid == 0) {
+          if (!pm_wait(sq_ctr, static_cast<unsigned>(nsq_wg), abort_w, flag)) s_abort = 1;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        __syncthreads();
+        if (aborted()) return;
+      }
+      load_rows(G2);
+    }
+    if (n_sq > 0 && r == 1 + n_sq) load_rows(G);  // G2's rounds done
     {
       // the round's LDS addresses, bounds and per-lane indices are rebuilt
       // from an opaque zero every round: left loop-invariant, the compiler
@@ -2920,7 +3034,7 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
     PC_MARK(45 + 2 * r);
   }
 
-  if (n_rounds == n_sq && n_sq > 0) load_rows(G);  // (n_iter even: the tail's product is by G)
+  if (n_sq > 0 && n_rounds == 1 + n_sq) load_rows(G);  // (the tail's product is by G)
   if (!transposed) {
     // The direct branch's last round (r06) as an implicit round: the RAW
     // product H_t = G_t B is exchanged beside the factor of W (as in the
@@ -2965,7 +3079,10 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
     if (aborted()) return;
     if (!s_fail) {
       if (t != 0) return;  // the tail runs on workgroup 0 only
-      if (tid == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {
+        __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sq_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       p16_rmul<kPnNW, true>(sY, sM2, part, Dp);  // Z = B M^T (into the scratch block)
       gather(sZ, x, kPnNT);                        // H as T transposed tiles
       __syncthreads();
@@ -3062,59 +3179,13 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   PC_PROBE_FLUSH();
 }
 
-// G2 = G G for the multi-workgroup solve's squared rounds (r06): one
-// workgroup per upper-triangle 16 x 16 tile (a <= b), its 4 waves splitting
-// the MFMA k-steps (f64 16x16x4) and summed in wave order; each element is
-// written at (i, j) and (j, i) by ONE thread, so G2 is exactly symmetric.
-// ~190 workgroups of ~19 k-steps each: a few microseconds on the whole chip
-// against the ~6.7 us of each exchange round it saves (3 of 7 at n_iter = 7).
-constexpr int kSqNT = 256;
 __device__ __forceinline__ void gram_square_tile(const double* __restrict__ G, int D,
                                                  double* __restrict__ G2, int blk) {
   __shared__ double part[kSqNT / kWave][256];
-  const int T = (D + 15) / 16;
-  int rem = blk, a = 0;  // blk -> (a, b), a <= b, row-major over the upper triangle
-  while (rem >= T - a) {
-    rem -= T - a;
-    ++a;
-  }
-  const int b = a + rem;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int Ks = (D + 3) / 4;
-  const int pa = a * 16 + (lane & 15), pb = b * 16 + (lane & 15);
-  // every k-step's two operands loaded before the first MFMA (<= 20 k-steps
-  // per wave at D <= 320): the kernel is one round trip of G reads, not one
-  // per k-step group
-  constexpr int kSqKs = (kP16MaxD / 4 + kSqNT / kWave - 1) / (kSqNT / kWave);  // 20
-  double x[kSqKs], y[kSqKs];
-#pragma unroll
-  for (int u = 0; u < kSqKs; ++u) {
-    const int st = wave + (kSqNT / kWave) * u;
-    const int q = 4 * st + (lane >> 4);
-    const bool okq = st < Ks && q < D;
-    // A[i][k] = G[a16 + i][q] = G[q][a16 + i] (symmetric), B[k][j] = G[q][b16 + j]
-    x[u] = (okq && pa < D) ? G[static_cast<int64_t>(q) * D + pa] : 0.0;
-    y[u] = (okq && pb < D) ? G[static_cast<int64_t>(q) * D + pb] : 0.0;
-  }
-  f64x4 acc = {0, 0, 0, 0};
-#pragma unroll
-  for (int u = 0; u < kSqKs; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x[u], y[u], acc, 0, 0, 0);
-#pragma unroll
-  for (int reg = 0; reg < 4; ++reg) part[wave][((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
+  square_tile_partials(G, D, blk, wave, lane, &part[0][0]);
   __syncthreads();
-  const int e = threadIdx.x, i = e >> 4, j = e & 15;
-  double v = 0.0;
-#pragma unroll
-  for (int w = 0; w < kSqNT / kWave; ++w) v += part[w][e];
-  const int r = a * 16 + i, c = b * 16 + j;
-  if (r < D && c < D && (a != b || i <= j)) {
-    G2[static_cast<int64_t>(r) * D + c] = v;
-    G2[static_cast<int64_t>(c) * D + r] = v;
-  }
-}
-__global__ __launch_bounds__(kSqNT) void gram_square_kernel(const double* __restrict__ G, int D,
-                                                            double* __restrict__ G2) {
-  gram_square_tile(G, D, G2, blockIdx.x);
+  square_tile_store<false>(D, G2, blk, threadIdx.x, &part[0][0]);
 }
 
 // The transposed branch's start in ONE launch (r06): workgroups [0, nsq)
@@ -3930,7 +4001,7 @@ extern "C" size_t mmb_pc_solve_mc_ws_bytes(int d) {
 // component's last digits (3.4e-9 of the reference's g3b rows against the
 // 1e-9 bar) -- G2 keeps the dominant directions to rounding, not the smaller
 // ones the later components live in
-static bool solve_squares(int npc, int n_iter) { return n_iter >= 2 && npc == 1; }
+static bool solve_squares(int npc, int n_iter) { return n_iter >= 3 && npc == 1; }
 
 static int launch_solve_mc(const double* g, int d, const double* z0, int k, int npc, int n_iter,
                            int transposed, double* pc_out, void* ws, int32_t* flag, bool g2_ready,
@@ -3968,11 +4039,14 @@ static int launch_solve_mc(const double* g, int d, const double* z0, int k, int 
   unsigned* ctl = static_cast<unsigned*>(ws);  // arrival counter, abort word (16-byte block)
   double* xbuf = reinterpret_cast<double*>(static_cast<char*>(ws) + 16);
   double* g2 = xbuf + static_cast<size_t>(2) * (d / 16 + 1) * 512;  // (mmb_pc_solve_mc_ws_bytes)
+  // G2 ready (pc_prep_kernel) or formed by nsq_wg extra workgroups of the
+  // solve's own launch, two tiles each, beside its first round (r06b: a
+  // launch in front of the solve before, ~5 us on the step's critical path)
+  int nsq_wg = 0;
   if (!solve_squares(npc, n_iter)) {
     g2 = nullptr;
   } else if (!g2_ready) {
-    gram_square_kernel<<<T * (T + 1) / 2, kSqNT, 0, stream>>>(g, d, g2);
-    MMB_LAUNCH_CHECK();
+    nsq_wg = (T * (T + 1) / 2 + 1) / 2;
   }
   static bool attr = false;
   if (!attr) {
@@ -4010,13 +4084,14 @@ static int launch_solve_mc(const double* g, int d, const double* z0, int k, int 
     auto kern = abl == 1 ? pc_solve_mc_kernel<1> : abl == 2 ? pc_solve_mc_kernel<2> : pc_solve_mc_kernel<3>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(p16_lds_bytes(kP16MaxD)));
-    kern<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, d, z0, k, npc, n_iter, transposed, pc_out, xbuf, ctl, flag);
+    kern<<<T + nsq_wg, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, nsq_wg, d, z0, k, npc, n_iter, transposed,
+                                                         pc_out, xbuf, ctl, flag);
     MMB_LAUNCH_CHECK();
     return MMB_OK;
   }
 #endif
-  pc_solve_mc_kernel<<<T, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, d, z0, k, npc, n_iter, transposed,
-                                                              pc_out, xbuf, ctl, flag);
+  pc_solve_mc_kernel<<<T + nsq_wg, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, nsq_wg, d, z0, k, npc, n_iter,
+                                                                        transposed, pc_out, xbuf, ctl, flag);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }

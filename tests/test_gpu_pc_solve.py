@@ -2,10 +2,11 @@
 the CPU oracle (oracle.sif_oracle.pc_from_gram, itself pinned to the
 reference's TruncatedSVD by the g3 fixtures, tests/test_oracle_golden.py):
 
-  * squared rounds: the first n_iter / 2 products by G2 = G G
-    (gram_square_kernel), the rest and the tail by G -- every n_iter 0..8
-    (odd and even: the fragment reload before the tail), direct and
-    transposed branches, npc = 1 (squared) and npc = 2 (not squared);
+  * squared rounds: one product by G, then (n_iter - 1) / 2 by G2 = G G
+    (formed by extra workgroups of the same launch, or by the transposed
+    start's prep launch), the rest and the tail by G -- every n_iter 0..8
+    (odd and even: the fragment reloads), direct and transposed branches,
+    npc = 1 (squared) and npc = 2 (not squared);
   * the direct branch's last round exchanged beside its factor, and a
     rank-deficient block whose Cholesky pivots fail there (MGS^2 fallback,
     a second exchange);

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""The product library's PC solve (mmb_pc_solve_mc: gram_square_kernel +
-pc_solve_mc_kernel since r06) timed alone and checked against the oracle:
+"""The product library's PC solve (mmb_pc_solve_mc: pc_solve_mc_kernel with
+its squaring workgroups since r06b) timed alone and checked against the oracle:
 HIP events around --reps back-to-back solves at n_iter = 7, for a synthetic
 4096 x 300 Gram (tools/pc_ab.py's), a bench-step Gram (--step-g rows) and
 the transposed branch of POM's real valid split (100 rows).  One JSON line:
