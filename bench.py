@@ -731,7 +731,9 @@ def dataset_splits_config(P, models, synth, dev, reps=30):
     graph with concurrent branches (the splits' PC solves side by side).  Every
     time is host wall around the call including the sync that reads the flag
     (what a CLI user waits for), median of `reps`; phase_ms: HIP events of an
-    eager run.  SIF rows of the POM splits against the reference's recorded
+    eager run queued behind a device sleep (the host ahead of the GPU: GPU time
+    per phase), phase_ms_host_bound: the same events with the launches issued
+    as the host gets to them (the GPU idles between phases).  SIF rows of the POM splits against the reference's recorded
     rows (g11)."""
     import numpy as np
     import torch
@@ -752,6 +754,13 @@ def dataset_splits_config(P, models, synth, dev, reps=30):
         for nm, sp, st in zip(names, splits, steps):
             st.run(check=True)
             tr = {}
+            st.run(trace=tr)  # launched as the host gets to them: the GPU waits between
+            torch.cuda.synchronize(dev)
+            ph_host = {k: round(sum(a.elapsed_time(b) for a, b in v), 4) for k, v in tr.items()}
+            # the same launches queued behind a device sleep, so the host is
+            # ahead and each phase's events bracket GPU work only
+            tr = {}
+            torch.cuda._sleep(5_000_000)
             st.run(trace=tr)
             torch.cuda.synchronize(dev)
             ph = {k: round(sum(a.elapsed_time(b) for a, b in v), 4) for k, v in tr.items()}
@@ -761,7 +770,8 @@ def dataset_splits_config(P, models, synth, dev, reps=30):
             n, L = sp["ids"].shape
             res["splits"][nm] = {"utts": n, "tokens": L, "eager_ms": eager[0],
                                  "graph_ms": graph[0], "graph_ms_min": graph[1],
-                                 "phase_ms": ph, "kernel_ms": round(sum(ph.values()), 4)}
+                                 "phase_ms": ph, "kernel_ms": round(sum(ph.values()), 4),
+                                 "phase_ms_host_bound": ph_host}
             if name == "pom":
                 got = st.sif.double().cpu().numpy()[::int(z["row_step"])]
                 res["splits"][nm]["sif_row_rel_err_vs_reference"] = float(

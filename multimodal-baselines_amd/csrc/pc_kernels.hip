@@ -1820,58 +1820,69 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
 }
 
 // Cholesky of the k x k SPD matrix whose row `lane` (lane < k) is w[]
-// (registers; zero elsewhere): lane i keeps row i of the trailing matrix,
-// column j's multipliers broadcast by readlane, pivots inverted once
-// (rsqrt_f64).  Writes L (compact, sL) and L^{-1} (compact, sLi; lane c solves
-// L x = e_c with the reciprocal pivots) and returns, in x[], lane c's column
-// of L^{-1}.  *fail is set if a pivot is not positive (the pivot is then
-// replaced by 1).
+// (registers; zero elsewhere) by one wave, pivots inverted once (rsqrt_f64).
+// Writes L^{-1} (compact, sLi) and returns, in x[], lane c's column of
+// L^{-1}; L itself goes to sL column by column (sL[j * 16 + i], internal).
+// *fail is set if a pivot is not positive (the pivot is then replaced by 1).
+//
+// r06b: both loops run over the pivots at run time -- one copy of a step,
+// where r05 unrolled all 16 (~6 KB of code per instance, five instances in
+// the multi-workgroup solve: after other kernels the solve's first pass
+// through each missed in the instruction cache, +16 us over a warm solve,
+// tools/pc_probe "cold").  Lane i keeps row i of the trailing matrix
+// SHIFTED, so pivot j is always w[0]: d_jj = lane j's w[0], l_ij = w[0] /
+// sqrt(d_jj), and w[m - 1] <- w[m] - l_ij l_(j+m)j (a readlane of lane j + m).  The substitution is right-looking in the same
+// shifted form: lane c's t = e_c, step i: x_i = t_0 / L_ii to LDS, t_(m-1) <-
+// t_m - L_(i+m)i x_i (column i of L as LDS broadcasts).
 __device__ __forceinline__ void p16_chol_regs(double (&w)[kMaxK], double* sL, double* sLi, int k,
                                               int lane, int* fail, double (&x)[kMaxK], int mark = 31) {
-  // L's columns and the reciprocal pivots go to LDS as they are produced
-  // (sLi's storage holds the pivots until the inverse overwrites it): at
-  // 1024 threads a wave has 128 VGPRs, and the arrays of L and 1 / L_jj held
-  // in registers spilled to scratch, one reload per substitution step
-  double* rl = sLi;
+  double* rl = sLi + kMaxK * kMaxK - kMaxK;  // the reciprocal pivots: sLi's last row until the end
   bool bad = false;
   PC_WMARK(mark);
+#pragma unroll 1
+  for (int j = 0; j < k; ++j) {
+    const double djj = readlane_f64(w[0], j);
+    bad = bad || !(djj > 0.0);
+    const double p = djj > 0.0 ? djj : 1.0;
+    const double r = rsqrt_f64(p);
+    const double lij = (lane == j) ? p * r : (lane > j ? w[0] * r : 0.0);
+    if (lane < kMaxK) sL[j * kMaxK + lane] = lij;
+    if (lane == 0) rl[j] = r;
+    // every lane's l_(j+m)j first (lanes past k hold zero rows: l = 0
+    // there), then the updates -- no per-column branches, so the broadcasts
+    // issue back to back
+    double lm[kMaxK];
 #pragma unroll
-  for (int j = 0; j < kMaxK; ++j) {
-    if (j < k) {
-      const double djj = readlane_f64(w[j], j);  // broadcast: no LDS round trip
-      bad = bad || !(djj > 0.0);
-      const double p = djj > 0.0 ? djj : 1.0;
-      const double r = rsqrt_f64(p);
-      const double lij = (lane == j) ? p * r : (lane > j ? w[j] * r : 0.0);
-      if (lane < k) sL[lane * k + j] = lij;
-      if (lane == 0) rl[kMaxK * kMaxK - kMaxK + j] = r;  // the last row of sLi's storage
+    for (int m = 1; m < kMaxK; ++m) lm[m] = readlane_f64(lij, j + m);
 #pragma unroll
-      for (int m = j + 1; m < kMaxK; ++m) w[m] -= lij * readlane_f64(lij, m);
-    }
+    for (int m = 1; m < kMaxK; ++m) w[m - 1] = w[m] - lij * lm[m];
+    w[kMaxK - 1] = 0.0;
   }
   if (bad && lane == 0) *fail = 1;
   wave_lds_sync();
   PC_WMARK(mark + 1);
-  // column c = lane of Linv: forward substitution, L entries and the
-  // reciprocal pivots read as LDS broadcasts
+  double t[kMaxK];
 #pragma unroll
-  for (int i = 0; i < kMaxK; ++i) {
-    x[i] = 0.0;
-    if (i < k) {
-      double s = (i == lane) ? 1.0 : 0.0;
+  for (int m = 0; m < kMaxK; ++m) t[m] = (m == lane) ? 1.0 : 0.0;
+  // in order within the wave: step i reads rl[i] before any lane's store of
+  // row i can reach it (k = 16: row 15 is rl's storage)
+#pragma unroll 1
+  for (int i = 0; i < k; ++i) {
+    // column i of L below the diagonal (rows past 15 clamped: they only
+    // reach t's rows past k, which never become t[0] before the loop ends)
+    double li[kMaxK];
 #pragma unroll
-      for (int m = 0; m < i; ++m) s -= sL[i * k + m] * x[m];
-      x[i] = s * rl[kMaxK * kMaxK - kMaxK + i];
-    }
+    for (int m = 1; m < kMaxK; ++m) li[m] = sL[i * kMaxK + min(i + m, kMaxK - 1)];
+    const double xi = t[0] * rl[i];
+    if (lane < k) sLi[i * k + lane] = (i < lane) ? 0.0 : xi;
+#pragma unroll
+    for (int m = 1; m < kMaxK; ++m) t[m - 1] = t[m] - li[m] * xi;
+    t[kMaxK - 1] = 0.0;
   }
   PC_WMARK(mark + 2);
-  wave_lds_sync();  // every lane has read the pivots before sLi is written
-  if (lane < k) {
-#pragma unroll
-    for (int i = 0; i < kMaxK; ++i)
-      if (i < k) sLi[i * k + lane] = (i < lane) ? 0.0 : x[i];
-  }
   wave_lds_sync();
+#pragma unroll
+  for (int i = 0; i < kMaxK; ++i) x[i] = (i < k && lane < k) ? sLi[i * k + lane] : 0.0;
 }
 
 // Cholesky W = L L^T (k x k, compact, LDS) and Linv = L^{-1} by one wave.
@@ -2934,7 +2945,10 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
       if (nsq_wg > 0) {  // G2 from this launch's squaring workgroups
         if (tid == 0) {
           if (!pm_wait(sq_ctr, static_cast<unsigned>(nsq_wg), abort_w, flag)) s_abort = 1;
+          // the acquire's L1 invalidate completes asynchronously: wait for it
+          // before the barrier releases the other waves' plain loads of G2
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
         if (aborted()) return;

@@ -11,7 +11,15 @@
 #include <random>
 #include <vector>
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1] = "cold": a 1 GiB device copy before every solve (caches and
+  // the instruction cache hold other data, as inside a step)
+  const bool cold = argc > 1 && argv[1][0] == 'c';
+  void *cpa = nullptr, *cpb = nullptr;
+  if (cold) {
+    (void)hipMalloc(&cpa, size_t{1} << 30);
+    (void)hipMalloc(&cpb, size_t{1} << 30);
+  }
   const int D = 300, k = 11, n = 4096;
   std::mt19937_64 rng(1);
   std::normal_distribution<double> nd;
@@ -41,6 +49,7 @@ int main() {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
+    if (cold) (void)mmb_probe_copy(cpa, cpb, int64_t{1} << 30, 512, 0, 0);  // a kernel, not a DMA copy
     (void)hipEventRecord(a, 0);
     const int rc = mmb_pc_solve_mc(dG, D, dz, k, 1, 7, 0, dpc, ws, flag, 0);
     (void)hipEventRecord(b, 0);
