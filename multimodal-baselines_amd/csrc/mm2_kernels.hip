@@ -402,244 +402,6 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
 
 
 
-// out = L2-normalised (num + s @ Wm[:, :D] + c0) / (total), the fp16 hi/lo
-// split GEMM on the f16 MFMA pipe (sif2.py:186-207).
-//   S_split [N][2][Kp] fp16: hi | lo of the row-scaled sums (mmb_mm2_stream)
-//   img     B chunk images (mm2_split_wm_kernel)
-// Both operands are staged by direct global->LDS copies (no VGPR staging, no
-// ds_write): B two chunks deep (L2-resident), A four chunks deep (streamed
-// once from HBM, three chunks in flight).  One barrier per chunk, behind a
-// counted vmcnt that leaves the newest A chunk in flight.
-template <int CT>
-__global__ __launch_bounds__(kXT) void mm2_project_x3_kernel(
-    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
-    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
-    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
-    const double* __restrict__ pc, float* __restrict__ sif) {
-  constexpr int LDW = 64 * CT;
-  constexpr int BBUF = x3_bbuf_halves<CT>();
-  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 16-byte pieces per thread per B chunk (= CT)
-  constexpr int AQ = kXAbufHalves * 2 / 16 / kXT;  // = 2
-  static_assert(BQ * kXT * 16 == BBUF * 2 && AQ * kXT * 16 == kXAbufHalves * 2, "staging split");
-  // one dynamic LDS array: B ring, A ring, per-row scalars
-  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-  _Float16* bring = lds;
-  _Float16* aring = lds + kXBbuf * BBUF;
-  float* s_rs = reinterpret_cast<float*>(aring + kXAbuf * kXAbufHalves);
-  float* s_tot = s_rs + kXM;
-  float(*s_ss)[kXM] = reinterpret_cast<float(*)[kXM]>(s_tot + kXM);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;  // rows wr*32 + [0,32), column tiles wc*CT + [0,CT)
-  const int hl = lane >> 5, cl = lane & 31;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
-  const int nch = Kp / kXK;
-
-  // A piece g = q * kXT + tid of a chunk: plane g >> 9, row (g >> 2) & 127,
-  // LDS slot position g & 3 <- data slot (g & 3) ^ swz(row); rows past N
-  // re-read row N-1 (never stored)
-  const _Float16* asrc[AQ];
-#pragma unroll
-  for (int q = 0; q < AQ; ++q) {
-    const int g = q * kXT + tid;
-    const int plane = g >> 9, row = (g >> 2) & (kXM - 1);
-    const int64_t r = min(n0 + row, N - 1);
-    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
-  }
-  auto stage_a = [&](int c) {
-    const int cc = min(c, nch - 1);
-    _Float16* dst = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
-#pragma unroll
-    for (int q = 0; q < AQ; ++q)
-      glds16(asrc[q] + cc * kXK, dst + (q * kXT + wave * 64) * 8);
-  };
-  auto stage_b = [&](int c) {
-    const int cc = min(c, nch - 1);
-    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
-    _Float16* dst = bring + (c & (kXBbuf - 1)) * BBUF;
-#pragma unroll
-    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, dst + (q * kXT + wave * 64) * 8);
-  };
-
-  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? aux[2 * N + n0 + tid] : 1.f;
-  stage_b(0);
-  stage_a(0);
-  stage_a(1);
-  stage_a(2);
-
-  f32x16 acc[CT];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-  struct Frag {
-    half8 ah, al, bh[CT], bl[CT];
-  };
-  auto read_frag = [&](const _Float16* a, const _Float16* b, int s, Frag& f) {
-    const int js = 2 * s + hl;  // 16-byte data slot of this lane's 8 k values
-    const int row = wr * 32 + cl;
-    const int ao = row * kXK + ((js ^ x3_swz(row)) * 8);
-    f.ah = *reinterpret_cast<const half8*>(a + ao);
-    f.al = *reinterpret_cast<const half8*>(a + kXM * kXK + ao);
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int col = (wc * CT + t) * 32 + cl;
-      const int bo = col * kXK + ((js ^ x3_swz(col)) * 8);
-      f.bh[t] = *reinterpret_cast<const half8*>(b + bo);
-      f.bl[t] = *reinterpret_cast<const half8*>(b + LDW * kXK + bo);
-    }
-  };
-  auto mfma = [&](const Frag& f) {
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah, f.bh[t], acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah, f.bl[t], acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al, f.bh[t], acc[t], 0, 0, 0);
-    }
-  };
-
-  for (int c = 0; c < nch; ++c) {
-    // chunk c landed: this wave's copies of B(c) and A(c) retired (only the
-    // newest A chunk, AQ copies, may still be in flight; in the first
-    // iteration A(1) and A(2) too), then every wave's, by the barrier; the
-    // barrier also retires all reads of the buffers restaged below
-    if (c == 0) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    stage_b(c + 1);
-    stage_a(c + 3);
-    const _Float16* a = aring + (c & (kXAbuf - 1)) * kXAbufHalves;
-    const _Float16* b = bring + (c & (kXBbuf - 1)) * BBUF;
-    Frag f0, f1;
-    read_frag(a, b, 0, f0);
-    read_frag(a, b, 1, f1);
-    mfma(f0);
-    mfma(f1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // epilogue (as mm2_project_kernel): unscale, add weighted text sum + c0,
-  // divide by the total weight (column D), L2-normalise the row.  Every load
-  // is unconditional (row and column clamped in range, results selected
-  // afterwards): a load behind a per-lane branch is waited for right after
-  // it, which serialises the whole epilogue on memory latency.
-  {
-    // all 16 x (CT + 1) loads of this lane first, then the arithmetic: one
-    // memory latency for the whole epilogue instead of one per row group
-    // (the fragment registers are dead here, so the loads fit)
-    float nv[16][CT], tv[16], cv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const int64_t rowc = min(n0 + rl, N - 1);
-      tv[r] = aux[N + rowc];
-      cv[r] = aux[rowc];
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int col = (wc * CT + t) * 32 + cl;
-        nv[r][t] = num[rowc * D + min(col, D - 1)];
-      }
-    }
-    float cadd[CT], cinv[CT];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int col = (wc * CT + t) * 32 + cl;
-      cinv[t] = col_inv[col];
-      cadd[t] = c0[col];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const float inv_rs = 1.f / s_rs[rl];
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int col = (wc * CT + t) * 32 + cl;
-        const float add = col < D ? text_sum(nv[r][t], cv[r]) : (col == D ? tv[r] : 0.f);
-        const float y = acc[t][r] * (cinv[t] * inv_rs) + add + cadd[t];
-        acc[t][r] = y;
-        if (col == D) s_tot[rl] = y;
-      }
-    }
-  }
-  __syncthreads();
-  float ss[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) ss[r] = 0.f;
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int col = (wc * CT + t) * 32 + cl;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      const float cs = acc[t][r] / s_tot[rl];
-      acc[t][r] = cs;
-      if (col < D) ss[r] = fmaf(cs, cs, ss[r]);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float sum = half_sum(ss[r]);
-    if (cl == 0) s_ss[wc][wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl] = sum;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rl = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    const int64_t row = n0 + rl;
-    const float inv = 1.f / sqrtf(s_ss[0][rl] + s_ss[1][rl]);
-    if (row < N) {
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        const int col = (wc * CT + t) * 32 + cl;
-        if (col < D) out[row * D + col] = acc[t][r] * inv;
-      }
-    }
-  }
-
-  if (pc) {
-    // fused first-PC removal of the a2 rows (sif_functions.py:77-78, npc = 1):
-    // sif = x - (x . pc) pc in f64, with the accumulators dead.  Wave w owns
-    // rows w, w + 8, ... of the tile (4 at a time, every load issued first);
-    // lane l columns l + 64 m.  The x rows come back from L2 / Infinity Cache
-    // (this workgroup read them for the text sum above).
-    constexpr int PER = (LDW + 63) / 64;
-    double pcv[PER];
-#pragma unroll
-    for (int m = 0; m < PER; ++m) {
-      const int col = lane + 64 * m;
-      pcv[m] = col < D ? pc[col] : 0.0;
-    }
-    for (int g = wave; g < kXM; g += 4 * (kXT / 64)) {
-      float xv[4][PER];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t rowc = min(n0 + g + q * (kXT / 64), N - 1);
-#pragma unroll
-        for (int m = 0; m < PER; ++m) xv[q][m] = num[rowc * D + min(lane + 64 * m, D - 1)];
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t row = n0 + g + q * (kXT / 64);
-        double dp = 0.0;
-#pragma unroll
-        for (int m = 0; m < PER; ++m) dp = fma(static_cast<double>(xv[q][m]), pcv[m], dp);
-        const double dot = wave_sum(dp);
-        if (row < N) {
-#pragma unroll
-          for (int m = 0; m < PER; ++m) {
-            const int col = lane + 64 * m;
-            if (col < D) sif[row * D + col] = static_cast<float>(static_cast<double>(xv[q][m]) - dot * pcv[m]);
-          }
-        }
-      }
-    }
-  }
-}
 
 // Row-wise epilogue (D % 4 == 0, 16-byte aligned rows, 256 <= D < 320) of
 // the fp16x3 projection kernels: the raw accumulators of 64 rows at a time
@@ -1169,402 +931,6 @@ __global__ __launch_bounds__(kXT) void mm2_project_x3b_kernel(
 }
 
 
-// Variant 3 (r02): A (the row sums) straight from HBM into registers, B (the
-// weight image) through a 3-slot LDS ring.  The K-loop ablation of the
-// variant-2 kernel (tools/proj_diag.py, r02d) showed its staging latency-bound:
-// the A and B LDS-DMA copies alone took 2.26 ms of its 3.57, A's 7.3 GB only
-// two chunks ahead because the 2 x 40 KB B ring + 4 x 16 KB A ring fill the
-// LDS.  Here the waves are 4 (rows) x 2 (columns), a wave 32 rows x 160
-// columns (2 x 10 tiles of v_mfma_f32_16x16x32_f16): its A fragments are its
-// own rows (16 bytes per lane per plane and row tile, shared by the two
-// column waves through L2), loaded AD chunks ahead into rotating register
-// buffers by inline-asm loads (hidden from hipcc's vmcnt bookkeeping so the
-// LDS-DMA stream of B is never drained), and the whole 120 KB ring holds B,
-// two chunks ahead.  One barrier per chunk: B(c) landed for every wave, and
-// every wave's reads of the slot B(c+2) overwrites are done.
-//   issue order per chunk c: B(c+2) (5 copies per thread), A(c+AD) (4 loads)
-constexpr int kX3cBslots = 3;
-template <int CT>
-constexpr size_t x3c_lds_bytes() {
-  return kX3cBslots * x3_bbuf_halves<CT>() * sizeof(_Float16) + kXM * sizeof(float);
-}
-
-__device__ __forceinline__ void gload16_asm(half8& v, const _Float16* p) {
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-}
-
-template <int AD, int DIAG = 0>
-__global__ __launch_bounds__(kXT) void mm2_project_x3c_kernel(
-    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
-    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
-    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
-    const double* __restrict__ pc, float* __restrict__ sif) {
-  static_assert(AD == 3, "vmcnt counts below are written for AD = 3");
-  constexpr int CT = 5, NT = 10;
-  constexpr int BBUF = x3_bbuf_halves<CT>();
-  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 5 copies per thread per B chunk
-  static_assert(BQ == 5, "staging split");
-  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-  _Float16* bring = lds;
-  float* s_rs = reinterpret_cast<float*>(lds + kX3cBslots * BBUF);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int lq = lane >> 4, lc = lane & 15;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
-  const int nch = Kp / kXK;
-
-  // lane's A fragment rows (rows past N re-read row N-1, never stored):
-  // row tile i -> row wr*32 + 16 i + lc, k offset 8 lq of each chunk
-  const _Float16* arow[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int64_t r = min(n0 + wr * 32 + i * 16 + lc, N - 1);
-    arow[i] = S + r * 2 * Kp + lq * 8;
-  }
-  auto load_a = [&](int c, half8 (&h)[2], half8 (&l)[2]) {
-    const int cc = (DIAG & 2) ? 0 : min(c, nch - 1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      gload16_asm(h[i], arow[i] + cc * kXK);
-      gload16_asm(l[i], arow[i] + Kp + cc * kXK);
-    }
-  };
-  auto stage_b = [&](int c) {
-    const int cc = min(c, nch - 1);
-    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
-    _Float16* dst = bring + (c % kX3cBslots) * BBUF;
-#pragma unroll
-    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, dst + (q * kXT + wave * 64) * 8);
-  };
-
-  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
-
-  f32x4 acc[2][NT];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  half8 a0h[2], a0l[2], a1h[2], a1l[2], a2h[2], a2l[2], a3h[2], a3l[2];
-  stage_b(0);
-  stage_b(1);
-  load_a(0, a0h, a0l);
-  load_a(1, a1h, a1l);
-  load_a(2, a2h, a2l);
-
-  // chunk c: B(c) in ring slot c % 3, A(c) in (ah, al); A(c + 3) is loaded
-  // into (nh, nl), the buffer chunk c - 1 consumed
-  auto chunk = [&](int c, half8 (&ah)[2], half8 (&al)[2], half8 (&nh)[2], half8 (&nl)[2]) {
-    // B(c) and A(c) landed for this wave: ops issued after them are at most
-    // A(c+2) + B(c+1), A(c+3)... = 13 (chunk 0: A1, A2 = 8)
-    if (c == 0) {
-      asm volatile("s_waitcnt vmcnt(8)" : "+v"(ah[0]), "+v"(ah[1]), "+v"(al[0]), "+v"(al[1])::"memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(13)" : "+v"(ah[0]), "+v"(ah[1]), "+v"(al[0]), "+v"(al[1])::"memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    stage_b(c + 2);
-    load_a(c + 3, nh, nl);
-    const _Float16* b = bring + (c % kX3cBslots) * BBUF;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = (wc * NT + t) * 16 + lc;
-      const int bo = col * kXK + ((lq ^ x3_swz(col)) * 8);
-      const half8 bh = *reinterpret_cast<const half8*>(b + bo);
-      const half8 bl = *reinterpret_cast<const half8*>(b + (64 * CT) * kXK + bo);
-      if constexpr ((DIAG & 8) != 0) {
-        asm volatile("" ::"v"(bh), "v"(bl), "v"(ah[0]), "v"(al[0]), "v"(ah[1]), "v"(al[1]));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][t], 0, 0, 0);
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][t], 0, 0, 0);
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][t], 0, 0, 0);
-        }
-      }
-    }
-  };
-#pragma unroll 1
-  for (int c = 0; c < nch; c += 4) {
-    chunk(c, a0h, a0l, a3h, a3l);
-    if (c + 1 < nch) chunk(c + 1, a1h, a1l, a0h, a0l);
-    if (c + 2 < nch) chunk(c + 2, a2h, a2l, a1h, a1l);
-    if (c + 3 < nch) chunk(c + 3, a3h, a3l, a2h, a2l);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if constexpr ((DIAG & 1) != 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) asm volatile("" ::"v"(acc[i][t]));
-    return;
-  }
-  x3_row_epilogue<CT, 2, 4, 1, NT>(acc, reinterpret_cast<float*>(lds), s_rs, kXM, wr, wc, lq, lc, wave,
-                                   lane, n0, N, D, num, aux, col_inv, c0, pc, out, sif);
-}
-
-
-// Variant 4 (r02): 256-row tiles.  The weight image is staged once per 256
-// rows instead of per 128 (the K-loop ablation, r02d: the B copies cost as
-// much as streaming A from HBM); A (32 KB) and B (40 KB) chunks in 2-slot
-// rings (144 KB), one chunk ahead; 8 waves as 4 (rows) x 2 (columns), a wave
-// 64 rows x 160 columns (4 x 10 tiles of v_mfma_f32_16x16x32_f16, 160
-// accumulator registers).  The row-wise epilogue in four 64-row passes.
-constexpr int kX4M = 256;
-template <int CT>
-constexpr size_t x3d_lds_bytes() {
-  return 2 * (x3_bbuf_halves<CT>() + 2 * kX4M * kXK) * sizeof(_Float16) + kX4M * sizeof(float);
-}
-
-template <int DIAG = 0>
-__global__ __launch_bounds__(kXT) void mm2_project_x3d_kernel(
-    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
-    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
-    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
-    const double* __restrict__ pc, float* __restrict__ sif) {
-  constexpr int CT = 5, NT = 10, NI = 4, M = kX4M;
-  constexpr int BBUF = x3_bbuf_halves<CT>();
-  constexpr int ABUF = 2 * M * kXK;
-  constexpr int BQ = BBUF * 2 / 16 / kXT;  // 5
-  constexpr int AQ = ABUF * 2 / 16 / kXT;  // 4
-  static_assert(BQ == 5 && AQ == 4, "staging split");
-  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-  _Float16* bring = lds;
-  _Float16* aring = lds + 2 * BBUF;
-  float* s_rs = reinterpret_cast<float*>(aring + 2 * ABUF);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int lq = lane >> 4, lc = lane & 15;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * M;
-  const int nch = Kp / kXK;
-
-  // A piece g = q * 512 + tid: plane g >> 10, row (g >> 2) & 255, LDS slot
-  // position g & 3 <- data slot (g & 3) ^ swz(row)
-  const _Float16* asrc[AQ];
-#pragma unroll
-  for (int q = 0; q < AQ; ++q) {
-    const int g = q * kXT + tid;
-    const int plane = g >> 10, row = (g >> 2) & (M - 1);
-    const int64_t r = min(n0 + row, N - 1);
-    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
-  }
-  auto stage = [&](int c) {
-    const int cc = min(c, nch - 1);
-    const _Float16* src = img + static_cast<int64_t>(cc) * BBUF;
-    _Float16* bd = bring + (c & 1) * BBUF;
-#pragma unroll
-    for (int q = 0; q < BQ; ++q) glds16(src + (q * kXT + tid) * 8, bd + (q * kXT + wave * 64) * 8);
-    _Float16* ad = aring + (c & 1) * ABUF;
-#pragma unroll
-    for (int q = 0; q < AQ; ++q) glds16(asrc[q] + cc * kXK, ad + (q * kXT + wave * 64) * 8);
-  };
-
-  if (tid < M) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
-
-  f32x4 acc[NI][NT];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage(0);
-#pragma unroll 1
-  for (int c = 0; c < nch; ++c) {
-    // chunk c landed (this wave's copies, then everyone's by the barrier);
-    // the barrier also retires every read of the slots chunk c + 1 overwrites
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < nch) stage(c + 1);
-    const _Float16* a = aring + (c & 1) * ABUF;
-    const _Float16* b = bring + (c & 1) * BBUF;
-    half8 ah[NI], al[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int row = wr * 64 + i * 16 + lc;
-      const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
-      ah[i] = *reinterpret_cast<const half8*>(a + ao);
-      al[i] = *reinterpret_cast<const half8*>(a + M * kXK + ao);
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = (wc * NT + t) * 16 + lc;
-      const int bo = col * kXK + ((lq ^ x3_swz(col)) * 8);
-      const half8 bh = *reinterpret_cast<const half8*>(b + bo);
-      const half8 bl = *reinterpret_cast<const half8*>(b + (64 * CT) * kXK + bo);
-      if constexpr ((DIAG & 8) != 0) {
-        asm volatile("" ::"v"(bh), "v"(bl));
-      } else {
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bh, acc[i][t], 0, 0, 0);
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[i], bl, acc[i][t], 0, 0, 0);
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[i], bh, acc[i][t], 0, 0, 0);
-        }
-      }
-    }
-    if constexpr ((DIAG & 8) != 0) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i) asm volatile("" ::"v"(ah[i]), "v"(al[i]));
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if constexpr ((DIAG & 1) != 0) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) asm volatile("" ::"v"(acc[i][t]));
-    return;
-  }
-  x3_row_epilogue<CT, NI, 1, 2, NT>(acc, reinterpret_cast<float*>(lds), s_rs, M, wr, wc, lq, lc, wave,
-                                    lane, n0, N, D, num, aux, col_inv, c0, pc, out, sif);
-}
-
-
-// Variant 6 (r02): B fragments straight from L2 into registers, one chunk
-// ahead; the LDS holds only A, eight chunks deep.  The K-loop ablation
-// (r02d) put the default kernel's time in its staging: 144 KB of rings keep
-// B one chunk and A (from HBM) two chunks ahead, too little in flight.  The
-// weight image is L2-resident and shared by every workgroup, so each wave
-// loads its own B fragments (80 columns x hi/lo: 10 x 16 bytes per lane per
-// chunk, one coalesced KB per instruction; the two row waves of a column
-// block both load them, 2x L2 traffic) into three rotating register sets,
-// and the 128 KB A ring runs six chunks ahead.  Waves and MFMA order as
-// variant 2 (2 x 4 waves of 64 rows x 80 columns, hh + hl + lh per tile), so
-// the rows are bit-identical.  The B loads are inline asm (saddr form: the
-// chunk's image base in SGPRs, a per-lane 32-bit offset) so hipcc's vmcnt
-// bookkeeping never drains the A LDS-DMA stream; one counted wait per chunk.
-//   issue order per chunk c: B(c+1) (10 loads), A(c+6) (2 copies per thread)
-constexpr int kX3eAslots = 8;
-template <int CT>
-constexpr size_t x3e_lds_bytes() {
-  return kX3eAslots * kXAbufHalves * sizeof(_Float16) + kXM * sizeof(float);
-}
-
-__device__ __forceinline__ void gload16_saddr(half8& v, const void* sbase, int voff) {
-  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
-}
-
-template <int DIAG = 0>
-__global__ __launch_bounds__(kXT) void mm2_project_x3e_kernel(
-    const _Float16* __restrict__ S, const float* __restrict__ num, const float* __restrict__ aux,
-    const _Float16* __restrict__ img, const float* __restrict__ col_inv,
-    const float* __restrict__ c0, int64_t N, int Kp, int D, float* __restrict__ out,
-    const double* __restrict__ pc, float* __restrict__ sif) {
-  constexpr int CT = 5, LDW = 64 * CT;
-  constexpr int BBUF = x3_bbuf_halves<CT>();       // halves per B chunk image
-  constexpr int AQ = kXAbufHalves * 2 / 16 / kXT;  // 2 copies per thread per A chunk
-  static_assert(AQ == 2, "staging split");
-  extern __shared__ __attribute__((aligned(16))) _Float16 lds[];
-  _Float16* aring = lds;
-  float* s_rs = reinterpret_cast<float*>(aring + kX3eAslots * kXAbufHalves);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int lq = lane >> 4, lc = lane & 15;
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * kXM;
-  const int nch = Kp / kXK;
-
-  const _Float16* asrc[AQ];
-#pragma unroll
-  for (int q = 0; q < AQ; ++q) {
-    const int g = q * kXT + tid;
-    const int plane = g >> 9, row = (g >> 2) & (kXM - 1);
-    const int64_t r = min(n0 + row, N - 1);
-    asrc[q] = S + r * 2 * Kp + plane * Kp + ((g & 3) ^ x3_swz(row)) * 8;
-  }
-  auto stage_a = [&](int c) {
-    const int cc = min(c, nch - 1);
-    _Float16* dst = aring + (c & (kX3eAslots - 1)) * kXAbufHalves;
-#pragma unroll
-    for (int q = 0; q < AQ; ++q) glds16(asrc[q] + cc * kXK, dst + (q * kXT + wave * 64) * 8);
-  };
-  // lane's B fragment of column tile t, plane p of a chunk image: column
-  // wc*80 + 16 t + lc, k slot lq at position lq ^ swz(col) (swz depends on
-  // lc only: 16 t and wc*80 are multiples of 16)
-  const int boff = ((wc * CT * 16 + lc) * kXK + ((lq ^ x3_swz(lc)) * 8)) * 2;  // bytes
-  using B10 = half8[2 * CT];
-  auto load_b = [&](int c, B10& b) {
-    const int cc = min(c, nch - 1);
-    const void* base = img + static_cast<int64_t>(cc) * BBUF;
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      gload16_saddr(b[2 * t], base, boff + t * 16 * kXK * 2);
-      gload16_saddr(b[2 * t + 1], base, boff + (LDW * kXK + t * 16 * kXK) * 2);
-    }
-  };
-
-  if (tid < kXM) s_rs[tid] = (n0 + tid < N) ? 1.f / aux[2 * N + n0 + tid] : 1.f;
-
-  f32x4 acc[4][CT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int t = 0; t < CT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  B10 b0, b1;
-#pragma unroll
-  for (int c = 0; c < kX3eAslots - 2; ++c) stage_a(c);
-  load_b(0, b0);
-
-  // chunk c: A(c) in ring slot c & 7, B(c) in (b); loads B(c+1) into (nb),
-  // then A(c+6).  Loads return in issue order, so the short-lead B loads go
-  // first: waiting for B(c) (chunk c-1's first ops) leaves A(c+5) in flight
-  // prologue: A(0..5), then B(0) -- all of it landed before chunk 0
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(b0[0]), "+v"(b0[1]), "+v"(b0[2]), "+v"(b0[3]), "+v"(b0[4]),
-               "+v"(b0[5]), "+v"(b0[6]), "+v"(b0[7]), "+v"(b0[8]), "+v"(b0[9])::"memory");
-  auto chunk = [&](int c, B10& b, B10& nb) {
-    asm volatile("s_waitcnt vmcnt(2)" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]),
-                 "+v"(b[5]), "+v"(b[6]), "+v"(b[7]), "+v"(b[8]), "+v"(b[9])::"memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    load_b(c + 1, nb);
-    stage_a(c + kX3eAslots - 2);
-    const _Float16* a = aring + (c & (kX3eAslots - 1)) * kXAbufHalves;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wr * 64 + i * 16 + lc;
-      const int ao = row * kXK + ((lq ^ x3_swz(row)) * 8);
-      const half8 ah = *reinterpret_cast<const half8*>(a + ao);
-      const half8 al = *reinterpret_cast<const half8*>(a + kXM * kXK + ao);
-      if constexpr ((DIAG & 8) != 0) {
-        asm volatile("" ::"v"(ah), "v"(al));
-      } else {
-#pragma unroll
-        for (int t = 0; t < CT; ++t) {
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b[2 * t], acc[i][t], 0, 0, 0);
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b[2 * t + 1], acc[i][t], 0, 0, 0);
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, b[2 * t], acc[i][t], 0, 0, 0);
-        }
-      }
-    }
-    if constexpr ((DIAG & 8) != 0) {
-#pragma unroll
-      for (int t = 0; t < 2 * CT; ++t) asm volatile("" ::"v"(b[t]));
-    }
-  };
-#pragma unroll 1
-  for (int c = 0; c < nch; c += 2) {
-    chunk(c, b0, b1);
-    if (c + 1 < nch) chunk(c + 1, b1, b0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if constexpr ((DIAG & 1) != 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int t = 0; t < CT; ++t) asm volatile("" ::"v"(acc[i][t]));
-    return;
-  }
-  x3_row_epilogue<CT, 4>(acc, reinterpret_cast<float*>(lds), s_rs, kXM, wr, wc, lq, lc, wave, lane,
-                         n0, N, D, num, aux, col_inv, c0, pc, out, sif);
-}
 
 template <int CT>
 constexpr size_t x3b_lds_bytes() { return x3_lds_bytes<CT>() + 2 * kXM * sizeof(float); }
@@ -1668,64 +1034,7 @@ __global__ __launch_bounds__(256) void x3_splitk_rows_kernel(
 // software-pipelined K loop.  MMB_PROJ_VARIANT overrides (read once).
 // Row-wise projection epilogue (1, default) or the MFMA-tile-layout one (0);
 // MMB_PROJ_ROWEPI overrides (tools build, read per launch).
-#ifdef MMB_DIAG
-static bool proj_row_epilogue() {  // re-read per launch (in-process A/B)
-  const char* e = getenv("MMB_PROJ_ROWEPI");
-  return e ? atoi(e) != 0 : true;
-}
 
-static int proj_diag() {  // re-read per launch: timing sweeps flip it in one process
-  const char* e = getenv("MMB_PROJ_DIAG");
-  return e ? atoi(e) : 0;
-}
-
-static int proj_variant() {  // re-read per launch (in-process A/B sweeps)
-  const char* e = getenv("MMB_PROJ_VARIANT");
-  return e ? atoi(e) : 2;
-}
-#else
-// the product library: variant 2 with the row-wise epilogue, no knobs
-constexpr bool proj_row_epilogue() { return true; }
-constexpr int proj_diag() { return 0; }
-constexpr int proj_variant() { return 2; }
-#endif
-
-#ifdef MMB_DIAG
-template <int CT, int D_>
-static void launch_diag1(int grid, size_t ldsb, const _Float16* s, const float* num, const float* aux,
-                         const _Float16* img, const float* ci, const float* c0, int64_t n, int kp,
-                         int d, float* out, const double* pc, float* sif, hipStream_t stream) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true, true, D_>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
-    attr = true;
-  }
-  mm2_project_x3b_kernel<CT, true, true, D_><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp,
-                                                                         d, out, pc, sif);
-}
-
-// timing-only ablations of the default kernel (MMB_PROJ_DIAG; see the DIAG bits)
-template <int CT>
-static void launch_diag(int v, int grid, size_t ldsb, const _Float16* s, const float* num,
-                        const float* aux, const _Float16* img, const float* ci, const float* c0,
-                        int64_t n, int kp, int d, float* out, const double* pc, float* sif,
-                        hipStream_t stream) {
-#define MMB_DIAG_CASE(D_) \
-  case D_: launch_diag1<CT, D_>(grid, ldsb, s, num, aux, img, ci, c0, n, kp, d, out, pc, sif, stream); break;
-  switch (v) {
-    MMB_DIAG_CASE(1) MMB_DIAG_CASE(2) MMB_DIAG_CASE(3) MMB_DIAG_CASE(4) MMB_DIAG_CASE(8)
-    MMB_DIAG_CASE(9) MMB_DIAG_CASE(11) MMB_DIAG_CASE(13) MMB_DIAG_CASE(17) MMB_DIAG_CASE(25)
-    MMB_DIAG_CASE(33) MMB_DIAG_CASE(41) MMB_DIAG_CASE(65) MMB_DIAG_CASE(73) MMB_DIAG_CASE(97)
-    MMB_DIAG_CASE(105) MMB_DIAG_CASE(121) MMB_DIAG_CASE(113)
-    default: break;
-  }
-#undef MMB_DIAG_CASE
-}
-
-#endif
-
-#ifndef MMB_DIAG
 // The product dispatch: the 16x16x32 kernel with the software-pipelined K
 // loop (variant 2), row-wise epilogue where the shape allows it.
 template <int CT>
@@ -1733,6 +1042,13 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
                              const _Float16* img, const float* ci, const float* c0, int64_t n,
                              int kp, int d, float* out, const double* pc, float* sif,
                              hipStream_t stream) {
+#ifndef MMB_HOOK_PROJECT_X3  // (tools/diag: the MMB_PROJ_* variants and ablations)
+#define MMB_HOOK_PROJECT_X3(rc) false
+#endif
+  {
+    int rc_ = MMB_OK;
+    if (MMB_HOOK_PROJECT_X3(rc_)) return rc_;
+  }
   const int grid = static_cast<int>(ceil_div(n, kXM));
   constexpr size_t ldsb = x3b_lds_bytes<CT>();
   static_assert(ldsb <= 160 * 1024, "x3b chunk rings exceed LDS");
@@ -1762,140 +1078,6 @@ static int launch_project_x3(const _Float16* s, const float* num, const float* a
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
-#else
-template <int CT>
-static int launch_project_x3(const _Float16* s, const float* num, const float* aux,
-                             const _Float16* img, const float* ci, const float* c0, int64_t n,
-                             int kp, int d, float* out, const double* pc, float* sif,
-                             hipStream_t stream) {
-  const int grid = static_cast<int>(ceil_div(n, kXM));
-  constexpr size_t lds = x3_lds_bytes<CT>();
-  static_assert(lds <= 160 * 1024, "x3 chunk rings exceed LDS");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3_kernel<CT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr = true;
-  }
-  if (proj_variant() >= 1) {
-    constexpr size_t ldsb = x3b_lds_bytes<CT>();
-    static_assert(ldsb <= 160 * 1024, "x3b chunk rings exceed LDS");
-    static bool attr_b = false;
-    if (!attr_b) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, false>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, false, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3b_kernel<CT, true, true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsb));
-      attr_b = true;
-    }
-    auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-    // the row-wise epilogue: D in [256, 320) (column D in a lane's second
-    // unit), whole float4 units, 16-byte aligned rows
-    const bool rowepi = CT == 5 && d >= 256 && d % 4 == 0 && a16(num) && a16(out) &&
-                        (sif == nullptr || a16(sif)) && proj_row_epilogue();
-    const bool pipe = proj_variant() == 2;
-    if constexpr (CT == 5) {
-      if (rowepi && proj_variant() == 6) {
-        constexpr size_t ldse = x3e_lds_bytes<CT>();
-        static_assert(ldse <= 160 * 1024, "x3e ring exceeds LDS");
-        static_assert(64 * 324 * sizeof(float) <= kX3eAslots * kXAbufHalves * sizeof(_Float16),
-                      "row epilogue scratch exceeds the A ring");
-        static bool attr_e = false;
-        if (!attr_e) {
-          for (const void* f : {reinterpret_cast<const void*>(&mm2_project_x3e_kernel<0>),
-                                reinterpret_cast<const void*>(&mm2_project_x3e_kernel<1>),
-                                reinterpret_cast<const void*>(&mm2_project_x3e_kernel<9>)})
-            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldse));
-          attr_e = true;
-        }
-        const int dg = proj_diag();
-        if (dg == 1)
-          mm2_project_x3e_kernel<1><<<grid, kXT, ldse, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        else if (dg == 9)
-          mm2_project_x3e_kernel<9><<<grid, kXT, ldse, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        else
-          mm2_project_x3e_kernel<0><<<grid, kXT, ldse, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        MMB_LAUNCH_CHECK();
-        return MMB_OK;
-      }
-      if (rowepi && proj_variant() == 4) {
-        constexpr size_t ldsd = x3d_lds_bytes<CT>();
-        static_assert(ldsd <= 160 * 1024, "x3d rings exceed LDS");
-        static bool attr_d = false;
-        if (!attr_d) {
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3d_kernel<0>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsd));
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3d_kernel<1>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsd));
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3d_kernel<9>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsd));
-          attr_d = true;
-        }
-        const int g4 = static_cast<int>(ceil_div(n, kX4M));
-        const int dg = proj_diag();
-        if (dg == 1)
-          mm2_project_x3d_kernel<1><<<g4, kXT, ldsd, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        else if (dg == 9)
-          mm2_project_x3d_kernel<9><<<g4, kXT, ldsd, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        else
-          mm2_project_x3d_kernel<0><<<g4, kXT, ldsd, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        MMB_LAUNCH_CHECK();
-        return MMB_OK;
-      }
-      if (rowepi && proj_variant() == 3) {
-        constexpr size_t ldsc = x3c_lds_bytes<CT>();
-        static_assert(ldsc <= 160 * 1024, "x3c ring exceeds LDS");
-        static_assert(64 * 324 * sizeof(float) <= kX3cBslots * x3_bbuf_halves<CT>() * sizeof(_Float16),
-                      "row epilogue scratch exceeds the B ring");
-        static bool attr_c = false;
-        if (!attr_c) {
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3c_kernel<3>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsc));
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3c_kernel<3, 1>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsc));
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mm2_project_x3c_kernel<3, 9>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(ldsc));
-          attr_c = true;
-        }
-        const int dg = proj_diag();
-        if (dg == 1)
-          mm2_project_x3c_kernel<3, 1><<<grid, kXT, ldsc, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        else if (dg == 9)
-          mm2_project_x3c_kernel<3, 9><<<grid, kXT, ldsc, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        else
-          mm2_project_x3c_kernel<3><<<grid, kXT, ldsc, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out, pc, sif);
-        MMB_LAUNCH_CHECK();
-        return MMB_OK;
-      }
-    }
-    if (rowepi && pipe && proj_diag() != 0) {
-      if constexpr (CT == 5) launch_diag<CT>(proj_diag(), grid, ldsb, s, num, aux, img, ci, c0, n, kp, d, out, pc, sif, stream);
-    } else if (rowepi && pipe) {
-      mm2_project_x3b_kernel<CT, true, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
-                                                                          n, kp, d, out, pc, sif);
-    } else if (pipe) {
-      mm2_project_x3b_kernel<CT, false, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0,
-                                                                           n, kp, d, out, pc, sif);
-    } else if (rowepi) {
-      mm2_project_x3b_kernel<CT, true><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n, kp,
-                                                                    d, out, pc, sif);
-    } else {
-      mm2_project_x3b_kernel<CT, false><<<grid, kXT, ldsb, stream>>>(s, num, aux, img, ci, c0, n,
-                                                                     kp, d, out, pc, sif);
-    }
-  } else {
-    mm2_project_x3_kernel<CT><<<grid, kXT, lds, stream>>>(s, num, aux, img, ci, c0, n, kp, d, out,
-                                                          pc, sif);
-  }
-  MMB_LAUNCH_CHECK();
-  return MMB_OK;
-}
-
-#endif
 
 template <int CT>
 static int launch_project(const float* s, const float* num, const float* aux, const float* wm,
@@ -2187,3 +1369,10 @@ extern "C" int mmb_mm2_text_cache(const float* table, int64_t v, int d, const fl
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
+
+// the tools build's projection variants, launches and knobs (tools/diag/);
+// the product library includes an empty header here
+#ifndef MMB_TOOLS_TAIL_MM2
+#define MMB_TOOLS_TAIL_MM2 "mmb_no_tools.h"
+#endif
+#include MMB_TOOLS_TAIL_MM2

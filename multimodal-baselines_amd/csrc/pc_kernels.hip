@@ -332,12 +332,9 @@ __global__ __launch_bounds__(kG2NT) void gram_tri_kernel(const float* __restrict
 // LDS ([digit][feature][4 slots of 16 rows], the conflict-free slot swizzle
 // of the 16x16x32 f16 fragment reads, whose lane map this read shares), then
 // each wave runs 13 MFMAs per tile and the f64 update.
-constexpr int kGiNT = 512;
 constexpr int kGiRows = 64;
 constexpr int kGiF = 320;       // padded feature count (D <= 320)
 constexpr int kGiDig = 4;       // base-256 digits per value
-constexpr int kGiMaxTiles = 12; // tiles per wave (<= 96 per workgroup: d <= 304)
-constexpr int kGiItems = kGiF / 16 * 16 * 4;  // (feature, 16-row slot) items per chunk
 
 // 16-byte slot swizzle of a feature's 64-byte digit row: slot kq of feature
 // f sits at kq ^ gi_swz(f).  (f >> 1) & 3 keeps the MFMA operand reads
@@ -378,221 +375,6 @@ __device__ __forceinline__ void gi_planes(unsigned v0, unsigned v1, unsigned v2,
   w[1] = __builtin_amdgcn_perm(q1, p1, 0x05040100u) ^ 0x80808080u;  // byte 2
   w[2] = __builtin_amdgcn_perm(q0, p0, 0x07060302u) ^ 0x80808080u;  // byte 1
   w[3] = __builtin_amdgcn_perm(q0, p0, 0x05040100u) ^ 0x80808080u;  // byte 0
-}
-
-// DIAG (timing-only builds, wrong results; MMB_GRAM_DIAG): bit 0 no MFMAs
-// (operands kept live), bit 1 no f64 update, bit 2 no slicing, bit 3 no
-// x loads
-template <int DIAG = 0>
-__global__ __launch_bounds__(kGiNT) void gram_i8_kernel(const float* __restrict__ x,
-                                                       const unsigned* __restrict__ colmax,
-                                                       int64_t N, int D, int nt, int R,
-                                                       int64_t chunk, int xcd_map,
-                                                       double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_dig[];  // [2][4][kGiF][64]
-  const int T = nt * (nt + 1) / 2;
-  int half, range;
-  if (xcd_map) {
-    const int b = blockIdx.x;
-    half = (b >> 3) & 1;
-    range = (b & 7) + 8 * (b >> 4);
-  } else {
-    half = blockIdx.x & 1;
-    range = blockIdx.x >> 1;
-  }
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t0 = half * ((T + 1) / 2), t1 = half ? T : (T + 1) / 2;
-  // this wave's tiles: a contiguous run of the triangle (row-major)
-  const int per = (t1 - t0 + (kGiNT / kWave) - 1) / (kGiNT / kWave);
-  const int q0 = t0 + wave * per;
-  int ti[kGiMaxTiles], tj[kGiMaxTiles];
-  int ntl = 0;
-#pragma unroll
-  for (int q = 0; q < kGiMaxTiles; ++q) {
-    ti[q] = tj[q] = 0;
-    if (q < per && q0 + q < t1) {
-      tri_tile(q0 + q, nt, ti[q], tj[q]);
-      ntl = q + 1;
-    }
-  }
-  double acc[kGiMaxTiles][4];
-#pragma unroll
-  for (int q = 0; q < kGiMaxTiles; ++q)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc[q][e] = 0.0;
-
-  const int64_t r0 = range * chunk;
-  const int64_t r1 = min(N, r0 + chunk);
-  const int nchunks = static_cast<int>(r1 > r0 ? (r1 - r0 + kGiRows - 1) / kGiRows : 0);
-  const int nf = nt * 16;  // features turned into digits (zero past D)
-  const int nitems = nf * 4;
-  constexpr int kIt = (kGiItems + kGiNT - 1) / kGiNT;  // items per thread (<= 3)
-  // item it = f + nf * kq: feature f, rows 16 kq .. 16 kq + 15 of the chunk
-  int it_f[kIt], it_kq[kIt], it_e[kIt];
-#pragma unroll
-  for (int u = 0; u < kIt; ++u) {
-    const int it = tid + kGiNT * u;
-    it_f[u] = it < nitems ? it % nf : 0;
-    it_kq[u] = it < nitems ? it / nf : 0;
-    it_e[u] = (it < nitems && it_f[u] < D) ? gi_exp(colmax[it_f[u]]) : 0;
-  }
-  // the range's rows through a buffer descriptor: rows past the range read 0
-  // (hardware range check), the per-row step is a scalar offset, and each
-  // item needs one 32-bit VGPR offset (64-bit addresses for the 48 prefetched
-  // values would not fit beside the f64 sums)
-  const int nrec = __builtin_amdgcn_readfirstlane(static_cast<int>((r1 > r0 ? r1 - r0 : 0) * D * 4));
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + r0 * D), 0, nrec, 0x00020000);
-  int it_off[kIt];
-#pragma unroll
-  for (int u = 0; u < kIt; ++u) {
-    const int it = tid + kGiNT * u;
-    // padding features / missing items read past the record count: 0
-    it_off[u] = (it < nitems && it_f[u] < D) ? (it_kq[u] * 16 * D + it_f[u]) * 4 : 0x7ffffff0;
-  }
-  float xv[kIt][16];
-  auto load = [&](int c) {
-    if constexpr ((DIAG & 8) != 0) {
-#pragma unroll
-      for (int u = 0; u < kIt; ++u)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(xv[u][j]));
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
-#pragma unroll
-      for (int u = 0; u < kIt; ++u)
-        xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
-    }
-  };
-  // item u of the x values in registers -> digit bytes in LDS buffer `buf`
-  auto load_item = [&](int u, int c) {
-    if constexpr ((DIAG & 8) != 0) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(xv[u][j]));
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int so = __builtin_amdgcn_readfirstlane((c * kGiRows + j) * D * 4);
-      xv[u][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, it_off[u], so, 0));
-    }
-  };
-  auto slice_item = [&](int u, unsigned char* buf) {
-    if constexpr ((DIAG & 4) != 0) return;
-    const int it = tid + kGiNT * u;
-    if (it < nitems) {
-      unsigned w[4][kGiDig];  // [row group g][plane]
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        gi_planes(gi_vbias(xv[u][4 * g + 0], it_e[u]), gi_vbias(xv[u][4 * g + 1], it_e[u]),
-                  gi_vbias(xv[u][4 * g + 2], it_e[u]), gi_vbias(xv[u][4 * g + 3], it_e[u]), w[g]);
-      const int f = it_f[u], slot = it_kq[u] ^ gi_swz(f);
-#pragma unroll
-      for (int a = 0; a < kGiDig; ++a)
-        *reinterpret_cast<uint4*>(buf + ((a * kGiF + f) * 4 + slot) * 16) =
-            make_uint4(w[0][a], w[1][a], w[2][a], w[3][a]);
-    }
-  };
-  constexpr int kBuf = kGiDig * kGiF * kGiRows;  // bytes of one chunk's digits
-
-  // Double-buffered digits (2 x 80 KB): chunk c's MFMAs read buffer c & 1
-  // while this wave slices chunk c + 1 (x already in registers) into the
-  // other buffer, and the loads of chunk c + 2 are in flight.  One barrier per
-  // chunk: it publishes chunk c + 1's digits and retires every read of the
-  // buffer the next iteration overwrites.
-  if (nchunks > 0) {
-    load(0);
-#pragma unroll
-    for (int u = 0; u < kIt; ++u) slice_item(u, s_dig);
-    if (nchunks > 1) load(1);
-  }
-  __syncthreads();
-  const int lf = lane & 15, lsl = lane >> 4;
-  for (int c = 0; c < nchunks; ++c) {
-    const unsigned char* cur = s_dig + (c & 1) * kBuf;
-    unsigned char* nxt = s_dig + ((c + 1) & 1) * kBuf;
-    const bool more = c + 1 < nchunks;
-    // lane l: feature (l & 15) of the tile's block, 16 rows of slot (l >> 4)
-    i32x4 A[kGiDig];
-#pragma unroll
-    for (int q = 0; q < kGiMaxTiles; ++q) {
-      if (q < ntl) {
-        if (q == 0 || ti[q] != ti[q - 1]) {  // the row block changes (wave-uniform)
-          const int fa = ti[q] * 16 + lf;
-#pragma unroll
-          for (int a = 0; a < kGiDig; ++a)
-            A[a] = *reinterpret_cast<const i32x4*>(cur + ((a * kGiF + fa) * 4 + (lsl ^ gi_swz(fa))) * 16);
-        }
-        const int fb = tj[q] * 16 + lf;
-        i32x4 B[kGiDig];
-#pragma unroll
-        for (int a = 0; a < kGiDig; ++a)
-          B[a] = *reinterpret_cast<const i32x4*>(cur + ((a * kGiF + fb) * 4 + (lsl ^ gi_swz(fb))) * 16);
-        const i32x4 z = {0, 0, 0, 0};
-        if constexpr ((DIAG & 1) != 0) {
-#pragma unroll
-          for (int a = 0; a < kGiDig; ++a) asm volatile("" ::"v"(A[a]), "v"(B[a]));
-        } else {
-        i32x4 H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[0], z, 0, 0, 0);
-        H <<= 8;
-        H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[1], H, 0, 0, 0);
-        H = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[0], H, 0, 0, 0);
-        i32x4 M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[2], z, 0, 0, 0);
-        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[1], M, 0, 0, 0);
-        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[0], M, 0, 0, 0);
-        M <<= 8;
-        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[3], M, 0, 0, 0);
-        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[2], M, 0, 0, 0);
-        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[1], M, 0, 0, 0);
-        M = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3], B[0], M, 0, 0, 0);
-        i32x4 Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[3], z, 0, 0, 0);
-        Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[2], Lo, 0, 0, 0);
-        Lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[3], B[1], Lo, 0, 0, 0);
-        if constexpr ((DIAG & 2) != 0) {
-          asm volatile("" ::"v"(H), "v"(M), "v"(Lo));
-        } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[q][e] = fma(static_cast<double>(H[e]), 0x1p-20, acc[q][e]);
-          acc[q][e] = fma(static_cast<double>(M[e]), 0x1p-36, acc[q][e]);
-          acc[q][e] = fma(static_cast<double>(Lo[e]), 0x1p-44, acc[q][e]);
-        }
-        }
-        }
-      }
-      // slicing of the next chunk spread between the tiles (item u after
-      // tile 4u + 3): VALU work beside the MFMAs in flight
-      if (more && (q & 3) == 3 && (q >> 2) < kIt) slice_item(q >> 2, nxt);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (c + 2 < nchunks) load(c + 2);
-    __syncthreads();
-  }
-  // partials in gram_tri_kernel's layout, scaled by 2^(e_i + e_j) (exact):
-  // C/D map of the 16x16 integer MFMA: row 4 (lane >> 4) + e, column lane & 15
-  double* pr = part + static_cast<int64_t>(range) * T * 256;
-  const int lc = lane & 15, lr = 4 * (lane >> 4);
-#pragma unroll
-  for (int q = 0; q < kGiMaxTiles; ++q) {
-    if (q < ntl) {
-      const int fj = tj[q] * 16 + lc;
-      const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
-      const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int fi = ti[q] * 16 + lr + e;
-        const int ei = fi < D ? gi_exp(colmax[fi]) : 0;
-        // a non-finite column bound (NaN / inf in x) makes its Gram rows and
-        // columns NaN, as the f64 Gram of such rows would be
-        const bool bad = (fi < D && !isfinite(__uint_as_float(colmax[fi]))) || !okj;
-        pr[static_cast<int64_t>(q0 + q) * 256 + (lr + e) * 16 + lc] =
-            bad ? __builtin_nan("") : ldexp(acc[q][e], ei + ej);
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------ Gram i8, range level sums (r05)
@@ -862,212 +644,6 @@ __global__ __launch_bounds__(S::kNT) void gram_i8l_kernel(const float* __restric
   for (int q = 0; q < MT; ++q) {
     if (q < ntl) {
       const int tau = ti[q] * nt - ti[q] * (ti[q] - 1) / 2 + (tj[q] - ti[q]);  // row-major triangle
-      const int fj = tj[q] * 16 + lc;
-      const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
-      const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int fi = ti[q] * 16 + lr + e;
-        const int ei = fi < D ? gi_exp(colmax[fi]) : 0;
-        const bool bad = (fi < D && !isfinite(__uint_as_float(colmax[fi]))) || !okj;
-        double sum = static_cast<double>(lev[q][0][e]);
-#pragma unroll
-        for (int l = 1; l < kGlLev; ++l) sum = fma(sum, 256.0, static_cast<double>(lev[q][l][e]));
-        pr[static_cast<int64_t>(tau) * 256 + (lr + e) * 16 + lc] =
-            bad ? __builtin_nan("") : ldexp(sum, ei + ej - 44);
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------ Gram i8, x staged in LDS (r05, tools build)
-// gram_i8l_kernel's digits, parts, tiles and level sums, but x reaches LDS by
-// buffer_load ... lds (16 bytes a lane, no VGPR destination) two chunks ahead
-// into two stages, the digit buffer is indexed by the part's own features (two
-// of the three groups: <= kGsF at d <= 304), and each chunk is sliced by every
-// wave from its stage, then multiplied (one digit buffer: 53 KB digits + 2 x
-// 53 KB stages).  The x prefetch registers of gram_i8l_kernel (32 per thread)
-// are gone; the loads stay in flight across the raw barriers (counted vmcnt).
-constexpr int kGsF = 208;                          // a part's features at most
-constexpr int kGsBuf = kGiDig * kGsF * kGiRows;    // one chunk's digits (bytes)
-constexpr int kGsStage = kGiRows * kGsF * 4;       // one chunk's x (bytes)
-constexpr size_t kGsLds = kGsBuf + 2 * static_cast<size_t>(kGsStage);
-
-template <int DIAG, class S>
-__global__ __launch_bounds__(S::kNT) void gram_i8s_kernel(const float* __restrict__ x,
-                                                         const unsigned* __restrict__ colmax,
-                                                         int64_t N, int D, int nt, int64_t chunk,
-                                                         int xcd_map, GlParts parts,
-                                                         double* __restrict__ part) {
-  constexpr int MT = S::kMT, NT = S::kNT, kIt = S::kIt, NW = S::kNW;
-  // ALL of the kernel's LDS in this one array (a second __shared__ object can
-  // make the compiler wait vmcnt(0) before LDS reads: cdna_hip_programming.md)
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_gs[];
-  unsigned char* const dig = s_gs;
-  float* const stage0 = reinterpret_cast<float*>(s_gs + kGsBuf);
-  float* const stage1 = reinterpret_cast<float*>(s_gs + kGsBuf + kGsStage);
-  int range, p;
-  if (xcd_map) {
-    const int b = blockIdx.x, sx = b >> 3;
-    range = (b & 7) + 8 * (sx / S::kP);
-    p = sx % S::kP;
-  } else {
-    range = blockIdx.x / S::kP;
-    p = blockIdx.x % S::kP;
-  }
-  const GlPart& pt = parts.p[p];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int npt = pt.n;
-  if (npt <= 0) return;
-  const int f0 = pt.f0, n0 = pt.n0, f1 = pt.f1;
-  const int nf = n0 + pt.n1;  // <= kGsF, a multiple of 4 (the launcher checks)
-  auto loc = [&](int f) { return f < f0 + n0 ? f - f0 : n0 + f - f1; };
-  const int per = (npt + NW - 1) / NW;
-  const int q0 = wave * per;
-  int ti[MT], tj[MT], la[MT], lb[MT];
-  int ntl = 0;
-#pragma unroll
-  for (int q = 0; q < MT; ++q) {
-    ti[q] = tj[q] = 0;
-    if (q < per && q0 + q < npt) {
-      const int t = pt.tile[q0 + q];
-      ti[q] = t & 255;
-      tj[q] = t >> 8;
-      ntl = q + 1;
-    }
-    la[q] = loc(16 * ti[q]);
-    lb[q] = loc(16 * tj[q]);
-  }
-  i32x4 lev[MT][kGlLev];
-#pragma unroll
-  for (int q = 0; q < MT; ++q)
-#pragma unroll
-    for (int l = 0; l < kGlLev; ++l) lev[q][l] = i32x4{0, 0, 0, 0};
-
-  const int64_t r0 = range * chunk;
-  const int64_t r1 = min(N, r0 + chunk);
-  const int nrows = static_cast<int>(r1 > r0 ? r1 - r0 : 0);
-  const int nchunks = (nrows + kGiRows - 1) / kGiRows;
-  // items it = tid + NT u: local feature k = it % nf, 16-row slot kq = it / nf
-  const int nitems = nf * 4;
-  int it_k[kIt], it_kq[kIt], it_e[kIt];
-  bool it_ok[kIt], it_v[kIt];
-#pragma unroll
-  for (int u = 0; u < kIt; ++u) {
-    const int it = tid + NT * u;
-    it_ok[u] = it < nitems;
-    it_k[u] = it_ok[u] ? it % nf : 0;
-    it_kq[u] = it_ok[u] ? it / nf : 0;
-    const int k = it_k[u];
-    const int f = k < n0 ? f0 + k : f1 + k - n0;
-    it_v[u] = it_ok[u] && f < D;  // padding features (f >= D) slice as 0
-    it_e[u] = it_v[u] ? gi_exp(colmax[f]) : 0;
-  }
-  const int nrec = __builtin_amdgcn_readfirstlane(nrows * D * 4);
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + r0 * D), 0, nrec, 0x00020000);
-  // chunk c into a stage: float4 unit v = 64 i + lane of its [64][nf] rows
-  // (instruction i = wave, wave + NW, ..., lane-linear 1 KB each); rows past
-  // the range read 0, features past d read the next row (never sliced)
-  const int nq = nf / 4;
-  const int my_dma = (nq - wave + NW - 1) / NW;  // this wave's instructions per chunk
-  auto dma = [&](int c, float* stg) {
-    if constexpr ((DIAG & 8) != 0) return;
-    for (int i = wave; i < nq; i += NW) {
-      const int v = 64 * i + lane;
-      const int row = v / nq, col = 4 * (v - row * nq);
-      const int f = col < n0 ? f0 + col : f1 + col - n0;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsrc, (__attribute__((address_space(3))) void*)(stg + 256 * i), 16,
-          ((c * kGiRows + row) * D + f) * 4, 0, 0, 0);
-    }
-  };
-  // wait for this wave's DMAs of the chunk before the newest `younger` ones
-  auto wait_older = [&](int younger) {
-    if (younger >= 7)
-      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else if (younger == 6)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  auto barrier = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  auto slice_item = [&](int u, const float* stg, int rows_left) {
-    if constexpr ((DIAG & 4) != 0) return;
-    if (it_ok[u]) {
-      const int k = it_k[u], kq = it_kq[u], e = it_e[u];
-      // every load issued, then masked (a per-element branch around each
-      // load waited for it: 16 dependent LDS round trips)
-      const int live = it_v[u] ? min(rows_left - 16 * kq, 16) : 0;
-      float xv[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) xv[j] = stg[(16 * kq + j) * nf + k];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) xv[j] = j < live ? xv[j] : 0.f;
-      unsigned w[4][kGiDig];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        gi_planes(gi_vbias(xv[4 * g + 0], e), gi_vbias(xv[4 * g + 1], e), gi_vbias(xv[4 * g + 2], e),
-                  gi_vbias(xv[4 * g + 3], e), w[g]);
-      const int slot = kq ^ gi_swz(k);
-#pragma unroll
-      for (int a = 0; a < kGiDig; ++a)
-        *reinterpret_cast<uint4*>(dig + ((a * kGsF + k) * 4 + slot) * 16) =
-            make_uint4(w[0][a], w[1][a], w[2][a], w[3][a]);
-    }
-  };
-  const int lf = lane & 15, lsl = lane >> 4;
-  auto rd = [&](int fl, int a) {
-    return *reinterpret_cast<const i32x4*>(dig + ((a * kGsF + fl) * 4 + (lsl ^ gi_swz(fl))) * 16);
-  };
-
-  if (nchunks > 0) dma(0, stage0);
-  if (nchunks > 1) dma(1, stage1);
-  for (int c = 0; c < nchunks; ++c) {
-    float* stg = (c & 1) ? stage1 : stage0;
-    wait_older(c + 1 < nchunks ? my_dma : 0);  // this wave's chunk-c DMAs have landed
-    barrier();  // every wave's chunk c is in the stage; chunk c - 1's MFMA reads are done
-#pragma unroll
-    for (int u = 0; u < kIt; ++u) slice_item(u, stg, nrows - c * kGiRows);
-    barrier();  // the digits are complete; the stage is free
-    if (c + 2 < nchunks) dma(c + 2, stg);
-#pragma unroll
-    for (int q = 0; q < MT; ++q) {
-      if (q < ntl) {
-        i32x4 A[kGiDig], Bd[kGiDig];
-#pragma unroll
-        for (int a = 0; a < kGiDig; ++a) A[a] = rd(la[q] + lf, a);
-#pragma unroll
-        for (int b = 0; b < kGiDig; ++b) Bd[b] = rd(lb[q] + lf, b);
-#pragma unroll
-        for (int b = 0; b < kGiDig; ++b) {
-          if constexpr ((DIAG & 1) != 0) {
-            asm volatile("" ::"v"(Bd[b]));
-          } else {
-#pragma unroll
-            for (int a = 0; a < kGiDig; ++a)
-              if (a + b < kGlLev)
-                lev[q][a + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[a], Bd[b], lev[q][a + b], 0, 0, 0);
-          }
-        }
-        if constexpr ((DIAG & 1) != 0) {
-#pragma unroll
-          for (int a = 0; a < kGiDig; ++a) asm volatile("" ::"v"(A[a]));
-        }
-      }
-    }
-  }
-  // the range's partials, as gram_i8l_kernel
-  const int T = nt * (nt + 1) / 2;
-  double* pr = part + static_cast<int64_t>(range) * T * 256;
-  const int lc = lane & 15, lr = 4 * (lane >> 4);
-#pragma unroll
-  for (int q = 0; q < MT; ++q) {
-    if (q < ntl) {
-      const int tau = ti[q] * nt - ti[q] * (ti[q] - 1) / 2 + (tj[q] - ti[q]);
       const int fj = tj[q] * 16 + lc;
       const int ej = fj < D ? gi_exp(colmax[fj]) : 0;
       const bool okj = fj >= D || isfinite(__uint_as_float(colmax[fj]));
@@ -2245,27 +1821,21 @@ __global__ __launch_bounds__(kP16NT) void pc_solve16_kernel(const double* __rest
 // the caller first hands ws over; workgroup 0 returns the counter to zero
 // once every workgroup has made its last arrival, so a launch -- eager or a
 // graph replay -- leaves ws ready for the next one).
-#ifdef MMB_DIAG  // the r04 kernel's (pc_solve_mc_v1_kernel) wave split
-constexpr int kPmPw = 15;  // waves holding G (wave 15 runs the Cholesky meanwhile)
-constexpr int kPmKs = 6;   // k-steps of G per wave: ceil(kP16MaxD / 4 / kPmPw)
-#endif
 constexpr int kPmMaxT = kP16MaxD / 16;  // tiles (20)
 
-#ifdef MMB_DIAG
-// tools build: a test shortens the bounded waits (mmb_diag_pc_wait_iters) and
+// tools/diag: a test shortens the bounded waits (mmb_diag_pc_wait_iters) and
 // names one workgroup that never arrives (mmb_diag_pc_skip_arrival), so the
 // count a wait polls for cannot be reached whatever the arrival skew: the
 // timeout path runs deterministically
-__device__ int g_pm_wait_iters = 1 << 20;
-__device__ int g_pm_skip_wg = -1;
+#ifndef MMB_HOOK_PM_WAIT_ITERS
+#define MMB_HOOK_PM_WAIT_ITERS (1 << 20)
+#endif
+#ifndef MMB_HOOK_PM_SKIP_ARRIVAL
+#define MMB_HOOK_PM_SKIP_ARRIVAL false
 #endif
 __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned* abort_w,
                                         int32_t* flag) {
-#ifdef MMB_DIAG
-  const int iters = g_pm_wait_iters;
-#else
-  constexpr int iters = 1 << 20;
-#endif
+  const int iters = MMB_HOOK_PM_WAIT_ITERS;
   for (int it = 0; it < iters; ++it) {
     // the abort word first: a set word (another workgroup gave up, or a
     // workspace handed over dirty) ends the wait even where the count is met
@@ -2289,9 +1859,7 @@ __device__ __forceinline__ bool pm_wait(unsigned* ctr, unsigned target, unsigned
 // waits pass before the other workgroups' tiles are written.
 __device__ __forceinline__ bool pm_arrive(unsigned* ctr, int T, int r, unsigned* abort_w,
                                           int32_t* flag) {
-#ifdef MMB_DIAG
-  if (static_cast<int>(blockIdx.x) == g_pm_skip_wg) return true;  // never arrives
-#endif
+  if (MMB_HOOK_PM_SKIP_ARRIVAL) return true;  // (tools/diag) never arrives
   const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old >= static_cast<unsigned>(T * r) && old < static_cast<unsigned>(T * (r + 1))) return true;
   __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2360,267 +1928,6 @@ __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* 
   wave_lds_sync();
   PC_WMARK(34);
 }
-
-#ifdef MMB_DIAG
-// The r03-r04 round (tools build, MMB_PC_SOLVE_V1=1 for A/B runs): the
-// Cholesky of W_r on wave 15 beside the partials of G_t B_r, then the
-// exchange of Y_t = G_t B_r M_r^T and P_t = Y_t^T Y_t -- the factor (~5.5 us
-// of a ~11 us round) and the exchange (~4.5 us) in sequence.
-__global__ __launch_bounds__(kP16NT) void pc_solve_mc_v1_kernel(const double* __restrict__ G, int D,
-                                                                  const double* __restrict__ z0, int k,
-                                                                  int npc, int n_iter, int transposed,
-                                                                  double* __restrict__ pc_out,
-                                                                  double* xbuf, unsigned* ctl,
-                                                                  int32_t* flag) {
-  extern __shared__ __attribute__((aligned(16))) double p16_lds[];
-  const int Dp = (D + 15) / 16 * 16;
-  const int T = Dp / 16;
-  double* sZ = p16_lds;               // the orthonormal block (explicit rounds)
-  double* sY = sZ + Dp * kP16W;       // the raw block B_r (z0, then G Z_{r-1})
-  double* part = sY + Dp * kP16W;     // max(16 x 256, Dp x 16)
-  P16_SMALL_DECL
-  __shared__ double sHt[256], sYt[256], sPt[256], sM[256], sM2[256], sd[kMaxK];
-  __shared__ int s_abort;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int t = blockIdx.x;
-  unsigned* ctr = ctl;
-  unsigned* abort_w = ctl + 1;
-
-  // this workgroup's 16 rows of G as MFMA A fragments on waves 0-14 (G
-  // symmetric: row p of the tile = column p, 16 consecutive doubles per k-row:
-  // coalesced); wave 15 is free for the k x k work that overlaps the product
-  double ga[kPmKs];
-  {
-    const int p = t * 16 + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < kPmKs; ++j) {
-      const int q = 4 * (wave + kPmPw * j) + (lane >> 4);
-      ga[j] = (wave < kPmPw && p < D && q < D) ? G[static_cast<int64_t>(q) * D + p] : 0.0;
-    }
-  }
-  // waves 0-14: their partial products of this tile of G with a [Dp][16] block
-  auto tile_partials = [&](const double* B) {
-    if (wave < kPmPw) {
-      f64x4 acc = {0, 0, 0, 0};
-#pragma unroll
-      for (int j = 0; j < kPmKs; ++j) {
-        const int q = 4 * (wave + kPmPw * j) + (lane >> 4);
-        if (4 * (wave + kPmPw * j) < Dp)
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ga[j], B[q * kP16W + (lane & 15)], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) part[wave * 256 + ((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
-    }
-  };
-  // ... summed over the waves in a fixed order (after a barrier)
-  auto tile_sum = [&](double* out) {
-    if (tid < 256) {
-      double s = 0.0;
-#pragma unroll
-      for (int w = 0; w < kPmPw; ++w) s += part[w * 256 + tid];
-      out[tid] = s;
-    }
-    __syncthreads();
-  };
-  auto tile_product = [&](const double* B, double* out) {
-    tile_partials(B);
-    __syncthreads();
-    tile_sum(out);
-  };
-  // MGS^2 of the k columns of a [Dp][16] block on wave 0 (extreme
-  // ill-conditioning: a Cholesky pivot <= 0), in place
-  auto mgs = [&](double* B) {
-    if (wave == 0) {
-      for (int e = lane; e < D * k; e += kWave) part[e] = B[(e / k) * kP16W + e % k];
-      wave_lds_sync();
-      orth_wave(part, D, k, lane);
-      for (int e = lane; e < D * k; e += kWave) B[(e / k) * kP16W + e % k] = part[e];
-    }
-    __syncthreads();
-  };
-
-  for (int e = tid; e < Dp * kP16W; e += kP16NT) {
-    const int p = e / kP16W, j = e % kP16W;
-    sY[e] = (p < D && j < k) ? z0[p * k + j] : 0.0;
-    sZ[e] = 0.0;
-  }
-  if (tid == 0) s_abort = 0;
-  __syncthreads();
-  PC_MARK(0);
-  p16_gram(sY, sY, Dp, k, part, sW);  // W_0 = B_0^T B_0 (every workgroup: identical)
-  PC_MARK(1);
-
-  // Round r: the raw block B_r (sY) and its Gram W_r (sW) -> Z_r = orth(B_r)
-  // -> this tile of G Z_r -> exchange -> B_{r+1}, W_{r+1}.  Rounds r <
-  // n_iter orthonormalise implicitly: Z_r = B_r M^T, so G_t Z_r = (G_t B_r)
-  // M^T and no row of Z_r is formed.  Round n_iter (the block entering the
-  // Rayleigh-Ritz tail) forms Z explicitly with CholeskyQR2.
-  for (int r = 0; r <= n_iter; ++r) {
-    const bool last = r == n_iter;
-    // the equilibrated Cholesky of W on wave 15 while waves 0-14 form this
-    // tile's partial products with the raw block B (G_t B: all the implicit
-    // path needs before M)
-    if (wave == kPmPw) {
-      p16_eq_chol(sW, sL, sLi, sM, sd, k, lane, &s_fail);
-    } else {
-      tile_partials(sY);
-    }
-    __syncthreads();
-    PC_MARK(44 + 2 * r);
-    // explicit rows: a failed pivot (MGS^2), or the block entering the
-    // transposed branch's tail (an orthonormal Q: CholeskyQR2).  The direct
-    // branch's tail is a generalised eigenproblem on span(Z), invariant to
-    // the basis, so its last block stays implicit; workgroup 0 forms its
-    // rows for the tail.
-    const bool explicit_z = (last && transposed) || s_fail;
-    if (last && !explicit_z && t == 0) p16_rmul(sY, sM, sZ, Dp);  // Z = B M^T
-    if (explicit_z) {
-      if (s_fail) {  // the equilibrated rows, orthonormalised by MGS^2
-        for (int e = tid; e < D * kP16W; e += kP16NT) sZ[e] = sY[e] * (e % kP16W < k ? sd[e % kP16W] : 0.0);
-        __syncthreads();
-        mgs(sZ);
-      } else {
-        p16_rmul(sY, sM, sZ, Dp);  // Z1 = B M1^T
-        __syncthreads();
-        p16_gram(sZ, sZ, Dp, k, part, sW);  // second CholeskyQR pass on the rows
-        if (wave == 0) {
-          if (lane == 0) s_fail = 0;
-          wave_lds_sync();
-          p16_chol(sW, sL, sLi, k, lane, &s_fail);
-          for (int e = lane; e < 256; e += kWave) {
-            const int j = e / kP16W, m = e % kP16W;
-            sM2[e] = (j < k && m <= j) ? sLi[j * k + m] : 0.0;
-          }
-        }
-        __syncthreads();
-        if (s_fail) {
-          mgs(sZ);
-        } else {
-          p16_rmul(sZ, sM2, sY, Dp);  // Z = Z1 L2^-T (sY free: B is no longer needed)
-          __syncthreads();
-          for (int e = tid; e < Dp * kP16W; e += kP16NT) sZ[e] = sY[e];
-          __syncthreads();
-        }
-      }
-      tile_product(sZ, sYt);  // Y_t = G_t Z
-    } else {
-      tile_sum(sHt);    // H_t = G_t B_r (its partials formed beside the Cholesky)
-      if (wave == 0) {  // Y_t = H_t M^T
-        f64x4 acc = {0, 0, 0, 0};
-#pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          const int m = 4 * st + (lane >> 4);
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sHt[(lane & 15) * 16 + m], sM[(lane & 15) * 16 + m],
-                                                     acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) sYt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = acc[reg];
-      }
-    }
-    PC_MARK(45 + 2 * r);
-    // wave 0: P_t = Y_t^T Y_t, then publishes Y_t | P_t with write-through
-    // 8-byte stores, drains them and adds one arrival
-    double* xb = xbuf + static_cast<int64_t>(r & 1) * T * 512;
-    if (wave == 0) {
-      wave_lds_sync();
-      f64x4 pa = {0, 0, 0, 0};
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const double y = sYt[(4 * st + (lane >> 4)) * 16 + (lane & 15)];
-        pa = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, pa, 0, 0, 0);
-      }
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) sPt[((lane >> 4) + 4 * reg) * 16 + (lane & 15)] = pa[reg];
-      wave_lds_sync();
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = lane + kWave * u;
-        const double v = e < 256 ? sYt[e] : sPt[e - 256];
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(xb + t * 512 + e),
-                           __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) {
-        // release: the tile stores above are visible at agent scope before
-        // the arrival that announces them
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (!pm_arrive(ctr, T, r, abort_w, flag)) {
-          s_abort = 1;
-        } else if (!(last && t != 0)) {
-          if (!pm_wait(ctr, static_cast<unsigned>(T * (r + 1)), abort_w, flag)) {
-            s_abort = 1;
-          } else if (last) {
-            // every workgroup has made its last arrival: the counter is free
-            // again, so the next launch (eager or a graph replay) finds it at
-            // 0 with no memset node in front of it
-            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          // acquire: the gather below reads the other workgroups' tiles only
-          // after their arrivals were observed (the __syncthreads that follows
-          // releases the other waves of this workgroup)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-      }
-    }
-    if (last && t != 0) return;  // the tail runs on workgroup 0 only
-    PC_MARK(2 + 3 * r);
-    __syncthreads();
-    if (s_abort) {
-      // no caller may go on with a stale PC: an aborted solve leaves NaN in
-      // pc_out (every aborting workgroup writes the same NaNs; workgroup 0
-      // cannot complete the tail once any workgroup has left)
-      for (int e = tid; e < npc * D; e += kP16NT) pc_out[e] = __builtin_nan("");
-      return;
-    }
-    PC_MARK(3 + 3 * r);
-    // gather every tile into sY and the partial Grams: all of a thread's
-    // loads (sc1, 8 B: the table's first row) issued before any is used
-    // (a load-then-store loop waited ~1.5 us per load), then W = sum_t P_t
-    // as four strided partial sums combined in a fixed order
-    {
-      const int e = tid & 255, g = tid >> 8;  // element, tile group (tiles g, g + 4, ..)
-      double yv[kPmMaxT / 4], pv[kPmMaxT / 4];
-#pragma unroll
-      for (int u = 0; u < kPmMaxT / 4; ++u) {
-        const int tt = g + 4 * u;
-        unsigned long long* src = reinterpret_cast<unsigned long long*>(xb + tt * 512 + e);
-        yv[u] = tt < T ? __builtin_bit_cast(double, __hip_atomic_load(src, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT))
-                       : 0.0;
-        pv[u] = tt < T ? __builtin_bit_cast(double, __hip_atomic_load(src + 256, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_AGENT))
-                       : 0.0;
-      }
-      double ps = 0.0;
-#pragma unroll
-      for (int u = 0; u < kPmMaxT / 4; ++u) {
-        const int tt = g + 4 * u;
-        if (tt < T) {
-          sY[(tt * 16 + (e >> 4)) * kP16W + (e & 15)] = yv[u];
-          ps += pv[u];
-        }
-      }
-      part[g * 256 + e] = ps;
-    }
-    __syncthreads();
-    if (tid < 256) {
-      const double s = (part[tid] + part[256 + tid]) + (part[512 + tid] + part[768 + tid]);
-      const int i = tid >> 4, j = tid & 15;
-      if (i < k && j < k) sW[i * k + j] = s;  // W_{r+1}; after the last round H = Y^T Y
-    }
-    __syncthreads();
-    PC_MARK(4 + 3 * r);
-  }
-  // workgroup 0: sZ = the final block, sY = G Z, sW = (G Z)^T (G Z)
-  for (int e = tid; e < k * k; e += kP16NT) sT[e] = sW[e];
-  __syncthreads();
-  PC_MARK(40);
-  p16_tail(sZ, sY, D, Dp, k, npc, transposed, part, sm, pc_out, sT);
-  PC_PROBE_FLUSH();
-}
-#endif  // MMB_DIAG
 
 // G2 = G G for the multi-workgroup solve's squared rounds (r06): one
 // upper-triangle 16 x 16 tile (a <= b) per 4 waves, which split the MFMA
@@ -3406,14 +2713,10 @@ __global__ __launch_bounds__(256) void pc_remove1_kernel(const float* __restrict
 // pc_remove1_kernel rows per wave (2, 4, 8); 0 = pc_remove_kernel.  Measured
 // (tools/remove_ab.py, 1M x 300, r02q): R = 0 / 2 / 4 / 8 = 0.529 / 0.455 /
 // 0.435 / 0.444 ms, all bit-identical
-static int remove_rows() {
-#ifdef MMB_DIAG
-  const char* e = getenv("MMB_PC_REMOVE_R");
-  return e ? atoi(e) : 4;
-#else
-  return 4;
+#ifndef MMB_HOOK_PC_REMOVE_R  // (tools/diag: MMB_PC_REMOVE_R)
+#define MMB_HOOK_PC_REMOVE_R 4
 #endif
-}
+static int remove_rows() { return MMB_HOOK_PC_REMOVE_R; }
 
 template <int VEC, int PER, typename TX = float>
 static int launch_remove(const TX* num, const float* cnt, int64_t n, int d, const double* pc,
@@ -3503,35 +2806,6 @@ static bool gram2_ok(const float* num, int d) {
 }
 
 
-template <int DIAG>
-static size_t gram_i8_lds() {
-  const size_t lds = 2 * kGiDig * kGiF * kGiRows;  // 160 KB: double-buffered digits
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8_kernel<DIAG>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr = true;
-  }
-  return lds;
-}
-
-template <int DIAG>
-static void launch_gram_i8(const float* x, const uint32_t* colmax, int64_t n, int d,
-                           const Gram2Plan& q, double* part, hipStream_t stream) {
-  gram_i8_kernel<DIAG><<<2 * q.R, kGiNT, gram_i8_lds<DIAG>(), stream>>>(x, colmax, n, d, q.nt, q.R,
-                                                                        q.chunk, q.xcd, part);
-}
-
-#ifdef MMB_DIAG
-static int gram_i8_diag() {  // timing-only ablations (MMB_GRAM_DIAG), re-read per launch
-  const char* e = getenv("MMB_GRAM_DIAG");
-  return e ? atoi(e) : 0;
-}
-static bool gram_i8_v1() {  // the round-4 kernel (per-k-step f64 updates) for A/B runs
-  const char* e = getenv("MMB_GRAM_I8_V1");
-  return e && atoi(e) != 0;
-}
-#endif
 
 // ---- level-sum int8 Gram (gram_i8l_kernel): plan and parts
 struct GramLPlan {
@@ -3691,9 +2965,8 @@ static GramLPlan gram_i8l_plan(int64_t n, int d) {
   q.T = q.nt * (q.nt + 1) / 2;
   q.P = S::kP;
   q.R = gram_i8l_ranges(n, S::kP);
-#ifdef MMB_DIAG
-  if (const char* e = getenv("MMB_GRAM_RANGES"); e && atoi(e) > 0)  // A/B: ranges (<= 128)
-    q.R = std::max<int>(q.R, std::min(atoi(e), 128));
+#ifdef MMB_HOOK_GRAM_RANGES  // (tools/diag: MMB_GRAM_RANGES, A/B runs of the range count)
+  MMB_HOOK_GRAM_RANGES(q.R);
 #endif
   q.xcd = (q.R % 8 == 0) ? 1 : 0;
   q.chunk = ceil_div(ceil_div(std::max<int64_t>(n, 1), q.R), kGiRows) * kGiRows;
@@ -3743,61 +3016,6 @@ static int gram_i8l_block(const float* x, const uint32_t* colmax, int64_t n, int
   return MMB_OK;
 }
 
-// The staged kernel on one block of rows (shape S, feature-group parts of
-// <= kGsF features each), then the range reduction.
-template <int DIAG, class S>
-static int gram_i8s_block(const float* x, const uint32_t* colmax, int64_t n, int d, double* g,
-                          int accumulate, double* part, hipStream_t stream) {
-  const GramLPlan q = gram_i8l_plan<S, true>(n, d);
-  int tiles = 0;
-  for (int k = 0; k < q.P; ++k) {
-    const GlPart& pk = q.parts.p[k];
-    MMB_REQUIRE(pk.n <= S::kPartMax);
-    MMB_REQUIRE(pk.n0 + pk.n1 <= kGsF && (pk.n0 + pk.n1) % 4 == 0 && pk.n0 % 16 == 0);
-    MMB_REQUIRE((pk.n0 + pk.n1) * 4 <= S::kIt * S::kNT);
-    tiles += pk.n;
-  }
-  MMB_REQUIRE(tiles == q.T);
-  MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gram_i8s_kernel<DIAG, S>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kGsLds));
-    attr = true;
-  }
-  gram_i8s_kernel<DIAG, S><<<S::kP * q.R, S::kNT, kGsLds, stream>>>(x, colmax, n, d, q.nt, q.chunk,
-                                                                    q.xcd, q.parts, part);
-  MMB_LAUNCH_CHECK();
-  const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
-  if (rc != MMB_OK) return rc;
-  MMB_LAUNCH_CHECK();
-  return MMB_OK;
-}
-
-#ifdef MMB_DIAG
-// tools build: the level-sum kernel's shape (MMB_GRAM_I8_SHAPE: 0 the
-// product's three feature-group parts x 8 waves x 8 tiles, 1 four triangle
-// runs x 8 waves x 6 tiles, 2 three triangle runs x 8 waves x 8 tiles, 3 the
-// product with LDS reads free to cross tiles, 4 the product with the next
-// tile's first B digit prefetched, 5 the product without the staggered
-// slicing, 6 x staged in LDS by DMA: gram_i8s_kernel) and its timing-only
-// ablations
-static int gram_i8_shape() {
-  const char* e = getenv("MMB_GRAM_I8_SHAPE");
-  return e ? atoi(e) : 0;
-}
-template <class S, bool GROUPS>
-static int gram_i8l_block_diag(const float* x, const uint32_t* colmax, int64_t n, int d,
-                               double* g, int accumulate, double* part, hipStream_t stream) {
-  switch (gram_i8_diag()) {
-    case 1: return gram_i8l_block<1, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
-    case 4: return gram_i8l_block<4, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
-    case 12: return gram_i8l_block<12, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
-    case 13: return gram_i8l_block<13, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
-    default: return gram_i8l_block<0, S, GROUPS>(x, colmax, n, d, g, accumulate, part, stream);
-  }
-}
-#endif
 
 }  // namespace mmb
 
@@ -3871,26 +3089,13 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
                            int accumulate, void* ws, hipStream_t stream) {
   MMB_REQUIRE(x && colmax && g && ws && n >= 0 && d > 0 && d <= 304 && d % 4 == 0);
   double* part = static_cast<double*>(ws);
-#ifdef MMB_DIAG
-  if (gram_i8_v1()) {  // the round-4 kernel (tools build only)
-    const Gram2Plan q = gram_i8_plan(n, d);
-    MMB_REQUIRE((q.T + 1) / 2 <= kGiMaxTiles * (kGiNT / kWave));
-    MMB_REQUIRE(q.chunk * d * 4 < (int64_t{1} << 31));
-    switch (gram_i8_diag()) {
-      case 1: launch_gram_i8<1>(x, colmax, n, d, q, part, stream); break;
-      case 2: launch_gram_i8<2>(x, colmax, n, d, q, part, stream); break;
-      case 4: launch_gram_i8<4>(x, colmax, n, d, q, part, stream); break;
-      case 12: launch_gram_i8<12>(x, colmax, n, d, q, part, stream); break;
-      case 15: launch_gram_i8<15>(x, colmax, n, d, q, part, stream); break;
-      default: launch_gram_i8<0>(x, colmax, n, d, q, part, stream); break;
-    }
-    MMB_LAUNCH_CHECK();
-    const int rc = launch_tri_reduce(part, d, q.nt, q.R, accumulate, g, stream);
-    if (rc != MMB_OK) return rc;
-    MMB_LAUNCH_CHECK();
-    return MMB_OK;
-  }
+#ifndef MMB_HOOK_GRAM_I8  // (tools/diag: MMB_GRAM_I8_V1, the r04 kernel)
+#define MMB_HOOK_GRAM_I8(rc) false
 #endif
+  {
+    int rc_ = MMB_OK;
+    if (MMB_HOOK_GRAM_I8(rc_)) return rc_;
+  }
   // blocks of <= kGlBlockRows rows (<= 128 ranges of <= 32768 rows: int32
   // level sums, at most 128 range partials per reduction); the first block
   // writes (or accumulates into) g, later ones accumulate
@@ -3899,27 +3104,10 @@ extern "C" int mmb_gram_i8(const float* x, const uint32_t* colmax, int64_t n, in
     const int64_t nb = std::min(n - b0, kGlBlockRows);
     const float* xb = x + b0 * d;
     const int acc = accumulate || b0 > 0;
-#ifdef MMB_DIAG
-    int rc;
-    switch (gram_i8_shape()) {
-      case 1: rc = gram_i8l_block_diag<GlShape<4, 8, 6, 3>, false>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 2: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 3>, false>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 3: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0x100, false, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 4: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2, 0, true, true>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 5: rc = gram_i8l_block_diag<GlShape<3, 8, 8, 2>, true>(xb, colmax, nb, d, g, acc, part, stream); break;
-      case 6:  // x staged in LDS (gram_i8s_kernel), the product's parts
-        switch (gram_i8_diag()) {
-          case 1: rc = gram_i8s_block<1, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
-          case 4: rc = gram_i8s_block<4, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
-          case 12: rc = gram_i8s_block<12, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
-          default: rc = gram_i8s_block<0, GlProduct>(xb, colmax, nb, d, g, acc, part, stream); break;
-        }
-        break;
-      default: rc = gram_i8l_block_diag<GlProduct, true>(xb, colmax, nb, d, g, acc, part, stream); break;
-    }
-#else
-    const int rc = gram_i8l_block<0, GlProduct, true>(xb, colmax, nb, d, g, acc, part, stream);
+#ifndef MMB_HOOK_GRAM_I8_BLOCK  // (tools/diag: MMB_GRAM_I8_SHAPE / MMB_GRAM_DIAG)
+#define MMB_HOOK_GRAM_I8_BLOCK gram_i8l_block<0, GlProduct, true>
 #endif
+    const int rc = MMB_HOOK_GRAM_I8_BLOCK(xb, colmax, nb, d, g, acc, part, stream);
     if (rc != MMB_OK) return rc;
     b0 += nb;
   } while (b0 < n);
@@ -4081,29 +3269,13 @@ static int launch_solve_mc(const double* g, int d, const double* z0, int k, int 
   // flag.  Since r05 every arrival checks the count it finds (pm_arrive) and
   // every wait the abort word first, so a dirty workspace aborts with
   // MMB_FLAG_SYNC_TIMEOUT and a NaN PC instead
-#ifdef MMB_DIAG
-  if (const char* e = getenv("MMB_PC_SOLVE_V1"); e && atoi(e) != 0) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_solve_mc_v1_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(p16_lds_bytes(kP16MaxD)));
-    pc_solve_mc_v1_kernel<<<T, kP16NT, p16_lds_bytes(d), stream>>>(g, d, z0, k, npc, n_iter, transposed,
-                                                                   pc_out, xbuf, ctl, flag);
-    MMB_LAUNCH_CHECK();
-    return MMB_OK;
-  }
+#ifndef MMB_HOOK_SOLVE_LAUNCH  // (tools/diag: MMB_PC_SOLVE_V1, the r04 kernel; MMB_PC_ABL ablations)
+#define MMB_HOOK_SOLVE_LAUNCH(rc) false
 #endif
-#ifdef MMB_DIAG
-  if (const char* e = getenv("MMB_PC_ABL"); e && atoi(e) != 0) {
-    const int abl = atoi(e);
-    auto kern = abl == 1 ? pc_solve_mc_kernel<1> : abl == 2 ? pc_solve_mc_kernel<2> : pc_solve_mc_kernel<3>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(p16_lds_bytes(kP16MaxD)));
-    kern<<<T + nsq_wg, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, nsq_wg, d, z0, k, npc, n_iter, transposed,
-                                                         pc_out, xbuf, ctl, flag);
-    MMB_LAUNCH_CHECK();
-    return MMB_OK;
+  {
+    int rc_ = MMB_OK;
+    if (MMB_HOOK_SOLVE_LAUNCH(rc_)) return rc_;
   }
-#endif
   pc_solve_mc_kernel<<<T + nsq_wg, kPnNT, p16_lds_bytes(d), stream>>>(g, g2, nsq_wg, d, z0, k, npc, n_iter,
                                                                         transposed, pc_out, xbuf, ctl, flag);
   MMB_LAUNCH_CHECK();
@@ -4124,17 +3296,10 @@ extern "C" int mmb_pc_remove(const float* num, const float* cnt, int64_t n, int 
   if (v4 && per == 2 && npc == 1 && out32 && rr > 0) {
     const int64_t waves = ceil_div(n, rr);
     const int grid = static_cast<int>(std::min<int64_t>(ceil_div(waves, 4), 256 * 8));
-#ifdef MMB_DIAG
-    const char* nte = getenv("MMB_PC_REMOVE_NT");
-    if (nte && atoi(nte) != 0 && rr == 4) {
-      pc_remove1_kernel<4, true><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
-    } else if (rr == 2) {
-      pc_remove1_kernel<2><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
-    } else if (rr == 8) {
-      pc_remove1_kernel<8><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
-    } else
+#ifndef MMB_HOOK_PC_REMOVE_LAUNCH  // (tools/diag: MMB_PC_REMOVE_NT / MMB_PC_REMOVE_R)
+#define MMB_HOOK_PC_REMOVE_LAUNCH false
 #endif
-    {
+    if (!(MMB_HOOK_PC_REMOVE_LAUNCH))    {
       pc_remove1_kernel<4><<<grid, 256, 0, stream>>>(num, cnt, n, d, pc, out32);
     }
     MMB_LAUNCH_CHECK();
@@ -4197,20 +3362,9 @@ extern "C" int mmb_pc_remove_f64(const double* x, int64_t n, int d, const double
   return MMB_EINVAL;
 }
 
-#ifdef MMB_DIAG
-// tools build: the multi-workgroup solve's bounded-wait budget (1 << 20 in
-// the product)
-extern "C" int mmb_diag_pc_wait_iters(int iters) {
-  MMB_REQUIRE(iters >= 1);
-  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_pm_wait_iters), &iters, sizeof(int));
-  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
-}
-
-// tools build: workgroup wg of the multi-workgroup solve skips its arrivals
-// (-1: none, the product behaviour); every wait of the launch then times out
-extern "C" int mmb_diag_pc_skip_arrival(int wg) {
-  MMB_REQUIRE(wg >= -1);
-  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_pm_skip_wg), &wg, sizeof(int));
-  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
-}
+// the tools build's variant kernels, launches, knobs and entry points
+// (tools/diag/); the product library includes an empty header here
+#ifndef MMB_TOOLS_TAIL_PC
+#define MMB_TOOLS_TAIL_PC "mmb_no_tools.h"
 #endif
+#include MMB_TOOLS_TAIL_PC

@@ -128,7 +128,6 @@ __device__ __forceinline__ void stage_token(const StreamArgs& a, int64_t i, int 
 // token order (wave ballots + a fixed-order prefix over the waves), so the
 // text loop runs over rows that carry new bytes only.  Out-of-range ids
 // (flagged) are dropped: they contribute nothing (sif_functions.py:8-15).
-constexpr int kStageIters = (kTokChunk + kNT - 1) / kNT;
 
 // The text rows of a staged token chunk (workgroup kernels): row slot rT
 // of the chunk's nkeep kept tokens, CT column units of VT floats at cT.
@@ -1347,14 +1346,9 @@ __global__ __launch_bounds__(1024) void colmax_reduce_kernel(const float* __rest
 // the default variant compiled for two waves per SIMD (amdgpu_waves_per_eu).
 // The sweep knobs (this one, MMB_STREAM_GRID_MULT, the fused kernel's
 // MMB_FUSED_*, the projection's MMB_PROJ_*, MMB_GRAM_DIAG, MMB_PC_REMOVE_R)
-// exist only in the tools build (-DMMB_DIAG, libmmb_diag.so): the product
-// library reads no environment variable and carries only the defaults.
-#ifdef MMB_DIAG
-static int stream_policy() {
-  const char* e = getenv("MMB_STREAM_POLICY");
-  return e ? atoi(e) : 5;
-}
-#endif
+// exist only in the tools build (libmmb_diag.so, tools/diag/): at each
+// MMB_HOOK_* point below the product library compiles its default and reads
+// no environment variable.
 
 template <bool MM2, int CT, int CA, int CV, int UNR, bool NT, bool NTS, int OCC = 1>
 static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
@@ -1369,15 +1363,10 @@ static void launch_wave_v(const StreamArgs& a, int grid, hipStream_t stream) {
 // waves at its occupancy (2 waves / SIMD), one even share of utterances per
 // wave.  Measured (tools/grid_sweep.sh, MI355X): 2/4/8/16/32 = 20.88/20.94/
 // 21.04/21.01/21.18 ms.  MMB_STREAM_GRID_MULT overrides it (tools build).
-static int stream_grid_mult() {
-#ifdef MMB_DIAG
-  const char* e = getenv("MMB_STREAM_GRID_MULT");  // re-read per launch (in-process A/B)
-  const int v = e ? atoi(e) : 2;
-  return v > 0 ? v : 2;
-#else
-  return 2;
+#ifndef MMB_HOOK_STREAM_GRID_MULT
+#define MMB_HOOK_STREAM_GRID_MULT 2
 #endif
-}
+static int stream_grid_mult() { return MMB_HOOK_STREAM_GRID_MULT; }
 
 // rows of the column-bound partials (one per wave / workgroup of a launch)
 constexpr int kCmaxRows = 8192;
@@ -1399,14 +1388,10 @@ constexpr int kCmaxRows = 8192;
 // spilled) 4.09 vs 3.84.
 // Timing-only ablations of 3 (wrong rows): no text 3.14 (6), no frames 2.32
 // (7), no row stores 3.61 (8), neither text nor frames 1.41 (9).
-static int narrow_variant() {
-#ifdef MMB_DIAG
-  const char* e = getenv("MMB_STREAM_NARROW");  // re-read per launch (in-process A/B)
-  return e ? atoi(e) : 10;
-#else
-  return 10;
+#ifndef MMB_HOOK_NARROW_VARIANT
+#define MMB_HOOK_NARROW_VARIANT 10
 #endif
-}
+static int narrow_variant() { return MMB_HOOK_NARROW_VARIANT; }
 
 static int launch_narrow(const StreamArgs& a, hipStream_t stream, int* parts) {
   const int var = narrow_variant();
@@ -1417,24 +1402,10 @@ static int launch_narrow(const StreamArgs& a, hipStream_t stream, int* parts) {
   if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
   if (parts) *parts = grid * 4;
-#ifdef MMB_DIAG
-  switch (var) {
-    case 2: utt_narrow_kernel<2, 4, 7, 4, 2><<<grid, 256, 0, stream>>>(a); break;
-    case 3: utt_narrow_kernel<2, 5, 7, 4, 2><<<grid, 256, 0, stream>>>(a); break;
-    case 4: utt_narrow_kernel<2, 10, 7, 4, 2><<<grid, 256, 0, stream>>>(a); break;
-    case 5: utt_narrow_kernel<2, 5, 7, 4, 4><<<grid, 256, 0, stream>>>(a); break;
-    case 6: utt_narrow_kernel<2, 5, 7, 4, 2, 1><<<grid, 256, 0, stream>>>(a); break;
-    case 7: utt_narrow_kernel<2, 5, 7, 4, 2, 2><<<grid, 256, 0, stream>>>(a); break;
-    case 8: utt_narrow_kernel<2, 5, 7, 4, 2, 4><<<grid, 256, 0, stream>>>(a); break;
-    case 9: utt_narrow_kernel<2, 5, 7, 4, 2, 3><<<grid, 256, 0, stream>>>(a); break;
-    case 11: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 0, 1><<<grid, 256, 0, stream>>>(a); break;
-    case 12: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
-    case 13: utt_narrow_kernel<2, 8, 7, 4, 2, 0, 1, 1><<<grid, 256, 0, stream>>>(a); break;
-    default: utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a); break;
-  }
-#else
-  utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a);
+#ifndef MMB_HOOK_NARROW_LAUNCH  // (tools/diag: the variant sweep)
+#define MMB_HOOK_NARROW_LAUNCH false
 #endif
+  if (!(MMB_HOOK_NARROW_LAUNCH)) utt_narrow_kernel<2, 5, 7, 4, 2, 0, 1, 0><<<grid, 256, 0, stream>>>(a);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1447,25 +1418,16 @@ static int launch_wave(const StreamArgs& a, hipStream_t stream, int* parts = nul
   if (a.cmax_part && grid_cap > kCmaxRows / 4) grid_cap = kCmaxRows / 4;
   const int grid = static_cast<int>(blocks < grid_cap ? blocks : grid_cap);
   if (parts) *parts = grid * 4;
-#ifdef MMB_DIAG
-  switch (MM2 ? stream_policy() & 15 : 0) {
-    case 13: launch_wave_v<MM2, CT, CA, CV, 4, true, false, 2>(a, grid, stream); break;
-    case 1: launch_wave_v<MM2, CT, CA, CV, 2, true, false>(a, grid, stream); break;
-    case 2: launch_wave_v<MM2, CT, CA, CV, 2, false, true>(a, grid, stream); break;
-    case 3: launch_wave_v<MM2, CT, CA, CV, 2, true, true>(a, grid, stream); break;
-    case 4: launch_wave_v<MM2, CT, CA, CV, 4, false, false>(a, grid, stream); break;
-    case 5: launch_wave_v<MM2, CT, CA, CV, 4, true, false>(a, grid, stream); break;
-    case 6: launch_wave_v<MM2, CT, CA, CV, 4, false, true>(a, grid, stream); break;
-    case 7: launch_wave_v<MM2, CT, CA, CV, 4, true, true>(a, grid, stream); break;
-    default: launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream); break;
-  }
-#else
-  if constexpr (MM2) {  // policy 5: 4-frame groups, non-temporal frame loads
-    launch_wave_v<MM2, CT, CA, CV, 4, true, false>(a, grid, stream);
-  } else {
-    launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream);
-  }
+#ifndef MMB_HOOK_WAVE_LAUNCH  // (tools/diag: the stream-policy sweep)
+#define MMB_HOOK_WAVE_LAUNCH false
 #endif
+  if (!(MMB_HOOK_WAVE_LAUNCH)) {
+    if constexpr (MM2) {  // policy 5: 4-frame groups, non-temporal frame loads
+      launch_wave_v<MM2, CT, CA, CV, 4, true, false>(a, grid, stream);
+    } else {
+      launch_wave_v<MM2, CT, CA, CV, 2, false, false>(a, grid, stream);
+    }
+  }
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -1533,18 +1495,12 @@ struct FusedArgs {
   int64_t big, nu;         // dynamic order: units [0, big) are 48-row batches, the rest 12 rows
 };
 
-#ifdef MMB_DIAG
-// tools build: a test shortens the bounded waits to drive the timeout path
-// (mmb_diag_fused_wait_iters)
-__device__ int g_fused_wait_iters = 1 << 23;
+// the bounded waits' budget (tools/diag: a test shortens it to drive the
+// timeout path)
+#ifndef MMB_HOOK_FUSED_WAIT_ITERS
+#define MMB_HOOK_FUSED_WAIT_ITERS (1 << 23)
 #endif
-__device__ __forceinline__ int fused_wait_iters() {
-#ifdef MMB_DIAG
-  return g_fused_wait_iters;
-#else
-  return 1 << 23;
-#endif
-}
+__device__ __forceinline__ int fused_wait_iters() { return MMB_HOOK_FUSED_WAIT_ITERS; }
 
 // bounded wait for *p >= target (workgroup scope); false once anything timed out
 __device__ __forceinline__ bool fused_wait(int* p, int target, int* abort_flag, int32_t* gflag) {
@@ -1703,18 +1659,9 @@ __device__ __forceinline__ void frame_piece(const float* base, int W, int L, int
 // projectors only hand the slots back (no loads, MFMAs or epilogue), bit 1
 // no MFMAs (B loads kept live), bit 2 no epilogue, bit 3 the streamers skip
 // the frames (constant sums: the projectors alone)
-#ifdef MMB_DIAG
-// tools build only: per-workgroup wall-clock marks of the fused kernel
-// (start; each streamer wave's and each projector wave's end), read back with
-// mmb_diag_fused_probe -- the spread of finishing times across the CUs
-constexpr int kFProbe = 9;
-__device__ unsigned long long g_fused_probe[1024 * kFProbe];
-#define FUSED_PROBE(slot)                                                              \
-  do {                                                                                 \
-    if ((threadIdx.x & (kWave - 1)) == 0 && blockIdx.x < 1024)                         \
-      g_fused_probe[blockIdx.x * kFProbe + (slot)] = wall_clock64();                   \
-  } while (0)
-#else
+// per-workgroup wall-clock marks of the fused kernel (tools/diag defines
+// them: mmb_diag_fused_probe)
+#ifndef FUSED_PROBE
 #define FUSED_PROBE(slot) \
   do {                    \
   } while (0)
@@ -2556,92 +2503,22 @@ static int fused_grid(int64_t nb, hipStream_t stream) {
   return static_cast<int>(std::min<int64_t>(nb, std::min(stream_cu_count(stream), kCmaxRows / 4)));
 }
 
-#ifndef MMB_DIAG
 static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
   const int grid = fused_grid(f.nb, stream);
   if (parts) *parts = grid * 4;
-  if (fused_pipe_ok(f, 8)) {
-    launch_fused_v<0, 8, 2>(f, grid, stream);
-  } else {
-    launch_fused_v<0, 8, 0>(f, grid, stream);
-  }
-  MMB_LAUNCH_CHECK();
-  return MMB_OK;
-}
-#else
-static int fused_unr() {  // streamer frames per load group (in-process sweeps)
-  const char* e = getenv("MMB_FUSED_UNR");
-  return e ? atoi(e) : 8;
-}
-
-static int fused_diag() {  // re-read per launch (in-process timing sweeps)
-  const char* e = getenv("MMB_FUSED_DIAG");
-  return e ? atoi(e) : 0;
-}
-
-static int fused_pipe() {
-  const char* e = getenv("MMB_FUSED_PIPE");
-  return e ? atoi(e) : 2;
-}
-
-static int fused_slots() {  // ring slots: 62 (default) or 60 (in-process A/B)
-  const char* e = getenv("MMB_FUSED_SLOTS");
-  return e ? atoi(e) : kGSlots;
-}
-
-static int launch_fused(const FusedArgs& f, hipStream_t stream, int* parts) {
-  const int grid = fused_grid(f.nb, stream);
-  if (parts) *parts = grid * 4;
-  const int dg = fused_diag(), un = fused_unr();
-  const bool pipe = fused_pipe() != 0 && fused_pipe_ok(f, un);
-  if (pipe && un == 8 && fused_pipe() == 2 && (dg == 0 || dg == 1 || dg == 4 || dg == 128 || dg == 256)) {
-    if (dg == 1) {
-      launch_fused_v<1, 8, 2>(f, grid, stream);
-    } else if (dg == 4) {
-      launch_fused_v<4, 8, 2>(f, grid, stream);
-    } else if (dg == 128) {
-      launch_fused_v<128, 8, 2>(f, grid, stream);
-    } else if (dg == 256) {
-      launch_fused_v<256, 8, 2>(f, grid, stream);
-    } else {
-      launch_fused_v<0, 8, 2>(f, grid, stream);
-    }
-  } else if (pipe && un == 8) {
-    switch (dg) {
-      case 1: launch_fused_v<1, 8, true>(f, grid, stream); break;
-      case 2: launch_fused_v<2, 8, true>(f, grid, stream); break;
-      case 4: launch_fused_v<4, 8, true>(f, grid, stream); break;
-      case 16: launch_fused_v<16, 8, true>(f, grid, stream); break;
-      case 32: launch_fused_v<32, 8, true>(f, grid, stream); break;
-      case 64: launch_fused_v<64, 8, true>(f, grid, stream); break;
-      default:
-        if (fused_slots() == 60) {
-          launch_fused_v<0, 8, true, 60>(f, grid, stream);
-        } else {
-          launch_fused_v<0, 8, true>(f, grid, stream);
-        }
-        break;
-    }
-  } else if (pipe && dg == 0 && un == 6) {
-    launch_fused_v<0, 6, true>(f, grid, stream);
-
-  } else if (dg == 0 && un == 12) {
-    launch_fused_v<0, 12>(f, grid, stream);
-  } else if (dg == 0 && un == 16) {
-    launch_fused_v<0, 16>(f, grid, stream);
-  } else if (dg == 1 && un == 16) {
-    launch_fused_v<1, 16>(f, grid, stream);
-  } else switch (dg) {
-    case 1: launch_fused_v<1>(f, grid, stream); break;
-    case 2: launch_fused_v<2>(f, grid, stream); break;
-    case 4: launch_fused_v<4>(f, grid, stream); break;
-    case 8: launch_fused_v<8>(f, grid, stream); break;
-    default: launch_fused_v<0>(f, grid, stream); break;
-  }
-  MMB_LAUNCH_CHECK();
-  return MMB_OK;
-}
+#ifndef MMB_HOOK_FUSED_LAUNCH  // (tools/diag: the MMB_FUSED_* sweeps and ablations)
+#define MMB_HOOK_FUSED_LAUNCH false
 #endif
+  if (!(MMB_HOOK_FUSED_LAUNCH)) {
+    if (fused_pipe_ok(f, 8)) {
+      launch_fused_v<0, 8, 2>(f, grid, stream);
+    } else {
+      launch_fused_v<0, 8, 0>(f, grid, stream);
+    }
+  }
+  MMB_LAUNCH_CHECK();
+  return MMB_OK;
+}
 
 __global__ void seq2weight_kernel(const int32_t* __restrict__ seq, const uint8_t* __restrict__ sel,
                                   int64_t total, const double* __restrict__ wtab, int64_t V,
@@ -2705,16 +2582,10 @@ static int launch_stream(const StreamArgs& a, hipStream_t stream, int* parts = n
     // tools/splits_ab.py, gpurun_out r05m: stream 0.180 -> 0.148 ms and
     // 0.217 -> 0.188 ms, the same sums bit for bit; 1024 threads x 4 / 4:
     // 0.157 / 0.193 ms)
-#ifdef MMB_DIAG
-    const char* e = getenv("MMB_STREAM_SMALL");  // 0: as large N, 1: 320 x 16 / 8, 2: 1024 x 4 / 4
-    const int v = e ? atoi(e) : 1;
-    if (v == 0) {
-      utt_stream_kernel<MM2, VT, VA, VV><<<grid, kNT, 0, stream>>>(a);
-    } else if (v == 2) {
-      utt_stream_kernel<MM2, VT, VA, VV, 4, 4, 1024><<<grid, 1024, 0, stream>>>(a);
-    } else
+#ifndef MMB_HOOK_STREAM_SMALL  // (tools/diag: MMB_STREAM_SMALL)
+#define MMB_HOOK_STREAM_SMALL false
 #endif
-    {
+    if (!(MMB_HOOK_STREAM_SMALL)) {
       utt_stream_kernel<MM2, VT, VA, VV, 16, 8><<<grid, kNT, 0, stream>>>(a);
     }
   } else
@@ -3059,13 +2930,8 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   f.sched = colmax ? reinterpret_cast<unsigned*>(static_cast<char*>(colmax_ws) +
                                                  static_cast<size_t>(kCmaxRows) * d * sizeof(float))
                    : nullptr;
-#ifdef MMB_DIAG
-  {  // in-process A/B switches
-    const char* e = getenv("MMB_FUSED_BALANCED");
-    f.balanced = e ? atoi(e) : 1;
-    const char* dn = getenv("MMB_FUSED_DYN");
-    if (dn && atoi(dn) == 0) f.sched = nullptr;
-  }
+#ifdef MMB_HOOK_FUSED_ARGS  // (tools/diag: MMB_FUSED_BALANCED / MMB_FUSED_DYN)
+  MMB_HOOK_FUSED_ARGS(f);
 #endif
   {
     // the dynamic order from 16 rounds of batches on (fewer: the static round
@@ -3092,27 +2958,6 @@ extern "C" int mmb_mm2_stream_project(const int32_t* ids, const float* table, in
   return MMB_OK;
 }
 
-#ifdef MMB_DIAG
-// tools build: the bounded waits' iteration budget (1 << 23 in the product)
-extern "C" int mmb_diag_fused_wait_iters(int iters) {
-  MMB_REQUIRE(iters >= 1);
-  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_fused_wait_iters), &iters, sizeof(int));
-  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
-}
-
-// tools build: copy the fused kernel's per-workgroup wall-clock marks
-// [1024][9] (start, streamer waves 0-3 end, projector waves 4-7 end) and the
-// wall-clock rate (kHz) to the host
-extern "C" int mmb_diag_fused_probe(unsigned long long* host_out, int* rate_khz) {
-  MMB_REQUIRE(host_out && rate_khz);
-  hipError_t e = hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_fused_probe), sizeof(g_fused_probe));
-  if (e != hipSuccess) return static_cast<int>(e);
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  e = hipDeviceGetAttribute(rate_khz, hipDeviceAttributeWallClockRate, dev);
-  return e == hipSuccess ? MMB_OK : static_cast<int>(e);
-}
-#endif
 
 namespace mmb {
 
@@ -3731,10 +3576,10 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   const int64_t cus = stream_cu_count(stream);
   f.rpw = kNFRpw;
   while (f.rpw > 1 && ceil_div(n, static_cast<int64_t>(kNFWaves) * f.rpw) < cus) --f.rpw;
-  int teams = 0;  // 1: two teams of 4 waves per workgroup, 2: the same, team 1 starting a phase later
-#ifdef MMB_DIAG
-  if (const char* e = getenv("MMB_NF_TEAMS")) teams = atoi(e);
+#ifndef MMB_HOOK_NF_TEAMS  // (tools/diag: MMB_NF_TEAMS)
+#define MMB_HOOK_NF_TEAMS 0
 #endif
+  int teams = MMB_HOOK_NF_TEAMS;  // 1: two teams of 4 waves per workgroup, 2: the same, team 1 starting a phase later
   if (kNFWaves != 8) teams = 0;
   f.team_lag = teams == 2 ? 1 : 0;
   // batches: of 8 rpw rows, or of 4 rpw rows per team (two per workgroup)
@@ -3743,22 +3588,18 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
-#ifdef MMB_DIAG
-    if (kNFWaves == 8)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV, kNFWaves == 8>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kNFLds));
+#ifdef MMB_HOOK_NF_TEAMS_ATTR
+    MMB_HOOK_NF_TEAMS_ATTR;
 #endif
     attr = true;
   }
   int64_t grid = stream_cu_count(stream);
   if (colmax && grid > kCmaxRows / kNFWaves) grid = kCmaxRows / kNFWaves;
   if (grid > (teams ? ceil_div(f.nb, int64_t{2}) : f.nb)) grid = teams ? ceil_div(f.nb, int64_t{2}) : f.nb;
-#ifdef MMB_DIAG
-  if (teams) {
-    utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV, kNFWaves == 8><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
-    MMB_LAUNCH_CHECK();
-  } else
+#ifndef MMB_HOOK_NF_TEAMS_LAUNCH
+#define MMB_HOOK_NF_TEAMS_LAUNCH false
 #endif
+  if (!(MMB_HOOK_NF_TEAMS_LAUNCH))
     utt_narrow_fused_kernel<NF_UNR, NF_HU, NF_GA, NF_GV><<<static_cast<unsigned>(grid), kNFThreads, kNFLds, stream>>>(f);
   MMB_LAUNCH_CHECK();
   if (!colmax) return MMB_OK;
@@ -3767,3 +3608,10 @@ extern "C" int mmb_mm2_stream_project_narrow(const int32_t* ids, const float* ta
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
+
+// the tools build's variant launches, knobs and probes (tools/diag/); the
+// product library includes an empty header here
+#ifndef MMB_TOOLS_TAIL_SIF
+#define MMB_TOOLS_TAIL_SIF "mmb_no_tools.h"
+#endif
+#include MMB_TOOLS_TAIL_SIF

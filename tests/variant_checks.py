@@ -7,7 +7,8 @@ register-B (6) kernels and its tile-layout epilogue, the stream kernel's
 load/store policies and grid sizes, the fused kernel's group-at-a-time and
 pipelined streamers and its unbalanced tail, the narrow fused kernel's
 4-wave teams, the int8 Gram with x staged in LDS, the one-row PC removal -- live in
-the tools build, libmmb_diag.so (`make diag`, -DMMB_DIAG), where MMB_* knobs
+the tools build, libmmb_diag.so (`make diag`: tools/diag/, plugged into the
+product sources' MMB_HOOK_* points), where MMB_* knobs
 select them per launch.  This script runs in a child process that loads
 that build explicitly (mmb_lib.load(path), tests/test_gpu_variants.py) and asserts
 that each variant reproduces the default path: bit-identical where the

@@ -1,6 +1,6 @@
 // Phase timing of pc_solve_mc_kernel (wall_clock64 marks of workgroup 0,
 // MMB_PC_PROBE build) and its PC against the one-workgroup solve.
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMMB_PC_PROBE -DMMB_DIAG -I../../include \
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DMMB_PC_PROBE -include ../diag/diag_hooks.h -I../../include \
 //     pc_probe_mc.hip ../../multimodal-baselines_amd/csrc/host_rng.cpp \
 //     ../../multimodal-baselines_amd/csrc/probe_kernels.hip -o pc_probe_mc
 #include "../../multimodal-baselines_amd/csrc/pc_kernels.hip"
