@@ -1938,6 +1938,16 @@ __device__ __forceinline__ void p16_eq_chol(const double* W, double* L, double* 
 // transposed start); the same k-steps per wave and the same sum order either
 // way, so G2 is the same bit for bit.
 constexpr int kSqNT = 256;
+// G2 tiles per squaring workgroup of the solve's launch (two at a time): 2
+// puts 95 workgroups beside the solve's 19 at d = 300, 4 puts 48 (fewer CUs
+// held with the solve's LDS allocation).  Alternated A/B (r06,
+// tools/ab_libs/build_sq.sh, profiles/r06/sq2/): the solve alone 75.1 vs
+// 76.7 us, MOSI's three-split graph 0.215 vs 0.216 ms, POM's 0.343 vs 0.344
+#ifndef MMB_SQ_PER_WG
+#define MMB_SQ_PER_WG 2
+#endif
+constexpr int kSqPerWg = MMB_SQ_PER_WG;
+static_assert(kSqPerWg % 2 == 0, "two tiles per pass");
 __device__ __forceinline__ void square_tile_ab(int blk, int T, int& a, int& b) {
   int rem = blk;
   a = 0;  // blk -> (a, b), a <= b, row-major over the upper triangle
@@ -2059,16 +2069,22 @@ __global__ __launch_bounds__(kPnNT) void pc_solve_mc_kernel(const double* __rest
   unsigned* sq_ctr = ctl + 2;  // the squaring workgroups' arrivals
 
   if (t >= T) {
-    // workgroups T .. T + nsq_wg - 1 (r06b): G2 = G G, two tiles each (waves
-    // 0-3 and 4-7), while the solve's workgroups run their first round by G.
-    // Write-through stores, drained by every wave, then one arrival; the
-    // solve waits for all nsq_wg before its first squared round.  An arrival
-    // that finds the count already met is a workspace handed over dirty.
+    // workgroups T .. T + nsq_wg - 1 (r06b): G2 = G G, kSqPerWg tiles each,
+    // two at a time (waves 0-3 and 4-7), while the solve's workgroups run
+    // their first round by G.  Write-through stores, drained by every wave,
+    // then one arrival; the solve waits for all nsq_wg before its first
+    // squared round.  An arrival that finds the count already met is a
+    // workspace handed over dirty.
     double* part4 = p16_lds + 2 * Dp * kP16W + (wave >> 2) * 4 * 256;
-    const int blk = 2 * (t - T) + (wave >> 2), ntiles = T * (T + 1) / 2;
-    if (blk < ntiles) square_tile_partials(G, D, blk, wave & 3, lane, part4);
-    __syncthreads();
-    if (blk < ntiles) square_tile_store<true>(D, G2, blk, tid & 255, part4);
+    const int ntiles = T * (T + 1) / 2;
+#pragma unroll 1
+    for (int pass = 0; pass < kSqPerWg / 2; ++pass) {
+      const int blk = kSqPerWg * (t - T) + 2 * pass + (wave >> 2);
+      if (blk < ntiles) square_tile_partials(G, D, blk, wave & 3, lane, part4);
+      __syncthreads();
+      if (blk < ntiles) square_tile_store<true>(D, G2, blk, tid & 255, part4);
+      __syncthreads();  // part4 is read before the next pass writes it
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -3248,7 +3264,7 @@ static int launch_solve_mc(const double* g, int d, const double* z0, int k, int 
   if (!solve_squares(npc, n_iter)) {
     g2 = nullptr;
   } else if (!g2_ready) {
-    nsq_wg = (T * (T + 1) / 2 + 1) / 2;
+    nsq_wg = (T * (T + 1) / 2 + kSqPerWg - 1) / kSqPerWg;
   }
   static bool attr = false;
   if (!attr) {

@@ -19,12 +19,19 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import mmb_lib as L  # noqa: E402
+
+# --lib PATH: an A/B clone of the product library (tools/ab_libs), loaded
+# explicitly before the mirror modules bind to it
+_lib = next((sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a == "--lib"), None)
+if _lib:
+    L.load(_lib)
 import models  # noqa: E402
 import pipeline as P  # noqa: E402
 import synth  # noqa: E402
 from oracle import sif_oracle as O  # noqa: E402
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--lib", default=None)
 ap.add_argument("--reps", type=int, default=200)
 ap.add_argument("--step-g", type=int, default=125_000)
 args = ap.parse_args()
