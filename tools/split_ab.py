@@ -19,10 +19,17 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import mmb_lib as L  # noqa: E402
+
+# --lib PATH: an A/B clone of the product library (tools/ab_libs), loaded
+# explicitly before the mirror modules bind to it
+_lib = next((sys.argv[i + 1] for i, a in enumerate(sys.argv[:-1]) if a == "--lib"), None)
+if _lib:
+    L.load(_lib)
 import pipeline as P  # noqa: E402
 import synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--lib", default=None)
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--parts", default="0,2,3,4,6,8,12,16")
 args = ap.parse_args()
