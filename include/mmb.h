@@ -247,15 +247,11 @@ int mmb_mm2_stream(const int32_t* ids, const float* table, int64_t v, const floa
  * workgroup per CU in all; parts > 0: that many, at most t), each range
  * summed by a text, an audio and a visual workgroup of its own whose
  * partial sums go to ws (mmb_mm2_stream_split_ws_bytes(n, t, d, a, vd, parts) bytes,
- * caller-owned scratch, 16-byte aligned: n arrival counters, then the
- * partials), and the utterance's last workgroup to arrive adds its partials
- * in fixed part order and writes the same outputs as mmb_mm2_stream (x, s in
- * the s_half format asked for, aux, colmax; n <= 8192 with colmax) -- one
- * launch.  ws is handed over ZEROED (its counters) and every launch leaves it
- * so; a counter found past its utterance's workgroups (a dirty workspace)
- * sets MMB_FLAG_SYNC_TIMEOUT and the rows are invalid: zero ws again.  Rows
- * are deterministic and equal mmb_mm2_stream's to the f32 order of the token
- * and frame sums (bit for bit with one range).
+ * caller-owned scratch), and a second kernel adds an utterance's partials in
+ * fixed part order and writes the same outputs as mmb_mm2_stream (x, s in
+ * the s_half format asked for, aux, colmax; n <= 8192 with colmax).  Rows are
+ * deterministic and equal mmb_mm2_stream's to the f32 order of the token and
+ * frame sums.
  * replaces: the frame loops of sif2.estimate_embedding_overall_gpu2
  *   /root/reference/sif2.py:181-205 at the per-split call sites
  *   /root/reference/simplesif.py:308-311 (POM's long transcripts)          */

@@ -435,17 +435,15 @@ __global__ __launch_bounds__(NT) void utt_stream_kernel(StreamArgs a) {
 // frame workgroup, in ONE launch: the text workgroups (blocks [0, N Pt):
 // token staging, the kept rows' gather, the counts) first, then the frame
 // workgroups (one modality each, audio then visual: pure streams, no
-// staging, no barrier before their reduction), each writing PARTIAL sums; the utterance's last
-// workgroup to arrive (r06: a counter per utterance) adds its partials in
-// fixed part order and finishes the row as
+// staging, no barrier before their reduction), each writing PARTIAL sums; utt_split_finish_kernel adds
+// an utterance's partials in fixed part order and finishes the row as
 // utt_stream_kernel does (x = num / count, the s row, aux, the row scale,
 // the column bounds) -- writing the fp16 hi / lo planes directly, so the
 // s_half path needs no split_rows pass.  Deterministic; against the
 // one-workgroup kernel only the f32 order of the token and frame sums
 // differs (with one range it is the same order: bit-identical).
 //
-// Workspace: N arrival counters (16-byte rounded), then (floats) text
-// partials [N][Pt][Wt] = [num (D) | Sx_e (D) |
+// Workspace (floats): text partials [N][Pt][Wt] = [num (D) | Sx_e (D) |
 // Sxx_e (D) | count_nonzero(w), sum w, row-0 tokens, their weight sum] (row
 // 0 excluded from the sums, as utt_stream_kernel), then frame partials
 // [N][Pf][Wf] = [Sx_a (A) | Sxx_a (A) | Sx_v (Vd) | Sxx_v (Vd)].
@@ -468,115 +466,9 @@ inline SplitPlan split_plan_of(int t, int d, int a, int vd, int Pf) {
   return q;
 }
 
-// The partials of utterance i in part order, then the row's
-// epilogue of utt_stream_kernel: row 0 once for its tokens, x, the s row
-// (fp32, or the fp16 hi / lo planes of s * rs), aux, the column bounds of
-// this workgroup (N <= kCmaxRows rows of cmax_part).  Thread tid owns
-// columns f = tid + NT j (j < kSplitJ) of [num | Sx_e | Sxx_e | frame sums]
-// and walks each kind's parts in order, all kSplitJ loads of a part issued
-// together (a loop over the parts per column was a chain of P dependent L2
-// round trips per column).
-constexpr int kSplitJ = 7;  // ceil((3 * 320 + 4 * 320) / kNT): every partial column
-// s_row: K floats of LDS (s_half: the fp32 row before the split), s_m: one
-// float per wave.  Run by the utterance's last part workgroup to arrive.
-__device__ __forceinline__ void split_finish_row(const StreamArgs& a, const SplitPlan& q,
-                                                 const float* __restrict__ part, int64_t i,
-                                                 float* s_row, float* s_m) {
-  constexpr int NT = kNT;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  const int K = 2 * (a.D + a.A + a.Vd);
-  const int D3 = 3 * a.D, W = a.D + K;  // text columns; all partial columns
-  const float* pt = part + i * q.Pt * static_cast<int64_t>(q.Wt);
-  const float* pf = part + a.N * q.Pt * static_cast<int64_t>(q.Wt) + i * q.Pf * static_cast<int64_t>(q.Wf);
-  float acc[kSplitJ], sc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < kSplitJ; ++j) acc[j] = 0.f;
-#pragma unroll 2
-  for (int p = 0; p < q.Pt; ++p) {
-    const float* pr = pt + static_cast<int64_t>(p) * q.Wt;
-    float v[kSplitJ], u[4];
-#pragma unroll
-    for (int j = 0; j < kSplitJ; ++j) {
-      const int f = tid + NT * j;
-      v[j] = f < D3 ? pr[f] : 0.f;
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) u[c] = pr[D3 + c];  // (a broadcast: every lane the same word)
-#pragma unroll
-    for (int j = 0; j < kSplitJ; ++j) acc[j] += v[j];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) sc[c] += u[c];
-  }
-#pragma unroll 2
-  for (int p = 0; p < q.Pf; ++p) {
-    const float* pr = pf + static_cast<int64_t>(p) * q.Wf - D3;
-    float v[kSplitJ];
-#pragma unroll
-    for (int j = 0; j < kSplitJ; ++j) {
-      const int f = tid + NT * j;
-      v[j] = (f >= D3 && f < W) ? pr[f] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < kSplitJ; ++j) acc[j] += v[j];
-  }
-  const float cnt = sc[0], sw = sc[1], c0 = sc[2], w0 = sc[3];
-  float cmx0 = 0.f, cmx1 = 0.f, smax = 0.f;
-#pragma unroll
-  for (int j = 0; j < kSplitJ; ++j) {
-    const int f = tid + NT * j;
-    if (f >= W) continue;
-    float v = acc[j];
-    if (f < a.D) {  // the weighted text sum: row 0 once for its c0 tokens (gather mode)
-      const float e0 = (c0 > 0.f) ? a.table[f] : 0.f;
-      v = fmaf(w0, e0, v);
-      const float xf = v / cnt;
-      a.num_out[i * a.D + f] = xf;
-      if (f < NT) cmx0 = bmax(cmx0, fabsf(xf)); else cmx1 = bmax(cmx1, fabsf(xf));
-      continue;
-    }
-    const int g = f - a.D;  // s column
-    if (g < 2 * a.D) {
-      const float e0 = (c0 > 0.f) ? a.table[g < a.D ? g : g - a.D] : 0.f;
-      v = g < a.D ? fmaf(c0, e0, v) : fmaf(c0 * e0, e0, v);
-    }
-    smax = fmaxf(smax, fabsf(v));
-    if (a.s_half) s_row[g] = v; else a.s_out[i * a.Kp + g] = v;
-  }
-  smax = wave_max(smax);
-  if (lane == 0) s_m[wave] = smax;
-  __syncthreads();
-  float m = 0.f;
-#pragma unroll
-  for (int w = 0; w < NT / kWave; ++w) m = fmaxf(m, s_m[w]);
-  const float rs = row_scale(m);
-  if (a.s_half) {
-    _Float16* hi = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * static_cast<int64_t>(a.Kp);
-    for (int f = tid; f < a.Kp; f += NT) {
-      const float x = f < K ? s_row[f] * rs : 0.f;
-      const _Float16 h = static_cast<_Float16>(x);
-      hi[f] = h;
-      hi[a.Kp + f] = static_cast<_Float16>(x - static_cast<float>(h));
-    }
-  } else {
-    for (int f = K + tid; f < a.Kp; f += NT) a.s_out[i * a.Kp + f] = 0.f;
-  }
-  if (tid == 0) {
-    if (cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
-    a.aux_out[i] = cnt;
-    a.aux_out[a.N + i] = sw;
-    a.aux_out[2 * a.N + i] = rs;
-  }
-  if (a.cmax_part) {
-    float* pr = a.cmax_part + i * a.D;
-    if (tid < a.D) pr[tid] = cmx0;
-    if (tid + NT < a.D) pr[tid + NT] = cmx1;
-  }
-}
-
 template <int VT, int VA, int VV, int FU = 16, int TU = 8>
 __global__ __launch_bounds__(kNT) void utt_split_part_kernel(StreamArgs a, SplitPlan q,
-                                                             float* __restrict__ part,
-                                                             unsigned* __restrict__ arrivals) {
+                                                             float* __restrict__ part) {
   constexpr int NT = kNT;
   constexpr int kRF = NT * 4;
   constexpr int kSI = (kTokChunk + NT - 1) / NT;
@@ -589,12 +481,9 @@ __global__ __launch_bounds__(kNT) void utt_split_part_kernel(StreamArgs a, Split
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), wave = tid / kWave;
   const int64_t ntext = a.N * q.Pt;
-  // the utterance of this workgroup: text ranges first, then audio, then visual
-  const int64_t bfr = static_cast<int64_t>(blockIdx.x) - ntext;
-  const int64_t i = bfr < 0 ? static_cast<int64_t>(blockIdx.x) / q.Pt
-                            : (bfr >= a.N * q.Pf ? bfr - a.N * q.Pf : bfr) / q.Pf;
-  if (bfr < 0) {
+  if (static_cast<int64_t>(blockIdx.x) < ntext) {
     // ---- a token range: staging, the kept rows, the counts
+    const int64_t i = blockIdx.x / q.Pt;
     const int p = static_cast<int>(blockIdx.x - i * q.Pt);
     const int tb = p * q.Lt, te = min(a.L, tb + q.Lt);
     const int CT = a.D / VT, RT = NT / CT;
@@ -694,11 +583,13 @@ __global__ __launch_bounds__(kNT) void utt_split_part_kernel(StreamArgs a, Split
       for (int w = 0; w < NT / kWave; ++w) sc += s_sc[tid][w];
       prow[3 * a.D + tid] = sc;
     }
-  } else {
+    return;
+  }
   // ---- a frame range of ONE modality (audio workgroups, then visual)
-  const int64_t b = bfr;
+  const int64_t b = blockIdx.x - ntext;
   const bool vis = b >= a.N * q.Pf;
   const int64_t bm = vis ? b - a.N * q.Pf : b;
+  const int64_t i = bm / q.Pf;
   const int p = static_cast<int>(bm - i * q.Pf);
   const int tb = p * q.Lf, te = min(a.L, tb + q.Lf);
   float* prow = part + ntext * q.Wt + (i * q.Pf + p) * static_cast<int64_t>(q.Wf);
@@ -743,34 +634,112 @@ __global__ __launch_bounds__(kNT) void utt_split_part_kernel(StreamArgs a, Split
     stream(a.visual, a.Vd, prow + 2 * a.A, std::integral_constant<int, VV>{});
   else
     stream(a.audio, a.A, prow, std::integral_constant<int, VA>{});
-  }
-  // r06: the utterance's LAST workgroup to arrive finishes its row (no second
-  // launch): every wave drains its partial stores, one release + arrival on
-  // the utterance's counter; the one that completes the count acquires, resets
-  // the counter for the next launch (every other workgroup of the utterance
-  // has arrived) and sums the partials in fixed part order -- whichever
-  // workgroup that is, the same row.  A count already past the utterance's
-  // workgroups is a workspace handed over dirty: MMB_FLAG_SYNC_TIMEOUT.
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned nparts = static_cast<unsigned>(q.Pt + 2 * q.Pf);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const unsigned old = __hip_atomic_fetch_add(arrivals + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old + 1 == nparts;
-    if (old >= nparts && a.flag) atomicOr(a.flag, MMB_FLAG_SYNC_TIMEOUT);
-    if (s_last) {
-      __hip_atomic_store(arrivals + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!s_last) return;
-  split_finish_row(a, q, part, i, s_red, s_sc[0]);
 }
 
+// The partials of utterance i (blockIdx.x) in part order, then the row's
+// epilogue of utt_stream_kernel: row 0 once for its tokens, x, the s row
+// (fp32, or the fp16 hi / lo planes of s * rs), aux, the column bounds of
+// this workgroup (grid = N <= kCmaxRows rows of cmax_part).  Thread tid owns
+// columns f = tid + NT j (j < kSplitJ) of [num | Sx_e | Sxx_e | frame sums]
+// and walks each kind's parts in order, all kSplitJ loads of a part issued
+// together (a loop over the parts per column was a chain of P dependent L2
+// round trips per column).
+constexpr int kSplitJ = 7;  // ceil((3 * 320 + 4 * 320) / kNT): every partial column
+__global__ __launch_bounds__(kNT) void utt_split_finish_kernel(StreamArgs a, SplitPlan q,
+                                                               const float* __restrict__ part) {
+  constexpr int NT = kNT;
+  extern __shared__ float s_row[];  // s_half: the fp32 row before the split
+  __shared__ float s_m[NT / kWave];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const int64_t i = blockIdx.x;
+  const int K = 2 * (a.D + a.A + a.Vd);
+  const int D3 = 3 * a.D, W = a.D + K;  // text columns; all partial columns
+  const float* pt = part + i * q.Pt * static_cast<int64_t>(q.Wt);
+  const float* pf = part + a.N * q.Pt * static_cast<int64_t>(q.Wt) + i * q.Pf * static_cast<int64_t>(q.Wf);
+  float acc[kSplitJ], sc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < kSplitJ; ++j) acc[j] = 0.f;
+#pragma unroll 2
+  for (int p = 0; p < q.Pt; ++p) {
+    const float* pr = pt + static_cast<int64_t>(p) * q.Wt;
+    float v[kSplitJ], u[4];
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) {
+      const int f = tid + NT * j;
+      v[j] = f < D3 ? pr[f] : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) u[c] = pr[D3 + c];  // (a broadcast: every lane the same word)
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) acc[j] += v[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) sc[c] += u[c];
+  }
+#pragma unroll 2
+  for (int p = 0; p < q.Pf; ++p) {
+    const float* pr = pf + static_cast<int64_t>(p) * q.Wf - D3;
+    float v[kSplitJ];
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) {
+      const int f = tid + NT * j;
+      v[j] = (f >= D3 && f < W) ? pr[f] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kSplitJ; ++j) acc[j] += v[j];
+  }
+  const float cnt = sc[0], sw = sc[1], c0 = sc[2], w0 = sc[3];
+  float cmx0 = 0.f, cmx1 = 0.f, smax = 0.f;
+#pragma unroll
+  for (int j = 0; j < kSplitJ; ++j) {
+    const int f = tid + NT * j;
+    if (f >= W) continue;
+    float v = acc[j];
+    if (f < a.D) {  // the weighted text sum: row 0 once for its c0 tokens (gather mode)
+      const float e0 = (c0 > 0.f) ? a.table[f] : 0.f;
+      v = fmaf(w0, e0, v);
+      const float xf = v / cnt;
+      a.num_out[i * a.D + f] = xf;
+      if (f < NT) cmx0 = bmax(cmx0, fabsf(xf)); else cmx1 = bmax(cmx1, fabsf(xf));
+      continue;
+    }
+    const int g = f - a.D;  // s column
+    if (g < 2 * a.D) {
+      const float e0 = (c0 > 0.f) ? a.table[g < a.D ? g : g - a.D] : 0.f;
+      v = g < a.D ? fmaf(c0, e0, v) : fmaf(c0 * e0, e0, v);
+    }
+    smax = fmaxf(smax, fabsf(v));
+    if (a.s_half) s_row[g] = v; else a.s_out[i * a.Kp + g] = v;
+  }
+  smax = wave_max(smax);
+  if (lane == 0) s_m[wave] = smax;
+  __syncthreads();
+  float m = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / kWave; ++w) m = fmaxf(m, s_m[w]);
+  const float rs = row_scale(m);
+  if (a.s_half) {
+    _Float16* hi = reinterpret_cast<_Float16*>(a.s_out) + i * 2 * static_cast<int64_t>(a.Kp);
+    for (int f = tid; f < a.Kp; f += NT) {
+      const float x = f < K ? s_row[f] * rs : 0.f;
+      const _Float16 h = static_cast<_Float16>(x);
+      hi[f] = h;
+      hi[a.Kp + f] = static_cast<_Float16>(x - static_cast<float>(h));
+    }
+  } else {
+    for (int f = K + tid; f < a.Kp; f += NT) a.s_out[i * a.Kp + f] = 0.f;
+  }
+  if (tid == 0) {
+    if (cnt == 0.f && a.flag) atomicOr(a.flag, MMB_FLAG_ZERO_WEIGHTS);
+    a.aux_out[i] = cnt;
+    a.aux_out[a.N + i] = sw;
+    a.aux_out[2 * a.N + i] = rs;
+  }
+  if (a.cmax_part) {
+    float* pr = a.cmax_part + i * a.D;
+    if (tid < a.D) pr[tid] = cmx0;
+    if (tid + NT < a.D) pr[tid + NT] = cmx1;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Wave-per-utterance variant (tokens/frames <= 64, widths % 4 == 0, <= 512):
@@ -2832,21 +2801,20 @@ extern "C" int mmb_mm2_stream_split_parts(int64_t n, int t) {
 static size_t split_ws_floats(int64_t n, const SplitPlan& q) {
   return static_cast<size_t>(n) * (static_cast<size_t>(q.Pt) * q.Wt + static_cast<size_t>(q.Pf) * q.Wf);
 }
-// workspace: the utterances' arrival counters first (a fixed place whatever
-// the plan, zero when handed over and after every launch), then the partials
-static size_t split_ctr_bytes(int64_t n) { return (static_cast<size_t>(n) * 4 + 15) / 16 * 16; }
 
 extern "C" size_t mmb_mm2_stream_split_ws_bytes(int64_t n, int t, int d, int a_, int vd, int parts) {
   if (n <= 0 || t <= 0 || d <= 0 || a_ <= 0 || vd <= 0) return 0;
   const int P = parts > 0 ? std::min(parts, t) : mmb_mm2_stream_split_parts(n, t);
-  return split_ctr_bytes(n) + split_ws_floats(n, split_plan_of(t, d, a_, vd, P)) * sizeof(float);
+  return split_ws_floats(n, split_plan_of(t, d, a_, vd, P)) * sizeof(float);
 }
 
 template <int VT, int VA, int VV>
-static int launch_split(const StreamArgs& a, const SplitPlan& q, float* part, unsigned* arrivals,
-                        hipStream_t stream) {
+static int launch_split(const StreamArgs& a, const SplitPlan& q, float* part, hipStream_t stream) {
   const int64_t grid = a.N * (q.Pt + 2 * q.Pf);
-  utt_split_part_kernel<VT, VA, VV><<<static_cast<unsigned>(grid), kNT, 0, stream>>>(a, q, part, arrivals);
+  utt_split_part_kernel<VT, VA, VV><<<static_cast<unsigned>(grid), kNT, 0, stream>>>(a, q, part);
+  MMB_LAUNCH_CHECK();
+  const size_t lds = a.s_half ? static_cast<size_t>(2 * (a.D + a.A + a.Vd)) * sizeof(float) : 0;
+  utt_split_finish_kernel<<<static_cast<unsigned>(a.N), kNT, lds, stream>>>(a, q, part);
   MMB_LAUNCH_CHECK();
   return MMB_OK;
 }
@@ -2875,10 +2843,9 @@ extern "C" int mmb_mm2_stream_split(const int32_t* ids, const float* table, int6
   }
   const int P = parts > 0 ? std::min(parts, t) : mmb_mm2_stream_split_parts(n, t);
   const SplitPlan q = split_plan_of(t, d, a_, vd, P);
-  MMB_REQUIRE(ws && (reinterpret_cast<uintptr_t>(ws) & 15) == 0 &&
-              ws_bytes >= split_ctr_bytes(n) + split_ws_floats(n, q) * sizeof(float));
+  MMB_REQUIRE(ws && ws_bytes >= split_ws_floats(n, q) * sizeof(float));
   MMB_REQUIRE(n * (q.Pt + 2 * q.Pf) <= (int64_t{1} << 31) - 1);
-  MMB_REQUIRE(3 * d + 2 * a_ + 2 * vd <= kSplitJ * kNT);  // the finishing workgroup's columns
+  MMB_REQUIRE(3 * d + 2 * a_ + 2 * vd <= kSplitJ * kNT);  // the finish kernel's columns
   StreamArgs s{};
   s.cmax_part = colmax ? static_cast<float*>(colmax_ws) : nullptr;
   s.ids = ids; s.table = table; s.V = v; s.wtab = wtab32; s.w_dense = w_dense;
@@ -2890,18 +2857,17 @@ extern "C" int mmb_mm2_stream_split(const int32_t* ids, const float* table, int6
   const bool va = (a_ % 4 == 0) && aligned16(audio);
   const bool vv = (vd % 4 == 0) && aligned16(visual);
   MMB_REQUIRE(d / (vt ? 4 : 1) <= kNT && a_ / (va ? 4 : 1) <= kNT && vd / (vv ? 4 : 1) <= kNT);
-  unsigned* arrivals = static_cast<unsigned*>(ws);
-  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + split_ctr_bytes(n));
+  float* part = static_cast<float*>(ws);
   int rc;
   switch ((vt ? 4 : 0) | (va ? 2 : 0) | (vv ? 1 : 0)) {
-    case 7: rc = launch_split<4, 4, 4>(s, q, part, arrivals, stream); break;
-    case 6: rc = launch_split<4, 4, 1>(s, q, part, arrivals, stream); break;
-    case 5: rc = launch_split<4, 1, 4>(s, q, part, arrivals, stream); break;
-    case 4: rc = launch_split<4, 1, 1>(s, q, part, arrivals, stream); break;
-    case 3: rc = launch_split<1, 4, 4>(s, q, part, arrivals, stream); break;
-    case 2: rc = launch_split<1, 4, 1>(s, q, part, arrivals, stream); break;
-    case 1: rc = launch_split<1, 1, 4>(s, q, part, arrivals, stream); break;
-    default: rc = launch_split<1, 1, 1>(s, q, part, arrivals, stream); break;
+    case 7: rc = launch_split<4, 4, 4>(s, q, part, stream); break;
+    case 6: rc = launch_split<4, 4, 1>(s, q, part, stream); break;
+    case 5: rc = launch_split<4, 1, 4>(s, q, part, stream); break;
+    case 4: rc = launch_split<4, 1, 1>(s, q, part, stream); break;
+    case 3: rc = launch_split<1, 4, 4>(s, q, part, stream); break;
+    case 2: rc = launch_split<1, 4, 1>(s, q, part, stream); break;
+    case 1: rc = launch_split<1, 1, 4>(s, q, part, stream); break;
+    default: rc = launch_split<1, 1, 1>(s, q, part, stream); break;
   }
   if (rc != MMB_OK || !colmax) return rc;
   colmax_reduce_kernel<<<static_cast<unsigned>(ceil_div(d, 64)), 1024, 0, stream>>>(

@@ -464,11 +464,9 @@ def split_parts(n: int, t: int) -> int:
 
 
 def split_ws(n: int, t: int, d: int, a: int, vd: int, device, parts: int = 0) -> torch.Tensor:
-    """Scratch of mmb_mm2_stream_split: the utterances' arrival counters
-    (handed over zeroed; every launch leaves them zero) and the per-range
-    partial rows.  Sized for `parts` ranges, it serves any fewer."""
+    """Scratch of mmb_mm2_stream_split (its per-range partial rows)."""
     nb = int(L.query("mmb_mm2_stream_split_ws_bytes", n, t, d, a, vd, parts))
-    return torch.zeros(max(nb, 16), dtype=torch.uint8, device=device)
+    return torch.empty(max(nb, 16), dtype=torch.uint8, device=device)
 
 
 def mm2_stream(n, t, d, a, vd, audio, visual, ids32=None, table=None, wtab32=None,
@@ -913,9 +911,6 @@ class FusedStep:
             # an aborted solve leaves its control words set (and a NaN PC):
             # hand the next launch a zeroed workspace again
             self.solve_ws[:16].zero_()
-        if self.split is not None and v & L.MMB_FLAG_SYNC_TIMEOUT:
-            # a split stream that found dirty arrival counters leaves them so
-            self.split.zero_()
         check_flag_bits(v & (PC_NONFINITE - 1), self.V, zero_weights=True)
         if v & PC_NONFINITE:
             raise ValueError("Input X contains NaN or infinity: the split's Gram is not finite "
