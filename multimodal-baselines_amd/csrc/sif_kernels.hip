@@ -451,7 +451,25 @@ struct SplitPlan {
   int Pt, Lt, Pf, Lf;  // text / frame parts per utterance and their lengths
   int Wt, Wf;          // partial row strides (floats, multiples of 4)
 };
-inline SplitPlan split_plan_of(int t, int d, int a, int vd, int Pf) {
+// A/B build constants of the split kernel (tools/ab_libs/build_split.sh):
+// text ranges per frame range of the automatic plan (MMB_SPLIT_TEXT_X; an
+// explicit part count keeps them equal), text / frame rows unrolled per
+// thread group (MMB_SPLIT_TU / MMB_SPLIT_FU; the sums' order is the same).
+// Alternated twice on POM's real splits (r06, profiles/r06/splitab*,
+// valid / test stream ms): TU 8 FU 16 0.0556-0.0567 / 0.126-0.128; FU 8
+// 0.0545-0.0551 / 0.123-0.125 (kept); FU 4 0.067 / 0.146; FU 32 0.065 /
+// 0.141; TU 16 0.072 / 0.151; TU 4 FU 8 0.067 / 0.116; two text ranges per
+// frame range 0.058 / 0.131 -- the text workgroups are not the long pole
+#ifndef MMB_SPLIT_TEXT_X
+#define MMB_SPLIT_TEXT_X 1
+#endif
+#ifndef MMB_SPLIT_TU
+#define MMB_SPLIT_TU 8
+#endif
+#ifndef MMB_SPLIT_FU
+#define MMB_SPLIT_FU 8
+#endif
+inline SplitPlan split_plan_of(int t, int d, int a, int vd, int Pf, int text_x = 1) {
   SplitPlan q;
   q.Lf = (t + Pf - 1) / Pf;
   q.Pf = (t + q.Lf - 1) / q.Lf;  // no empty part
@@ -459,8 +477,8 @@ inline SplitPlan split_plan_of(int t, int d, int a, int vd, int Pf) {
   // staged chunk by chunk): with one range the sums run in the one-workgroup
   // kernel's order.  One LDS chunk per text workgroup instead measured no
   // faster (POM valid 57.5 vs 55.3 us, r06 tools/split_ab.py)
-  q.Lt = q.Lf;
-  q.Pt = q.Pf;
+  q.Lt = (t + q.Pf * text_x - 1) / (q.Pf * text_x);
+  q.Pt = (t + q.Lt - 1) / q.Lt;
   q.Wt = (3 * d + 4 + 3) / 4 * 4;
   q.Wf = (2 * a + 2 * vd + 3) / 4 * 4;
   return q;
@@ -2805,13 +2823,13 @@ static size_t split_ws_floats(int64_t n, const SplitPlan& q) {
 extern "C" size_t mmb_mm2_stream_split_ws_bytes(int64_t n, int t, int d, int a_, int vd, int parts) {
   if (n <= 0 || t <= 0 || d <= 0 || a_ <= 0 || vd <= 0) return 0;
   const int P = parts > 0 ? std::min(parts, t) : mmb_mm2_stream_split_parts(n, t);
-  return split_ws_floats(n, split_plan_of(t, d, a_, vd, P)) * sizeof(float);
+  return split_ws_floats(n, split_plan_of(t, d, a_, vd, P, parts > 0 ? 1 : MMB_SPLIT_TEXT_X)) * sizeof(float);
 }
 
 template <int VT, int VA, int VV>
 static int launch_split(const StreamArgs& a, const SplitPlan& q, float* part, hipStream_t stream) {
   const int64_t grid = a.N * (q.Pt + 2 * q.Pf);
-  utt_split_part_kernel<VT, VA, VV><<<static_cast<unsigned>(grid), kNT, 0, stream>>>(a, q, part);
+  utt_split_part_kernel<VT, VA, VV, MMB_SPLIT_FU, MMB_SPLIT_TU><<<static_cast<unsigned>(grid), kNT, 0, stream>>>(a, q, part);
   MMB_LAUNCH_CHECK();
   const size_t lds = a.s_half ? static_cast<size_t>(2 * (a.D + a.A + a.Vd)) * sizeof(float) : 0;
   utt_split_finish_kernel<<<static_cast<unsigned>(a.N), kNT, lds, stream>>>(a, q, part);
@@ -2842,7 +2860,7 @@ extern "C" int mmb_mm2_stream_split(const int32_t* ids, const float* table, int6
     return MMB_OK;
   }
   const int P = parts > 0 ? std::min(parts, t) : mmb_mm2_stream_split_parts(n, t);
-  const SplitPlan q = split_plan_of(t, d, a_, vd, P);
+  const SplitPlan q = split_plan_of(t, d, a_, vd, P, parts > 0 ? 1 : MMB_SPLIT_TEXT_X);
   MMB_REQUIRE(ws && ws_bytes >= split_ws_floats(n, q) * sizeof(float));
   MMB_REQUIRE(n * (q.Pt + 2 * q.Pf) <= (int64_t{1} << 31) - 1);
   MMB_REQUIRE(3 * d + 2 * a_ + 2 * vd <= kSplitJ * kNT);  // the finish kernel's columns
