@@ -140,6 +140,7 @@ __device__ __forceinline__ void tri_tile(int tau, int nt, int& ti, int& tj) {
 constexpr int kGsNT = 1024;
 constexpr int64_t kGsMaxN = 4096;
 
+template <int G = 8>
 __global__ __launch_bounds__(kGsNT) void gram_small_kernel(const float* __restrict__ num,
                                                            const float* __restrict__ cnt,
                                                            int64_t N, int D, int nt, int accumulate,
@@ -151,8 +152,8 @@ __global__ __launch_bounds__(kGsNT) void gram_small_kernel(const float* __restri
   constexpr int NW = kGsNT / kWave;
   const int ca = 16 * bi + (lane & 15), cb = 16 * bj + (lane & 15), kr = lane >> 4;
   f64x4 acc = {0, 0, 0, 0};
-  // wave w: k-steps w, w + 16, ... (4 rows each), loads issued ahead in groups
-  constexpr int G = 8;
+  // wave w: k-steps w, w + 16, ... (4 rows each), loads issued ahead in
+  // groups of G k-steps (one round trip per group)
   const int64_t nks = (N + 3) / 4;
   for (int64_t s0 = wave; s0 < nks; s0 += NW * G) {
     double av[G], bv[G];
@@ -3059,7 +3060,13 @@ extern "C" int mmb_gram(const float* num, const float* cnt, int64_t n, int d, do
   const int64_t total = static_cast<int64_t>(d) * d;
   if (n <= kGsMaxN && d <= 320) {  // small splits: tile-parallel, one launch, no partials
     const int nt = static_cast<int>(ceil_div(d, 16));
-    gram_small_kernel<<<nt * (nt + 1) / 2, kGsNT, 0, stream>>>(num, cnt, n, d, nt, accumulate, g);
+    // 12 k-steps a group from 512 rows on (24 and 16 spill at 1024
+    // threads): MOSI's train split (1284 rows) in two round trips of loads
+    // instead of three
+    if (n > 512)
+      gram_small_kernel<12><<<nt * (nt + 1) / 2, kGsNT, 0, stream>>>(num, cnt, n, d, nt, accumulate, g);
+    else
+      gram_small_kernel<8><<<nt * (nt + 1) / 2, kGsNT, 0, stream>>>(num, cnt, n, d, nt, accumulate, g);
     MMB_LAUNCH_CHECK();
     return MMB_OK;
   }
