@@ -58,6 +58,25 @@ def test_product_library_reads_no_knobs():
     assert "getenv" not in undef
 
 
+def test_product_sources_carry_no_tools_code():
+    """The product kernel sources hold only what libmmb.so runs (r06): no
+    environment reads and no MMB_DIAG blocks -- the tools build's variants,
+    knobs and probes live in tools/diag/ and plug into named MMB_HOOK_*
+    points whose product defaults are compiled here."""
+    csrc = os.path.join(ROOT, "multimodal-baselines_amd", "csrc")
+    srcs = [f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp"))]
+    assert "sif_kernels.hip" in srcs and "pc_kernels.hip" in srcs
+    for f in srcs:
+        text = open(os.path.join(csrc, f)).read()
+        assert "getenv" not in text, f
+        assert "MMB_DIAG" not in text, f
+    # the tails the tools build includes exist; the product's target is empty
+    for tail in ("sif_tail.inc", "pc_tail.inc", "mm2_tail.inc", "diag_hooks.h"):
+        assert os.path.exists(os.path.join(ROOT, "tools", "diag", tail)), tail
+    code = re.sub(r"//[^\n]*", "", open(os.path.join(csrc, "mmb_no_tools.h")).read())
+    assert code.strip() == ""
+
+
 def test_library_carries_gfx950_code_objects():
     data = open(mmb_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
